@@ -1,0 +1,165 @@
+"""Synthetic assembly of the linear KdV problem (reference ``lkdv/lkdv.py``).
+
+Exact 1-D DG(1) element algebra on ``PeriodicIntervalMesh(M, 40)``
+(``lkdv/lkdv.py:17,23``), mixed space (u, v, w) laid out field-major
+(``lkdv/refd.py:34-62``; ``np.asarray(...).reshape(-1)``, ``lkdv/lkdv.py:111``).
+
+Forms (``lkdv/lkdv.py:59-61,96-105``), with ``g(u, v) = int u' v dx -
+sum_facets jump(u, n) avg(v)``:
+
+* ``F1 = (u - u0)/dt phi + g(v, phi)``
+* ``F2 = (v - (u + u0)/2) psi - g((w + w0)/2, psi)``
+* ``F3 = w chi - g(u, chi)``
+
+Sparsity follows Firedrake/PyOP2: a block that carries an interior-facet
+integral couples every dof of both facet cells (explicit zeros included), so
+u/v/w rows carry 8/10/8 entries (8.67 nnz per row on average).
+
+Everything here is exact element algebra except the initial condition, which
+is the DG(1) L2 projection of ``sin(beta x) + 1`` computed by 2-point Gauss
+quadrature per cell (Firedrake projects with a higher-order rule).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .._assembly import Triplets, embed_blocks, with_pattern
+
+
+class problem:
+    """Mirror of ``lkdv/lkdv.py:15-37``."""
+
+    def __init__(self, N, M, degree, space="DG"):
+        if degree != 1 or space != "DG":
+            raise NotImplementedError("synthetic lkdv assembly supports DG1 only")
+        self.mlength = 40
+        self.degree = degree
+        self.dim = 3
+        self.N = N
+        self.M = M
+        self.space = space
+        self.h = self.mlength / M
+
+    def exact(self, x, t):
+        alpha = 4
+        period = 2 * np.pi / self.mlength
+        beta = alpha * period
+        return np.sin(beta * (x - (1 - beta ** 2) * t)) + 1
+
+
+def dg1_operators(M, length):
+    """DG(1) mass and ``g`` on a periodic interval: returns (Mass, G, Gpat).
+
+    ``G[i, j] = g(phi_j, phi_i)``; ``Gpat`` is the cell+facet sparsity pattern
+    (zeros) that any block carrying ``g`` has.
+    """
+    h = length / M
+    n = 2 * M
+    cells = np.arange(M)
+    cdofs = np.stack([2 * cells, 2 * cells + 1], axis=1)
+    mass_e = np.broadcast_to(h / 6.0 * np.array([[2.0, 1.0], [1.0, 2.0]]), (M, 2, 2))
+    Mass = Triplets(n, n).add_blocks(cdofs, cdofs, mass_e).csr()
+
+    # volume term  int phi_j' phi_i = (+-1/h)(h/2)
+    vol = np.broadcast_to(np.array([[-0.5, 0.5], [-0.5, 0.5]]), (M, 2, 2))
+    t = Triplets(n, n).add_blocks(cdofs, cdofs, vol)
+    # facet f sits between L = f-1 (its dof 1) and R = f (its dof 0), periodic.
+    left = (cells - 1) % M
+    fdofs = np.stack([2 * left, 2 * left + 1, 2 * cells, 2 * cells + 1], axis=1)
+    # -(u_L1 - u_R0) * (v_L1 + v_R0)/2 ; local order (L0, L1, R0, R1)
+    fac = np.zeros((4, 4))
+    for test in (1, 2):
+        fac[test, 1] += -0.5
+        fac[test, 2] += +0.5
+    t.add_blocks(fdofs, fdofs, np.broadcast_to(fac, (M, 4, 4)))
+    G = t.csr()
+    Gpat = Triplets(n, n).add_blocks(fdofs, fdofs, np.zeros((M, 4, 4))).csr()
+    return Mass, G, Gpat, cdofs
+
+
+def project_dg1(f, M, length):
+    """L2 projection of ``f`` into DG(1) (2-point Gauss per cell; the DG mass
+    matrix is block-diagonal so this is exact for the quadrature)."""
+    h = length / M
+    xi = np.array([0.5 - 0.5 / np.sqrt(3.0), 0.5 + 0.5 / np.sqrt(3.0)])
+    x0 = np.arange(M)[:, None] * h
+    xq = x0 + xi[None, :] * h
+    fq = f(xq)  # (M, 2)
+    phi = np.stack([1 - xi, xi], axis=0)  # phi[i, q]
+    rhs = 0.5 * h * fq @ phi.T  # (M, 2)
+    minv = np.linalg.inv(h / 6.0 * np.array([[2.0, 1.0], [1.0, 2.0]]))
+    return (rhs @ minv.T).reshape(-1)
+
+
+def solve_mass(Mass, rhs):
+    """Mass^{-1} rhs for the block-diagonal DG(1) mass (2x2 blocks)."""
+    d = Mass.diagonal()
+    off = np.asarray(Mass[np.arange(0, Mass.shape[0], 2), np.arange(1, Mass.shape[0], 2)]).ravel()
+    a, bb = d[0::2], d[1::2]
+    det = a * bb - off * off
+    r0, r1 = rhs[0::2], rhs[1::2]
+    out = np.empty_like(rhs)
+    out[0::2] = (bb * r0 - off * r1) / det
+    out[1::2] = (a * r1 - off * r0) / det
+    return out
+
+
+def linforms(N=100, M=50, degree=1, T=1, space="DG", zinit=None):
+    prob = problem(N=N, M=M, degree=degree, space=space)
+    Mass, G, Gpat, _ = dg1_operators(M, prob.mlength)
+    nf = 2 * M
+    n = 3 * nf
+    off = [0, nf, 2 * nf]
+    if zinit is None:
+        u0 = project_dg1(lambda x: prob.exact(x, 0.0), M, prob.mlength)
+        w0 = solve_mass(Mass, G @ u0)  # gfuncproject, lkdv/lkdv.py:62-69,79
+    else:
+        zinit = np.asarray(zinit, dtype=np.float64)
+        u0, w0 = zinit[:nf].copy(), zinit[2 * nf:].copy()
+    dt = float(T) / N
+    Gf = with_pattern(G, Gpat)
+    A = embed_blocks(
+        {
+            (0, 0): Mass * (1.0 / dt),
+            (0, 1): Gf,
+            (1, 0): Mass * -0.5,
+            (1, 1): Mass,
+            (1, 2): Gf * -0.5,
+            (2, 0): Gf * -1.0,
+            (2, 2): Mass,
+        },
+        off,
+        n,
+    )
+    b = np.zeros(n)
+    b[:nf] = Mass @ u0 / dt
+    b[nf:2 * nf] = 0.5 * (Mass @ u0) + 0.5 * (G @ w0)
+    Mfull = embed_blocks({(0, 0): Mass}, off, n)
+    Lfull = embed_blocks({(2, 2): Mass}, off, n)
+    omega = np.zeros(n)
+    omega[:nf] = np.asarray(Mass.sum(axis=0)).ravel()
+    z_vec = np.zeros(n)
+    z_vec[:nf] = u0
+    z_vec[2 * nf:] = w0
+    out = {
+        "A": A,
+        "b": b,
+        "z0": z_vec,
+        "M": Mfull,
+        "L": Lfull,
+        "omega": omega,
+        "m0": float(omega[:nf] @ u0),
+        "mo0": float(0.5 * u0 @ Mass @ u0),
+        "e0": float(0.5 * w0 @ Mass @ w0 - 0.5 * u0 @ Mass @ u0),
+        "T": T,
+    }
+    return out, prob
+
+
+def compute_invariants(prob, dic, uvec):
+    """``lkdv/lkdv.py:154-166`` on the assembled operators."""
+    return {
+        "mass": float(dic["omega"] @ uvec),
+        "momentum": float(0.5 * uvec @ dic["M"] @ uvec),
+        "energy": float(0.5 * uvec @ dic["L"] @ uvec - 0.5 * uvec @ dic["M"] @ uvec),
+    }

@@ -1,0 +1,259 @@
+"""Generate the golden vectors in ``tests/golden/*.npz`` from the REFERENCE.
+
+Runs the reference ``/root/reference/solvers.py`` (and the reference
+``heat``/``lkdv``/``swe``/``lkdvRK`` ``LinearSolver.py`` wrappers) in the build
+container — the only place the reference exists — on this package's synthetic
+operators, and stores inputs + outputs as compressed ``.npz`` fixtures.  The
+GPU box never sees the reference: tests read only these fixtures.
+
+Import notes:
+* ``solvers.py`` does ``from firedrake import *`` and uses only ``warning``;
+  a stub module providing ``warning`` (recorded) is placed in ``sys.modules``.
+* ``lkdvRK/LinearSolver.py`` needs ``lkdvRK.z1calc``/``dz1calc``; the
+  reference ``lkdvRK.py`` needs Firedrake + Irksome, so a stub ``lkdvRK`` module
+  carrying this package's restatement of those two functions
+  (``lkdvRK/lkdvRK.py:162-189``) is injected instead.
+* ``scipy.optimize`` is wrapped (in the reference module's namespace only) to
+  log every SLSQP call: (p, number of constraints, exit message, solution).
+* ``PYTHONDONTWRITEBYTECODE`` keeps ``/root/reference`` free of ``__pycache__``.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import types
+import warnings
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import scipy.optimize as _spo  # noqa: E402
+import scipy.sparse as sps  # noqa: E402
+import scipy.sparse.linalg as spla  # noqa: E402
+
+from structurepreservingiterativesolvers_amd.heat import assembly as heat_asm  # noqa: E402
+from structurepreservingiterativesolvers_amd.lkdv import assembly as lkdv_asm  # noqa: E402
+from structurepreservingiterativesolvers_amd.lkdvRK import assembly as rk_asm  # noqa: E402
+from structurepreservingiterativesolvers_amd.swe import assembly as swe_asm  # noqa: E402
+
+FD_WARNINGS: list[str] = []
+CALLS: list[tuple] = []
+
+
+def _load_reference():
+    fd = types.ModuleType("firedrake")
+    fd.warning = lambda msg, *a: FD_WARNINGS.append(str(msg))
+    fd.__all__ = ["warning"]
+    sys.modules["firedrake"] = fd
+    spec = importlib.util.spec_from_file_location("solvers", os.path.join(REF, "solvers.py"))
+    solvers = importlib.util.module_from_spec(spec)
+    sys.modules["solvers"] = solvers
+    spec.loader.exec_module(solvers)
+
+    def logged_minimize(fun, x0, *args, **kw):
+        out = _spo.minimize(fun, x0, *args, **kw)
+        CALLS.append((len(x0), len(kw.get("constraints", [])), str(out.message), np.array(out.x)))
+        return out
+
+    solvers.spo = types.SimpleNamespace(minimize=logged_minimize)
+    rk = types.ModuleType("lkdvRK")
+    rk.z1calc = rk_asm.z1calc
+    rk.dz1calc = rk_asm.dz1calc
+    sys.modules["lkdvRK"] = rk
+    wrappers = {}
+    for name in ("heat", "lkdv", "swe", "lkdvRK"):
+        spec = importlib.util.spec_from_file_location(f"ref_{name}_ls", os.path.join(REF, name, "LinearSolver.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        wrappers[name] = mod
+    return solvers, wrappers
+
+
+def _csr_fields(prefix, m):
+    m = sps.csr_matrix(m)
+    return {
+        f"{prefix}_data": m.data,
+        f"{prefix}_indices": m.indices.astype(np.int32),
+        f"{prefix}_indptr": m.indptr.astype(np.int32),
+        f"{prefix}_shape": np.array(m.shape),
+    }
+
+
+def _dic_fields(dic):
+    out = {}
+    for key, val in dic.items():
+        if sps.issparse(val):
+            out.update(_csr_fields(f"dic_{key}", val))
+        elif isinstance(val, (int, float, np.floating, np.integer)):
+            out[f"dic_{key}"] = np.array(float(val))
+        elif isinstance(val, np.ndarray):
+            out[f"dic_{key}"] = val
+    return out
+
+
+def _run(case, fn):
+    FD_WARNINGS.clear()
+    CALLS.clear()
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        x, d = fn()
+    return x, d, list(FD_WARNINGS), [str(w.message) for w in caught], list(CALLS)
+
+
+def _save(name, meta, inputs, x, d, fdw, pyw, calls):
+    xs = np.asarray(d["x"])
+    k = max([c[0] for c in calls], default=1)
+    ylog = np.full((len(calls), k), np.nan)
+    for i, c in enumerate(calls):
+        ylog[i, : c[0]] = c[3]
+    out = dict(inputs)
+    out.update(
+        x_all=xs,
+        x_final=np.asarray(x),
+        res=np.asarray(d["res"]),
+        steps=np.array(d.get("steps", -1)),
+        name=np.array(d["name"]),
+        calls_p=np.array([c[0] for c in calls], dtype=np.int32),
+        calls_ncons=np.array([c[1] for c in calls], dtype=np.int32),
+        calls_msg=np.array([c[2] for c in calls]),
+        calls_y=ylog,
+        fd_warnings=np.array(fdw, dtype=object).astype(str) if fdw else np.array([], dtype="<U1"),
+        py_warnings=np.array(pyw, dtype=object).astype(str) if pyw else np.array([], dtype="<U1"),
+        meta=np.array(repr(meta)),
+    )
+    if d.get("timings") is not None:
+        out["timing_keys"] = np.array(sorted(d["timings"].keys()))
+        out["timing_constrained_steps"] = np.array(d["timings"]["constrained_steps"])
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"{name:28s} N={len(inputs['b']):6d} steps={d.get('steps', '-')!s:>3} res[-1]={(d['res'][-1] if len(d['res']) else float('nan')):.3e} "
+          f"calls={len(calls)} fdw={len(fdw)} pyw={len(pyw)} {os.path.getsize(path) / 1024:.0f} KB")
+
+
+def main():
+    solvers, W = _load_reference()
+    cases = []
+
+    # ---- heat (config C1: N=1024, 50 iterations, 2 constraints) ----------------
+    dh, _ = heat_asm.linforms(M=31)
+    x0 = np.zeros_like(dh["b"])
+    cases.append(("heat_c1_cgmres", dict(problem="heat", M=31, solver="cgmres", k=50, tol=1e-19), dh, x0,
+                  lambda: W["heat"].cgmresWrapper(dh, x0=x0, k=50, tol=1e-19)))
+    cases.append(("heat_c1_gmres", dict(problem="heat", M=31, solver="gmres", k=50, tol=1e-50), dh, x0,
+                  lambda: W["heat"].gmresWrapper(dh, x0=x0, k=50)))
+    dh15, _ = heat_asm.linforms(M=15)
+    x015 = np.zeros_like(dh15["b"])
+    cases.append(("heat_m15_cgmres_p", dict(problem="heat", M=15, solver="cgmres_p", k=20, tol=1e-50), dh15, x015,
+                  lambda: W["heat"].cgmresWrapper(dh15, x0=x015, k=20, tol=1e-50)))
+    cases.append(("heat_m15_cgmres_tol1e-3", dict(problem="heat", M=15, solver="cgmres", k=40, tol=1e-3), dh15,
+                  x015, lambda: W["heat"].cgmresWrapper(dh15, x0=x015, k=40, tol=1e-3)))
+
+    # ---- lkdv (3 constraints) -----------------------------------------------------
+    dl, _ = lkdv_asm.linforms(M=50)
+    xl = np.zeros_like(dl["b"])
+    cases.append(("lkdv_m50_cgmres_tol1e-6", dict(problem="lkdv", M=50, solver="cgmres", k=30, tol=1e-6), dl, xl,
+                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=30, tol=1e-6)))
+    cases.append(("lkdv_m50_cgmres_tol1e-19", dict(problem="lkdv", M=50, solver="cgmres", k=30, tol=1e-19), dl,
+                  xl, lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=30, tol=1e-19)))
+    cases.append(("lkdv_m50_cgmres_p", dict(problem="lkdv", M=50, solver="cgmres_p", k=12, tol=1e-50), dl, xl,
+                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=12, tol=1e-50)))
+    cases.append(("lkdv_m50_gmres", dict(problem="lkdv", M=50, solver="gmres", k=30, tol=1e-10), dl, xl,
+                  lambda: W["lkdv"].gmresWrapper(dl, x0=xl, k=30, tol=1e-10)))
+    # overconstrained terminal step: p = 2 < 3 constraints -> failure/fallback path
+    cases.append(("lkdv_m50_overconstrained", dict(problem="lkdv", M=50, solver="cgmres", k=2, tol=1e-6), dl, xl,
+                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=2, tol=1e-6)))
+    # left-behind rare path: contol so large that constraints are enforced from j = 0
+    cases.append(("lkdv_m50_contol_big", dict(problem="lkdv", M=50, solver="cgmres", k=8, tol=1e-6,
+                                              contol=1e12), dl, xl,
+                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=8, tol=1e-6, contol=1e12)))
+    ilu = spla.spilu(dl["A"].tocsc(), drop_tol=1e-2, fill_factor=10)
+    cases.append(("lkdv_m50_gmres_spilu", dict(problem="lkdv", M=50, solver="gmres", k=10, tol=1e-12, pre="spilu"),
+                  dl, xl, lambda: solvers.gmres(dl["A"], dl["b"], xl, 10, tol=1e-12, pre=ilu)))
+
+    # ---- swe (2 constraints; + synthetic third) -----------------------------------
+    ds, _ = swe_asm.linforms(M=8)
+    xs0 = np.zeros_like(ds["b"])
+    cases.append(("swe_m8_cgmres_tol1e-19", dict(problem="swe", M=8, solver="cgmres", k=30, tol=1e-19), ds, xs0,
+                  lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=30, tol=1e-19)))
+    cases.append(("swe_m8_cgmres_tol1e-7", dict(problem="swe", M=8, solver="cgmres", k=30, tol=1e-7), ds, xs0,
+                  lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=30, tol=1e-7)))
+    cases.append(("swe_m8_gmres", dict(problem="swe", M=8, solver="gmres", k=30, tol=1e-50), ds, xs0,
+                  lambda: W["swe"].gmresWrapper(ds, x0=xs0, k=30)))
+    ds6, _ = swe_asm.linforms(M=6)
+    x6 = np.zeros_like(ds6["b"])
+    cases.append(("swe_m6_cgmres_p", dict(problem="swe", M=6, solver="cgmres_p", k=15, tol=1e-50), ds6, x6,
+                  lambda: W["swe"].cgmresWrapper(ds6, x0=x6, k=15, tol=1e-50)))
+    cases.append(("swe_m8_cgmres_timing", dict(problem="swe", M=8, solver="cgmres", k=12, tol=1e-7, timing=True),
+                  ds, xs0, lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=12, tol=1e-7, timing=True)))
+    jac = sps.diags(1.0 / ds["A"].diagonal(), format="csr")
+    cases.append(("swe_m8_cgmres_jacobi", dict(problem="swe", M=8, solver="cgmres", k=20, tol=1e-19, pre="jacobi"),
+                  ds, xs0, lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=20, tol=1e-19, pre=jac)))
+    rng = np.random.default_rng(5)
+    xr = rng.normal(size=ds["b"].shape)
+    cases.append(("swe_m8_cgmres_x0", dict(problem="swe", M=8, solver="cgmres", k=20, tol=1e-19, x0="random5"),
+                  ds, xr, lambda: W["swe"].cgmresWrapper(ds, x0=xr, k=20, tol=1e-19)))
+    D3, c3 = swe_asm.extra_constraint(len(ds["b"]), ds["z0"], seed=2)
+
+    class _Mass:
+        def __init__(self):
+            self.M, self.v, self.c = 0 * ds["A"], ds["omega"], -ds["m0"]
+
+    class _Energy:
+        def __init__(self):
+            self.M, self.v, self.c = ds["L"], np.zeros_like(xs0), -ds["e0"]
+
+    class _Extra:
+        def __init__(self):
+            self.M, self.v, self.c = D3, np.zeros_like(xs0), c3
+
+    ds3 = dict(ds)
+    ds3["D3"] = D3
+    ds3["c3"] = c3
+    cases.append(("swe_m8_cgmres_3cons", dict(problem="swe3", M=8, solver="cgmres", k=30, tol=1e-19), ds3, xs0,
+                  lambda: solvers.cgmres(ds["A"], ds["b"], xs0, 30, tol=1e-19,
+                                         conlist=[_Mass(), _Energy(), _Extra()])))
+    cases.append(("swe_m8_cgmres_nocons", dict(problem="swe", M=8, solver="cgmres", k=15, tol=1e-19, cons="none"),
+                  ds, xs0, lambda: solvers.cgmres(ds["A"], ds["b"], xs0, 15, tol=1e-19, conlist=[])))
+
+    # ---- lkdvRK (dict-form constraints through the reference wrapper) --------------
+    dr, pr = rk_asm.linforms(M=20, tstages=2)
+    xr0 = np.zeros_like(dr["b"])
+    drk = dict(dr)
+    drk["dt"] = pr.dt
+    drk["butcher_b"] = pr.butcher_tableau.b
+    cases.append(("lkdvrk_m20_s2_cgmres", dict(problem="lkdvRK", M=20, s=2, solver="cgmres", k=30, tol=1e-6),
+                  drk, xr0, lambda: W["lkdvRK"].cgmresWrapper(dr, x0=xr0, k=30, prob=pr, tol=1e-6)))
+    cases.append(("lkdvrk_m20_s2_cgmres_tight", dict(problem="lkdvRK", M=20, s=2, solver="cgmres", k=25,
+                                                     tol=1e-19), drk, xr0,
+                  lambda: W["lkdvRK"].cgmresWrapper(dr, x0=xr0, k=25, prob=pr, tol=1e-19)))
+
+    # ---- edge: exact breakdown at j = 0 (returns r0 as the "solution") -------------
+    n = 64
+    A2 = sps.csr_matrix(2.0 * sps.identity(n))
+    A2 = sps.csr_matrix((A2.data, A2.indices.astype(np.int32), A2.indptr.astype(np.int32)), shape=A2.shape)
+    e0v = np.zeros(n)
+    e0v[0] = 1.0
+    dbk = {"A": A2, "b": e0v}
+    xb = np.zeros(n)
+    cases.append(("edge_breakdown_cgmres", dict(problem="edge", solver="cgmres", k=5, tol=1e-8, cons="none"), dbk,
+                  xb, lambda: solvers.cgmres(A2, e0v, xb, 5, tol=1e-8, conlist=[])))
+    cases.append(("edge_breakdown_gmres", dict(problem="edge", solver="gmres", k=5, tol=1e-50), dbk, xb,
+                  lambda: solvers.gmres(A2, e0v, xb, 5)))
+
+    for name, meta, dic, x0c, fn in cases:
+        inputs = _dic_fields(dic)
+        inputs["b"] = np.asarray(dic["b"])
+        inputs["x0"] = x0c
+        x, d, fdw, pyw, calls = _run(name, fn)
+        _save(name, meta, inputs, x, d, fdw, pyw, calls)
+
+
+if __name__ == "__main__":
+    main()
