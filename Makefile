@@ -1,0 +1,37 @@
+# libspis.so — MI355X (gfx950) build of the CGMRES/FGMRES inner loop.  hipcc cross-compiles
+# here (no GPU needed); the .so travels to the GPU box with the repo snapshot.
+ROCM     ?= /opt/rocm
+HIPCC    ?= $(ROCM)/bin/hipcc
+ARCH     ?= gfx950
+PKG      := structurepreservingiterativesolvers_amd
+SRC      := $(PKG)/csrc
+LIB      := $(PKG)/libspis.so
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I include -I $(SRC)
+HIPFLAGS := --offload-arch=$(ARCH) -munsafe-fp-atomics
+OBJS     := build/kernels.o build/spis.o build/lsq.o
+
+all: $(LIB) $(PKG)/liblsq_host.so
+
+build/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -c $< -o $@
+
+build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/lsq.h include/spis.h
+	@mkdir -p build
+	$(HIPCC) $(CXXFLAGS) -x hip --offload-arch=$(ARCH) -c $< -o $@
+
+build/lsq.o: $(SRC)/lsq.cpp $(SRC)/lsq.h include/spis.h
+	@mkdir -p build
+	g++ $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+# host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
+$(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp
+	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp
+
+clean:
+	rm -rf build $(LIB) $(PKG)/liblsq_host.so
+
+.PHONY: all clean

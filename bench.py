@@ -1,0 +1,201 @@
+"""Benchmark: CGMRES iterations/sec + Arnoldi-SpMV achieved HBM GB/s (BASELINE.json).
+
+Workload (BASELINE.json configs[2]): swe-shaped RT2 x DG0
+CSR, N = 12 M^2 = 1,002,252 DoF per GPU (M = 289), 12.5 nnz/row, fp64;
+``swe.LinearSolver.cgmresWrapper`` semantics (mass + energy constraints),
+k = 30, tol = 1e-19 so every solve runs all 30 iterations and the last one is
+the constrained projection.  One "step" = one CGMRES(30) solve; inputs (A, b,
+x0, constraint operators) are resident in HBM before the timed region.
+
+Multi-GPU (``--gpus N`` under torch.distributed.run): one global solve of
+N x 1,002,252 DoF row-partitioned over the N ranks (weak scaling), RCCL
+all-reduce for every dot/norm, halo exchange before every SpMV.  ``value`` =
+iterations x N / time (Mdof-normalised iterations per second of the whole
+job), max time over ranks.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "CGMRES iterations/sec + SpMV achieved HBM GB/s, N=10^6 DoF CSR fp64"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def spmv_bytes(n_rows, nnz):
+    """Algorithmic bytes of one CSR SpMV: fp64 val + int32 col per nnz,
+    int32 rowptr, x read once, y written once."""
+    return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
+
+
+def mgs_bytes(n, p):
+    """Algorithmic bytes of one MGS chain over p basis vectors + normalise (fused form:
+    per step read y, q_i, q_{i+1}, write y; normalise reads y, writes q)."""
+    return 32 * n * p + 16 * n
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the Arnoldi SpMV from the committed PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "spmv_traffic.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def cpu_baseline(dic, conlist, k, tol, budget_s):
+    """The oracle (CPU restatement of the reference solvers.cgmres, NumPy/SciPy +
+    SLSQP exactly as the reference) on the same workload, bounded sample."""
+    import oracle
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        blas_threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        blas_threads = 1
+    x0 = np.zeros_like(dic["b"])
+    iters = 0
+    solves = 0
+    t0 = time.perf_counter()
+    while True:
+        _, d = oracle.cgmres(dic["A"], dic["b"], x0, k, tol=tol, conlist=conlist)
+        iters += d["steps"]
+        solves += 1
+        if time.perf_counter() - t0 > budget_s or solves >= 3:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": iters / dt,
+        "unit": "iterations/s",
+        "cores": int(blas_threads),
+        "kind": "port",
+        "sample": f"{solves} full CGMRES({k}) solve(s) of the same N={len(x0)} system ({iters} iterations, "
+                  f"{dt:.1f} s); SciPy csr_matvec single-threaded, OpenBLAS {blas_threads} threads",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--M", type=int, default=289, help="swe mesh per GPU (N = 12 M^2)")
+    ap.add_argument("--k", type=int, default=30)
+    ap.add_argument("--tol", type=float, default=1e-19)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 or world > 1:
+        from structurepreservingiterativesolvers_amd import distributed
+
+        return distributed.bench_main(args, METRIC)
+
+    from structurepreservingiterativesolvers_amd import _lib, solvers
+    from structurepreservingiterativesolvers_amd.device import DeviceVector, device_matrix, get_context
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly
+
+    dic, _ = assembly.linforms(M=args.M)
+    A = dic["A"]
+    n = A.shape[0]
+    ctx = get_context(0)
+    device_matrix(A, ctx=ctx)
+    bd = DeviceVector.from_host(dic["b"], ctx=ctx)
+    x0 = np.zeros(n)
+    x0d = DeviceVector.from_host(x0, ctx=ctx)
+    conlist = swe_ls.constraints(dic, x0)
+
+    def solve():
+        return solvers.cgmres(A, bd, x0d, args.k, tol=args.tol, conlist=conlist)
+
+    for _ in range(args.warmup):
+        solve()
+    ctx.synchronize()
+    L = ctx.L
+    import ctypes as C
+
+    _lib.check(L.spis_profile_enable(ctx.handle, 1), "spis_profile_enable")
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        _, d = solve()
+        iters += d["steps"]
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    ms = (C.c_double * 4)()
+    cnt = (C.c_int64 * 4)()
+    _lib.check(L.spis_profile_read(ctx.handle, ms, cnt), "spis_profile_read")
+    _lib.check(L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
+    elapsed = t1 - t0
+
+    S = spmv_bytes(n, A.nnz)
+    spmv_ms = ms[_lib.PROF_SPMV] / max(cnt[_lib.PROF_SPMV], 1)
+    spmv_gbs = S / (spmv_ms * 1e-3) / 1e9
+    p_mean = (args.k + 1) / 2.0
+    mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
+    mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9
+    res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
+    gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
+    traffic = load_traffic()
+    out = {
+        "metric": METRIC,
+        "value": iters / elapsed,
+        "unit": "iterations/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"swe-shaped RT2xDG0 CSR (config C3), N={n:,} DoF, nnz={A.nnz:,}, "
+                        f"CGMRES(k={args.k}, tol={args.tol:g}) with mass+energy constraints per step",
+            "global_dof": n,
+            "k": args.k,
+            "parallelism": "single GPU",
+        },
+        "roofline": {
+            "kernel": "spmv_rowblock_kernel<kEpiDot> (Arnoldi SpMV, solvers.py:191)",
+            "bound": "hbm",
+            "achieved": spmv_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": spmv_gbs / HBM_PEAK_GBS,
+            "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
+            "algorithmic_bytes_per_launch": S,
+            "avg_launch_us": 1e3 * spmv_ms,
+            "launches": int(cnt[_lib.PROF_SPMV]),
+        },
+        "kernels": {
+            "spmv_arnoldi_us": 1e3 * spmv_ms,
+            "spmv_residual_us": 1e3 * res_ms,
+            "mgs_chain_us_mean": 1e3 * mgs_ms,
+            "mgs_chain_GBs": mgs_gbs,
+            "gemv_us_mean": 1e3 * gemv_ms,
+            "iteration_us": 1e6 * elapsed / max(iters, 1),
+        },
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(dic, conlist, args.k, args.tol, args.cpu_budget)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+/*
+ * spis.h — C-ABI of libspis.so, the MI355X-native CGMRES/FGMRES inner loop.
+ *
+ * This is the drop-in boundary for the hot path of the reference
+ * (JamesJackaman/StructurePreservingIterativeSolvers, /root/reference):
+ *
+ *   spis_solve (method SPIS_CGMRES)   replaces solvers.cgmres    solvers.py:131-323
+ *   spis_solve (method SPIS_GMRES)    replaces solvers.gmres     solvers.py:58-127
+ *   spis_solve (method SPIS_CGMRES_P) replaces solvers.cgmres_p  solvers.py:328-445
+ *   spis_constraint_terms             replaces constraint_container.__init__
+ *                                     (class form)               solvers.py:21-40
+ *   spis_csr_upload                   replaces the CSR the wrappers hand over
+ *                                     (csr_matrix of getValuesCSR, e.g. swe/swe.py:90-91)
+ *   spis_spmv / spis_residual_norm    A @ z (solvers.py:191), ||A x - b|| (:290)
+ *   spis_dot / spis_nrm2 / spis_axpy  np.dot / norm / y - h q (:194-198)
+ *   spis_gemv                         Z @ yk + x0 (solvers.py:287)
+ *
+ * Conventions:
+ *   - every export returns int status (SPIS_OK = 0) and never throws;
+ *     spis_last_error() returns a thread-local message for the last failure;
+ *   - "_dev" pointers are device (HBM) pointers on the context's device,
+ *     "_host" pointers are host memory; sizes are element counts;
+ *   - all arithmetic is fp64; CSR indices are int32 (PETSc AIJ via SciPy);
+ *   - every call is ordered on the context's HIP stream and returns after the
+ *     results it reports are complete (host outputs are valid on return);
+ *   - handles are not re-entrant: one host thread per context.
+ *
+ * Multi-GPU: one process per GPU.  Each process uploads its local rows with
+ * columns renumbered [0, n_local) owned, [n_local, n_local + n_ghost) ghosts,
+ * plus a halo plan (spis_halo_desc).  After spis_comm_init, dots/norms are
+ * all-reduced with RCCL over xGMI and ghosts are exchanged with grouped
+ * ncclSend/ncclRecv before every SpMV.
+ */
+#ifndef SPIS_H
+#define SPIS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPIS_ABI_VERSION 1
+
+enum spis_status {
+  SPIS_OK = 0,
+  SPIS_ERR_ARG = 1,      /* bad argument (shape, null pointer, range)        */
+  SPIS_ERR_HIP = 2,      /* HIP runtime error                                */
+  SPIS_ERR_RCCL = 3,     /* RCCL error                                       */
+  SPIS_ERR_ALLOC = 4,    /* device/host allocation failed                    */
+  SPIS_ERR_CALLBACK = 5, /* a host callback (preconditioner/constraint) failed */
+  SPIS_ERR_STATE = 6     /* handle used in the wrong state                   */
+};
+
+enum spis_method { SPIS_CGMRES = 0, SPIS_GMRES = 1, SPIS_CGMRES_P = 2 };
+
+/* what the least-squares step of iteration j did (solvers.py:230-278) */
+enum spis_branch {
+  SPIS_BRANCH_UNCON = 0,    /* unconstrained LS (solvers.py:230-235)          */
+  SPIS_BRANCH_CON = 1,      /* constrained LS kept (:236-270)                 */
+  SPIS_BRANCH_FALLBACK = 2  /* constrained LS failed -> unconstrained (:271-278) */
+};
+
+/* per-iteration event bits (the reference's warnings, replayed by the host) */
+enum spis_event {
+  SPIS_EV_BREAKDOWN = 1 << 0,    /* h[j+1,j] == 0 -> warn + break (:197-202)      */
+  SPIS_EV_LS_MESSAGE = 1 << 1,   /* LS exit message not accepted (:280-284); code in msg[] */
+  SPIS_EV_NAN = 1 << 2,          /* NaN in constrained solution (:259-260)        */
+  SPIS_EV_VIOLATION = 1 << 3,    /* constraint_checker > ctol (:267-269)          */
+  SPIS_EV_FALLBACK = 1 << 4      /* fallback warning emitted (:272-273 / :419)    */
+};
+
+/* exit-message codes (numbering of scipy SLSQP exit modes, which the
+ * reference compares against in solvers.py:280-282) */
+enum spis_ls_message {
+  SPIS_MSG_SUCCESS = 0,          /* "Optimization terminated successfully"           */
+  SPIS_MSG_MORE_EQ = 2,          /* "More equality constraints than independent variables" */
+  SPIS_MSG_SINGULAR_C = 6,       /* "Singular matrix C in LSQ subproblem"            */
+  SPIS_MSG_ITER_LIMIT = 9        /* "Iteration limit reached"                        */
+};
+
+typedef struct spis_context spis_context;
+typedef struct spis_matrix spis_matrix;
+typedef struct spis_workspace spis_workspace;
+
+/* ---- library / context ---------------------------------------------------- */
+int spis_abi_version(void);
+const char* spis_last_error(void);
+int spis_device_count(int32_t* count);
+int spis_context_create(int32_t device, spis_context** out);
+int spis_context_destroy(spis_context* ctx);
+int spis_context_synchronize(spis_context* ctx);
+/* HIP stream (hipStream_t) the context orders its work on */
+int spis_context_stream(spis_context* ctx, void** stream_out);
+
+/* ---- live kernel timing ------------------------------------------------------
+ * When enabled, spis_solve records HIP events on the context stream around the
+ * Arnoldi SpMV, the MGS chain (+ normalise), the GEMV and the true-residual
+ * SpMV of every iteration; totals (ms) and launch counts accumulate until the
+ * next spis_profile_enable.  Used by bench.py for the roofline numbers. */
+enum spis_prof_kind {
+  SPIS_PROF_SPMV = 0,      /* Arnoldi SpMV, solvers.py:191            */
+  SPIS_PROF_MGS = 1,       /* MGS chain + normalise, :193-198          */
+  SPIS_PROF_GEMV = 2,      /* Z y + x0, :287                           */
+  SPIS_PROF_SPMV_RES = 3,  /* true-residual SpMV + norm, :290          */
+  SPIS_PROF_KINDS = 4
+};
+int spis_profile_enable(spis_context* ctx, int32_t on);
+int spis_profile_read(spis_context* ctx, double ms_out[4], int64_t count_out[4]);
+
+/* ---- multi-GPU (RCCL over xGMI) ----------------------------------------------
+ * rank 0 creates the id (128 bytes), the host side broadcasts it (e.g. over
+ * torch.distributed), every rank calls spis_comm_init. */
+int spis_comm_unique_id(uint8_t id_out[128]);
+int spis_comm_init(spis_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int spis_comm_allreduce_sum(spis_context* ctx, double* buf_dev, int64_t count);
+int spis_comm_barrier(spis_context* ctx);
+
+/* ---- matrices ----------------------------------------------------------------
+ * Local CSR rows (n_rows x (n_rows + n_ghost)), host arrays, copied to HBM.
+ * The matrix is partitioned into row blocks of <= 2048 merge items (rows +
+ * nnz) here (SpMV schedule). */
+typedef struct spis_halo_desc {
+  int32_t n_ghost;            /* ghost columns appended after the owned ones     */
+  int32_t n_neighbors;        /* peer ranks exchanged with                       */
+  const int32_t* neighbors;   /* [n_neighbors] peer ranks                        */
+  const int32_t* send_counts; /* [n_neighbors] owned entries sent to each peer   */
+  const int32_t* send_idx;    /* [sum send_counts] local row ids, grouped by peer */
+  const int32_t* recv_counts; /* [n_neighbors] ghosts received from each peer;
+                                 ghosts of one peer are contiguous, peers in order */
+} spis_halo_desc;
+
+int spis_csr_upload(spis_context* ctx, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                    const int32_t* indptr_host, const int32_t* indices_host,
+                    const double* data_host, const spis_halo_desc* halo /* NULL = 1 GPU */,
+                    spis_matrix** out);
+int spis_matrix_destroy(spis_matrix* A);
+/* info[0]=n_rows info[1]=n_cols info[2]=nnz info[3]=row blocks info[4]=long-row blocks
+ * info[5]=n_ghost info[6]=all values zero (1/0) */
+int spis_matrix_info(spis_matrix* A, int64_t info[8]);
+
+/* ---- vectors / BLAS-1 primitives (device pointers, n = local length) -------- */
+int spis_malloc(spis_context* ctx, int64_t bytes, void** dev_out);
+int spis_free(spis_context* ctx, void* dev);
+int spis_memcpy_h2d(spis_context* ctx, void* dst_dev, const void* src_host, int64_t bytes);
+int spis_memcpy_d2h(spis_context* ctx, void* dst_host, const void* src_dev, int64_t bytes);
+
+/* y = A x (x must hold n_rows + n_ghost entries; ghosts are exchanged first) */
+int spis_spmv(spis_context* ctx, spis_matrix* A, double* x_dev, double* y_dev);
+/* out = ||A x - b||_2 (global) */
+int spis_residual_norm(spis_context* ctx, spis_matrix* A, double* x_dev, const double* b_dev,
+                       double* out_host);
+int spis_dot(spis_context* ctx, int64_t n, const double* x_dev, const double* y_dev, double* out_host);
+int spis_nrm2(spis_context* ctx, int64_t n, const double* x_dev, double* out_host);
+/* y = y - h x  (numpy's y - h*x: product rounded, then subtracted) */
+int spis_axpy(spis_context* ctx, int64_t n, double h, const double* x_dev, double* y_dev);
+/* x = Z[:, :p] y + x0, Z row-major (p, pitch) */
+int spis_gemv(spis_context* ctx, int64_t n, int32_t p, const double* Z_dev, int64_t pitch,
+              const double* y_host, const double* x0_dev, double* x_dev);
+/* Gram: G (nu x nv, row-major, host) = U^T V for lists of device vectors */
+int spis_gram(spis_context* ctx, int64_t n, int32_t nu, const double* const* U_dev_host_list,
+              int32_t nv, const double* const* V_dev_host_list, double* G_host);
+
+/* ---- constraints (class form: 1/2 X'MX + v.X + c with X = x0 + Z y) --------- */
+typedef struct spis_constraint_desc {
+  spis_matrix* M;       /* NULL or all-zero matrix: skipped (mass constraint 0*A) */
+  const double* v_dev;  /* [n] or NULL (= 0) */
+  double c;
+} spis_constraint_desc;
+
+/* term0 (scalar), term1 (p), term2 (p x p row-major) of solvers.py:33-36 for the
+ * basis Z[:, :p] (row-major (p, pitch)) */
+int spis_constraint_terms(spis_context* ctx, const spis_constraint_desc* con, int64_t n, int32_t p,
+                          const double* Z_dev, int64_t pitch, const double* x0_dev,
+                          double* term0_host, double* term1_host, double* term2_host);
+
+/* ---- the solver ------------------------------------------------------------ */
+/* host preconditioner callback (objects with .solve, solvers.py:152-154):
+ * z = P^{-1} q on host arrays of the local length; return 0 on success */
+typedef int (*spis_precond_fn)(void* user, const double* q_host, double* z_host, int64_t n);
+/* host constrained-LS callback for constraints the library cannot reduce
+ * (dict form: solvers.py:27-28,38-40,46,52).  H is (p+1) x p column-major,
+ * y0 the warm start (solvers.py:225-227).  The callback writes y_out and
+ * *branch_out (SPIS_BRANCH_CON / SPIS_BRANCH_FALLBACK) and *events_out. */
+typedef int (*spis_conls_fn)(void* user, spis_workspace* ws, int32_t j, int32_t p, const double* H,
+                             double beta, const double* y0, double* y_out, int32_t* branch_out,
+                             int32_t* events_out, int32_t* msg_out);
+
+typedef struct spis_solve_opts {
+  int32_t method;            /* spis_method                                      */
+  int32_t k;                 /* max iterations (Krylov dimension)                */
+  double tol;                /* solvers.py:132 (cgmres), :58 (gmres)             */
+  double contol;             /* solvers.py:133                                   */
+  int32_t timing;            /* solvers.py:136: skip NaN/checker, record stamps  */
+  int32_t n_constraints;
+  const spis_constraint_desc* constraints;
+  spis_matrix* pre_matrix;   /* device preconditioner (pre @ vec, :156-161)       */
+  spis_precond_fn pre_fn;    /* host preconditioner (pre.solve, :152-154)         */
+  void* pre_user;
+  spis_conls_fn conls_fn;    /* dict-form constraints                              */
+  void* conls_user;
+} spis_solve_opts;
+
+typedef struct spis_solve_out {
+  int32_t steps;     /* iterations run (solvers.py:189)                          */
+  int32_t n_res;     /* residual norms written: res[0] = ||r0||, then one per step */
+  double* res_host;          /* capacity k+1                                    */
+  double* y_host;            /* capacity k*k: y of iteration j at y_host + j*k   */
+  int32_t* branch_host;      /* capacity k                                      */
+  int32_t* events_host;      /* capacity k                                      */
+  int32_t* msg_host;         /* capacity k: spis_ls_message of iteration j       */
+  double* stamps_host;       /* capacity 4k+2 or NULL: iter start/end, constraint
+                                build start/end (seconds), then run start/end   */
+  double* x_final_dev;       /* [n] receives x[-1] (device), or NULL             */
+} spis_solve_out;
+
+/* Runs the solver; *ws_out receives a workspace holding the Krylov basis so
+ * that the iterate list x[i] (solvers.py:169,287) can be materialised lazily
+ * with spis_workspace_iterate.  Release it with spis_workspace_release. */
+int spis_solve(spis_context* ctx, spis_matrix* A, const double* b_dev, const double* x0_dev,
+               const spis_solve_opts* opts, spis_solve_out* out, spis_workspace** ws_out);
+/* x[i]: i = 0 -> r0 = b - A x0 ; i >= 1 -> Z[:, :i] y_i + x0 */
+int spis_workspace_iterate(spis_workspace* ws, int32_t i, double* x_dev_out);
+/* Z[:, :p] to host, row-major (p, n) */
+int spis_workspace_basis(spis_workspace* ws, int32_t p, double* Z_host);
+int spis_workspace_release(spis_workspace* ws);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPIS_H */

@@ -1,0 +1,67 @@
+// kernels.h — device kernels of the CGMRES/FGMRES inner loop (gfx950, fp64).
+// Internal header of libspis.so; the public boundary is include/spis.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace spis {
+
+constexpr int kBlock = 256;      // threads per workgroup (4 waves of 64)
+constexpr int kRowCap = 256;     // rows per SpMV row block (one thread per row)
+constexpr int kNnzCap = 2048;    // nnz staged in LDS per row block (16 KiB fp64)
+constexpr int kItemCap = 2048;   // merge items (rows + nnz) per row block
+constexpr int kSpmvGrid = 2048;  // max SpMV workgroups (= max epilogue partials)
+constexpr int kRedGrid = 1024;   // max BLAS-1 workgroups (= max reduction partials)
+constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's LDS copy of y
+constexpr int kGramChunk = 64;   // vector elements staged per Gram tile
+constexpr int kGramMaxVec = 72;  // max vectors on either side of a Gram product
+
+// SpMV epilogues (fused into the row reduction of the same launch)
+enum Epilogue : int {
+  kEpiPlain = 0,    // y = A x
+  kEpiDot = 1,      // y = A x ; partial += aux . y       (first MGS dot, solvers.py:194)
+  kEpiResNorm = 2,  // partial += (A x - b)^2, no store   (true residual, solvers.py:290)
+  kEpiR0 = 3        // y = b - A x ; partial += y^2       (r0 and beta, solvers.py:167-175)
+};
+
+struct CsrView {
+  int64_t n_rows;
+  const int32_t* indptr;
+  const int32_t* indices;
+  const double* vals;
+  const int32_t* blk_row;  // row-block boundaries [n_blk + 1]
+  int32_t n_blk;
+};
+
+// grid sizes (a fixed count when partials are all-reduced across ranks)
+int spmv_grid(const CsrView& A, bool fixed);
+int blas_grid(int64_t n, bool fixed);
+
+hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
+                       double* partials, int grid, hipStream_t s);
+// y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
+hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
+                           const double* part_in, int n_in, double* part_out, double* h_out,
+                           int grid, hipStream_t s);
+// h = sqrt(sum(part_in)); q_next = y / h (if h != 0)
+hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
+                            int n_in, double* h_out, hipStream_t s, int grid);
+// x = Z[:, :p] y + x0
+hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
+                       const double* x0, double* x, hipStream_t s);
+// partial dot / sum of squares
+hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_out, int grid,
+                      hipStream_t s);
+// out[0] = sum(part) (op 0) or sqrt(sum(part)) (op 1)
+hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s);
+hipError_t launch_axpy(int64_t n, double h, const double* x, double* y, hipStream_t s);
+hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
+// send[i] = x[idx[i]]
+hipError_t launch_gather(int64_t m, const int32_t* idx, const double* x, double* send,
+                         hipStream_t s);
+// G_partial[block][a*nv+b] over the block's chunks; then reduced into G
+hipError_t launch_gram(int64_t n, int nu, const double* const* U, int nv, const double* const* V,
+                       double* partials, int grid, double* G, hipStream_t s);
+
+}  // namespace spis

@@ -1,0 +1,1181 @@
+// spis.cpp — libspis.so: context, CSR upload + SpMV schedule, halo exchange (RCCL), BLAS-1
+// primitives and the CGMRES / FGMRES / prototypical-CGMRES driver (include/spis.h).
+//
+// The driver restates solvers.py:131-323 (cgmres), :58-127 (gmres) and :328-445 (cgmres_p)
+// around device-resident data: the Krylov basis Q (and Z when preconditioned) lives in HBM as
+// row-major (k+1, pitch) fp64, every N-length operation is a HIP kernel (kernels.hip), and only
+// the Hessenberg column (j+2 scalars), residual partials and the small LS solution cross PCIe.
+// One host synchronisation per iteration: the GEMV + true-residual SpMV of iteration j are
+// enqueued together with the Arnoldi step of iteration j+1 (which does not depend on them), and
+// the host then waits once for both; a stop at j discards the speculative Arnoldi work.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "lsq.h"
+#include "spis.h"
+
+using namespace spis;
+
+// ------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(SPIS_ERR_HIP, "%s:%d: %s -> %s", __FILE__, __LINE__, #expr,               \
+                  hipGetErrorString(_e));                                                     \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                        \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess)                                                                    \
+      return fail(SPIS_ERR_RCCL, "%s:%d: %s -> %s", __FILE__, __LINE__, #expr,              \
+                  ncclGetErrorString(_r));                                                    \
+  } while (0)
+
+#define ST_TRY(expr)                  \
+  do {                                \
+    int _s = (expr);                  \
+    if (_s != SPIS_OK) return _s;     \
+  } while (0)
+
+#define ABI_GUARD(...)                                                           \
+  try {                                                                          \
+    __VA_ARGS__                                                                  \
+  } catch (const std::bad_alloc&) {                                              \
+    return fail(SPIS_ERR_ALLOC, "host allocation failed");                      \
+  } catch (...) {                                                                \
+    return fail(SPIS_ERR_STATE, "unexpected C++ exception");                    \
+  }
+
+static double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// ------------------------------------------------------------------------------------------------
+// objects
+// ------------------------------------------------------------------------------------------------
+struct spis_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  double* partA = nullptr;  // reduction partials, ping
+  double* partB = nullptr;  // reduction partials, pong
+  double* partR = nullptr;  // true-residual partials
+  double* dscal = nullptr;  // small device scalars (kMaxK + 8)
+  double* pinned = nullptr;  // pinned host staging
+  size_t pinned_len = 0;     // doubles
+  double* gram_part = nullptr;
+  size_t gram_part_len = 0;
+  double* gram_G = nullptr;
+  const double** gram_ptrs = nullptr;  // device array of 2 * kGramMaxVec pointers
+  double* gram_pinned = nullptr;       // host staging of Gram tiles + pointer lists
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<spis_workspace*> pool;
+  // live kernel timing (spis_profile_*): HIP events on this stream around each timed launch
+  bool prof = false;
+  std::vector<hipEvent_t> ev_free;
+  struct Pending { int kind; hipEvent_t a, b; };
+  std::vector<Pending> ev_pending;
+  double prof_ms[SPIS_PROF_KINDS] = {0};
+  int64_t prof_n[SPIS_PROF_KINDS] = {0};
+};
+
+struct spis_matrix {
+  spis_context* ctx = nullptr;
+  int64_t n_rows = 0, n_cols = 0, nnz = 0;
+  int32_t* indptr = nullptr;
+  int32_t* indices = nullptr;
+  double* vals = nullptr;
+  int32_t* blk_row = nullptr;
+  int32_t n_blk = 0, n_long = 0;
+  bool all_zero = false;
+  // halo plan
+  int32_t n_ghost = 0;
+  std::vector<int32_t> nbr, scnt, rcnt, soff, roff;
+  int64_t n_send = 0;
+  int32_t* send_idx = nullptr;
+  double* send_buf = nullptr;
+  CsrView view() const { return CsrView{n_rows, indptr, indices, vals, blk_row, n_blk}; }
+};
+
+struct ConCache {
+  double* MZ = nullptr;  // (k) x pitch_n : M z_i
+  int cols = 0;
+  double* Mx0 = nullptr;
+  bool mx0_done = false;
+};
+
+struct spis_workspace {
+  spis_context* ctx = nullptr;
+  int64_t n = 0, pitch = 0, pitch_n = 0;
+  int k = 0;
+  bool sep_z = false;
+  double* Q = nullptr;
+  double* Zb = nullptr;  // == Q when not preconditioned
+  double* w = nullptr;   // Arnoldi vector
+  double* xj = nullptr;  // iterate (with ghost space)
+  double* r0 = nullptr;
+  double* x0 = nullptr;  // copy of x0 (n)
+  double* ext = nullptr;  // scratch SpMV input with ghost space (constraint / preconditioner halos)
+  double* ydev = nullptr;
+  int32_t ext_len = 0;
+  std::vector<ConCache> con;
+  std::vector<double> y_all;  // k*k host copy of every iteration's y
+  std::vector<double> H;      // (k+1) x k column-major Hessenberg (host)
+  int steps = 0;
+  int n_iter_y = 0;           // iterations with a stored y
+  bool broke_at_start = false;
+};
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+static bool fixed_grid(const spis_context* c) { return c->comm != nullptr; }
+
+// ---- live kernel timing ------------------------------------------------------------------------
+static hipEvent_t prof_event(spis_context* c) {
+  if (!c->ev_free.empty()) {
+    hipEvent_t e = c->ev_free.back();
+    c->ev_free.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct ProfScope {  // records [a, b] around the launches issued in its lifetime
+  spis_context* c;
+  int kind;
+  hipEvent_t a = nullptr;
+  ProfScope(spis_context* c_, int kind_) : c(c_), kind(kind_) {
+    if (c->prof) {
+      a = prof_event(c);
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~ProfScope() {
+    if (c->prof && a) {
+      hipEvent_t b = prof_event(c);
+      (void)hipEventRecord(b, c->stream);
+      c->ev_pending.push_back({kind, a, b});
+    }
+  }
+};
+
+// after a stream synchronisation: fold completed event pairs into the totals
+static void prof_drain(spis_context* c) {
+  for (auto& p : c->ev_pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      c->prof_ms[p.kind] += ms;
+      c->prof_n[p.kind] += 1;
+    }
+    c->ev_free.push_back(p.a);
+    c->ev_free.push_back(p.b);
+  }
+  c->ev_pending.clear();
+}
+
+static int allreduce(spis_context* c, double* buf, int64_t count) {
+  if (!c->comm || count <= 0) return SPIS_OK;
+  NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
+  return SPIS_OK;
+}
+
+static int exchange(spis_context* c, const spis_matrix* M, double* x) {
+  if (!c->comm || M->nbr.empty()) return SPIS_OK;
+  HIP_TRY(launch_gather(M->n_send, M->send_idx, x, M->send_buf, c->stream));
+  NCCL_TRY(ncclGroupStart());
+  for (size_t i = 0; i < M->nbr.size(); ++i) {
+    if (M->scnt[i] > 0)
+      NCCL_TRY(ncclSend(M->send_buf + M->soff[i], M->scnt[i], ncclDouble, M->nbr[i], c->comm, c->stream));
+    if (M->rcnt[i] > 0)
+      NCCL_TRY(ncclRecv(x + M->n_rows + M->roff[i], M->rcnt[i], ncclDouble, M->nbr[i], c->comm, c->stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return SPIS_OK;
+}
+
+static int ensure_pinned(spis_context* c, size_t len) {
+  if (c->pinned_len >= len) return SPIS_OK;
+  if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
+  c->pinned = nullptr;
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double), hipHostMallocDefault));
+  c->pinned_len = len;
+  return SPIS_OK;
+}
+
+// y = M x where x is a local vector (owned part valid); ghosts gathered through scratch if needed
+static int spmv_local(spis_context* c, spis_workspace* ws, const spis_matrix* M, const double* x,
+                      double* y) {
+  const int g = spmv_grid(M->view(), fixed_grid(c));
+  if (c->comm && M->n_ghost > 0) {
+    if (!ws->ext || ws->ext_len < M->n_rows + M->n_ghost) {
+      if (ws->ext) HIP_TRY(hipFree(ws->ext));
+      ws->ext_len = static_cast<int32_t>(M->n_rows + M->n_ghost);
+      HIP_TRY(hipMalloc(&ws->ext, sizeof(double) * ws->ext_len));
+    }
+    HIP_TRY(launch_copy(M->n_rows, x, ws->ext, c->stream));
+    ST_TRY(exchange(c, M, ws->ext));
+    HIP_TRY(launch_spmv(M->view(), kEpiPlain, ws->ext, y, nullptr, nullptr, g, c->stream));
+    return SPIS_OK;
+  }
+  HIP_TRY(launch_spmv(M->view(), kEpiPlain, x, y, nullptr, nullptr, g, c->stream));
+  return SPIS_OK;
+}
+
+// G (nu x nv, host row-major) = U^T V, tiled by kGramMaxVec-vector panels; all-reduced
+static int gram(spis_context* c, int64_t n, int nu, const double* const* U, int nv,
+                const double* const* V, double* G_host) {
+  const int T = 64;
+  const int grid = fixed_grid(c) ? 512 : static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(512, (n + kGramChunk - 1) / kGramChunk)));
+  const size_t need = static_cast<size_t>(grid) * T * T;
+  if (c->gram_part_len < need) {
+    if (c->gram_part) HIP_TRY(hipFree(c->gram_part));
+    HIP_TRY(hipMalloc(&c->gram_part, need * sizeof(double)));
+    c->gram_part_len = need;
+  }
+  if (!c->gram_G) HIP_TRY(hipMalloc(&c->gram_G, sizeof(double) * T * T));
+  if (!c->gram_ptrs) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->gram_ptrs), sizeof(double*) * 2 * kGramMaxVec));
+  if (!c->gram_pinned)
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->gram_pinned), sizeof(double) * (T * T + 2 * kGramMaxVec),
+                          hipHostMallocDefault));
+  for (int u0 = 0; u0 < nu; u0 += T) {
+    const int tu = std::min(T, nu - u0);
+    for (int v0 = 0; v0 < nv; v0 += T) {
+      const int tv = std::min(T, nv - v0);
+      const double** hp = reinterpret_cast<const double**>(c->gram_pinned + T * T);
+      for (int a = 0; a < tu; ++a) hp[a] = U[u0 + a];
+      for (int b = 0; b < tv; ++b) hp[kGramMaxVec + b] = V[v0 + b];
+      HIP_TRY(hipMemcpyAsync(c->gram_ptrs, hp, sizeof(double*) * 2 * kGramMaxVec, hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(launch_gram(n, tu, c->gram_ptrs, tv, c->gram_ptrs + kGramMaxVec, c->gram_part, grid, c->gram_G, c->stream));
+      ST_TRY(allreduce(c, c->gram_G, static_cast<int64_t>(tu) * tv));
+      HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->gram_G, sizeof(double) * tu * tv, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (int a = 0; a < tu; ++a)
+        for (int b = 0; b < tv; ++b)
+          G_host[static_cast<size_t>(u0 + a) * nv + v0 + b] = c->gram_pinned[static_cast<size_t>(a) * tv + b];
+    }
+  }
+  return SPIS_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// library / context
+// ------------------------------------------------------------------------------------------------
+extern "C" int spis_abi_version(void) { return SPIS_ABI_VERSION; }
+extern "C" const char* spis_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int spis_device_count(int32_t* count) {
+  ABI_GUARD({
+    if (!count) return fail(SPIS_ERR_ARG, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_context_create(int32_t device, spis_context** out) {
+  ABI_GUARD({
+    if (!out) return fail(SPIS_ERR_ARG, "null out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+      return fail(SPIS_ERR_HIP, "no HIP device visible (libspis needs an MI355X)");
+    if (device < 0 || device >= n) return fail(SPIS_ERR_ARG, "device %d out of range [0,%d)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<spis_context> c(new spis_context());
+    c->device = device;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const int np = std::max(kSpmvGrid, kRedGrid);
+    HIP_TRY(hipMalloc(&c->partA, sizeof(double) * np));
+    HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
+    HIP_TRY(hipMalloc(&c->partR, sizeof(double) * np));
+    HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
+    ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
+    *out = c.release();
+    return SPIS_OK;
+  })
+}
+
+static void free_workspace(spis_workspace* ws) {
+  (void)hipFree(ws->Q);
+  if (ws->sep_z) (void)hipFree(ws->Zb);
+  (void)hipFree(ws->w);
+  (void)hipFree(ws->xj);
+  (void)hipFree(ws->r0);
+  (void)hipFree(ws->x0);
+  (void)hipFree(ws->ydev);
+  if (ws->ext) (void)hipFree(ws->ext);
+  for (auto& cc : ws->con) {
+    if (cc.MZ) (void)hipFree(cc.MZ);
+    if (cc.Mx0) (void)hipFree(cc.Mx0);
+  }
+  delete ws;
+}
+
+extern "C" int spis_context_destroy(spis_context* c) {
+  ABI_GUARD({
+    if (!c) return SPIS_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto* ws : c->pool) free_workspace(ws);
+    (void)hipFree(c->partA);
+    (void)hipFree(c->partB);
+    (void)hipFree(c->partR);
+    (void)hipFree(c->dscal);
+    if (c->gram_part) (void)hipFree(c->gram_part);
+    if (c->gram_G) (void)hipFree(c->gram_G);
+    if (c->gram_ptrs) (void)hipFree(c->gram_ptrs);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->gram_pinned) (void)hipHostFree(c->gram_pinned);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    for (auto& p : c->ev_pending) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_context_synchronize(spis_context* c) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_context_stream(spis_context* c, void** s) {
+  if (!c || !s) return fail(SPIS_ERR_ARG, "null argument");
+  *s = c->stream;
+  return SPIS_OK;
+}
+
+extern "C" int spis_profile_enable(spis_context* c, int32_t on) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    prof_drain(c);
+    c->prof = on != 0;
+    for (int i = 0; i < SPIS_PROF_KINDS; ++i) {
+      c->prof_ms[i] = 0.0;
+      c->prof_n[i] = 0;
+    }
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_profile_read(spis_context* c, double ms_out[SPIS_PROF_KINDS], int64_t count_out[SPIS_PROF_KINDS]) {
+  ABI_GUARD({
+    if (!c || !ms_out || !count_out) return fail(SPIS_ERR_ARG, "null argument");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    prof_drain(c);
+    for (int i = 0; i < SPIS_PROF_KINDS; ++i) {
+      ms_out[i] = c->prof_ms[i];
+      count_out[i] = c->prof_n[i];
+    }
+    return SPIS_OK;
+  })
+}
+
+// ------------------------------------------------------------------------------------------------
+// RCCL
+// ------------------------------------------------------------------------------------------------
+extern "C" int spis_comm_unique_id(uint8_t id_out[128]) {
+  ABI_GUARD({
+    if (!id_out) return fail(SPIS_ERR_ARG, "null id");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id_out, id.internal, 128);
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_comm_init(spis_context* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+  ABI_GUARD({
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPIS_ERR_ARG, "bad comm args");
+    if (nranks == 1) return SPIS_OK;  // single rank: no collectives
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, 128);
+    NCCL_TRY(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_comm_allreduce_sum(spis_context* c, double* buf, int64_t count) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    ST_TRY(allreduce(c, buf, count));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_comm_barrier(spis_context* c) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    ST_TRY(allreduce(c, c->dscal, 1));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+// ------------------------------------------------------------------------------------------------
+// matrices
+// ------------------------------------------------------------------------------------------------
+// Row blocks: greedy walk over rows; a block closes before it would exceed kRowCap rows,
+// kNnzCap nnz or kItemCap merge items (rows + nnz).  A row with more than kNnzCap entries forms
+// a block of its own (workgroup-wide reduction in the kernel).  For bounded FE rows this is the
+// merge-path partition snapped to row boundaries: every block carries ~kItemCap items.
+static void build_row_blocks(int64_t n, const int32_t* rp, std::vector<int32_t>& blk, int32_t& n_long) {
+  blk.clear();
+  blk.push_back(0);
+  n_long = 0;
+  int64_t rows = 0, nnz = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t len = static_cast<int64_t>(rp[r + 1]) - rp[r];
+    if (len > kNnzCap) {
+      if (rows > 0) blk.push_back(static_cast<int32_t>(r));
+      blk.push_back(static_cast<int32_t>(r + 1));
+      ++n_long;
+      rows = nnz = 0;
+      continue;
+    }
+    if (rows > 0 && (rows + 1 > kRowCap || nnz + len > kNnzCap || rows + 1 + nnz + len > kItemCap)) {
+      blk.push_back(static_cast<int32_t>(r));
+      rows = nnz = 0;
+    }
+    ++rows;
+    nnz += len;
+  }
+  if (rows > 0) blk.push_back(static_cast<int32_t>(n));
+}
+
+extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                               const int32_t* indptr, const int32_t* indices, const double* data,
+                               const spis_halo_desc* halo, spis_matrix** out) {
+  ABI_GUARD({
+    if (!c || !out || !indptr || (nnz > 0 && (!indices || !data)))
+      return fail(SPIS_ERR_ARG, "null argument");
+    if (n_rows < 0 || n_cols < 0 || nnz < 0 || n_rows >= (int64_t(1) << 31) || nnz >= (int64_t(1) << 31))
+      return fail(SPIS_ERR_ARG, "sizes out of int32 range");
+    if (indptr[0] != 0 || indptr[n_rows] != nnz) return fail(SPIS_ERR_ARG, "indptr[0] != 0 or indptr[n] != nnz");
+    const int32_t n_ghost = halo ? halo->n_ghost : 0;
+    if (n_cols != n_rows + n_ghost)
+      return fail(SPIS_ERR_ARG, "n_cols (%lld) must equal n_rows + n_ghost (%lld)", (long long)n_cols,
+                  (long long)(n_rows + n_ghost));
+    for (int64_t r = 0; r < n_rows; ++r)
+      if (indptr[r + 1] < indptr[r]) return fail(SPIS_ERR_ARG, "indptr not monotone at row %lld", (long long)r);
+    bool all_zero = true;
+    for (int64_t i = 0; i < nnz; ++i) {
+      if (indices[i] < 0 || indices[i] >= n_cols)
+        return fail(SPIS_ERR_ARG, "column index %d out of range at %lld", indices[i], (long long)i);
+      if (data[i] != 0.0) all_zero = false;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    std::unique_ptr<spis_matrix> M(new spis_matrix());
+    M->ctx = c;
+    M->n_rows = n_rows;
+    M->n_cols = n_cols;
+    M->nnz = nnz;
+    M->all_zero = all_zero;
+    std::vector<int32_t> blk;
+    build_row_blocks(n_rows, indptr, blk, M->n_long);
+    M->n_blk = static_cast<int32_t>(blk.size()) - 1;
+    HIP_TRY(hipMalloc(&M->indptr, sizeof(int32_t) * (n_rows + 1)));
+    HIP_TRY(hipMalloc(&M->indices, sizeof(int32_t) * std::max<int64_t>(nnz, 1)));
+    HIP_TRY(hipMalloc(&M->vals, sizeof(double) * std::max<int64_t>(nnz, 1)));
+    HIP_TRY(hipMalloc(&M->blk_row, sizeof(int32_t) * blk.size()));
+    HIP_TRY(hipMemcpy(M->indptr, indptr, sizeof(int32_t) * (n_rows + 1), hipMemcpyHostToDevice));
+    if (nnz > 0) {
+      HIP_TRY(hipMemcpy(M->indices, indices, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(M->vals, data, sizeof(double) * nnz, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(M->blk_row, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+    if (halo && halo->n_neighbors > 0) {
+      M->n_ghost = n_ghost;
+      const int nn = halo->n_neighbors;
+      M->nbr.assign(halo->neighbors, halo->neighbors + nn);
+      M->scnt.assign(halo->send_counts, halo->send_counts + nn);
+      M->rcnt.assign(halo->recv_counts, halo->recv_counts + nn);
+      M->soff.assign(nn, 0);
+      M->roff.assign(nn, 0);
+      int64_t so = 0, ro = 0;
+      for (int i = 0; i < nn; ++i) {
+        M->soff[i] = static_cast<int32_t>(so);
+        M->roff[i] = static_cast<int32_t>(ro);
+        so += M->scnt[i];
+        ro += M->rcnt[i];
+      }
+      if (ro != n_ghost) return fail(SPIS_ERR_ARG, "sum(recv_counts)=%lld != n_ghost=%d", (long long)ro, n_ghost);
+      for (int64_t i = 0; i < so; ++i)
+        if (halo->send_idx[i] < 0 || halo->send_idx[i] >= n_rows) return fail(SPIS_ERR_ARG, "send_idx out of range");
+      M->n_send = so;
+      HIP_TRY(hipMalloc(&M->send_idx, sizeof(int32_t) * std::max<int64_t>(so, 1)));
+      HIP_TRY(hipMalloc(&M->send_buf, sizeof(double) * std::max<int64_t>(so, 1)));
+      if (so > 0) HIP_TRY(hipMemcpy(M->send_idx, halo->send_idx, sizeof(int32_t) * so, hipMemcpyHostToDevice));
+    } else if (n_ghost > 0) {
+      M->n_ghost = n_ghost;  // ghost columns without peers: caller fills them
+    }
+    *out = M.release();
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_matrix_destroy(spis_matrix* M) {
+  ABI_GUARD({
+    if (!M) return SPIS_OK;
+    (void)hipSetDevice(M->ctx->device);
+    (void)hipStreamSynchronize(M->ctx->stream);
+    (void)hipFree(M->indptr);
+    (void)hipFree(M->indices);
+    (void)hipFree(M->vals);
+    (void)hipFree(M->blk_row);
+    if (M->send_idx) (void)hipFree(M->send_idx);
+    if (M->send_buf) (void)hipFree(M->send_buf);
+    delete M;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_matrix_info(spis_matrix* M, int64_t info[8]) {
+  if (!M || !info) return fail(SPIS_ERR_ARG, "null argument");
+  info[0] = M->n_rows;
+  info[1] = M->n_cols;
+  info[2] = M->nnz;
+  info[3] = M->n_blk;
+  info[4] = M->n_long;
+  info[5] = M->n_ghost;
+  info[6] = M->all_zero ? 1 : 0;
+  info[7] = 0;
+  return SPIS_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// memory + primitives
+// ------------------------------------------------------------------------------------------------
+extern "C" int spis_malloc(spis_context* c, int64_t bytes, void** out) {
+  ABI_GUARD({
+    if (!c || !out || bytes < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(out, std::max<int64_t>(bytes, 16)));
+    HIP_TRY(hipMemsetAsync(*out, 0, std::max<int64_t>(bytes, 16), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_free(spis_context* c, void* p) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (p) HIP_TRY(hipFree(p));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_memcpy_h2d(spis_context* c, void* dst, const void* src, int64_t bytes) {
+  ABI_GUARD({
+    if (!c || (bytes > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
+    if (bytes > 0) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_memcpy_d2h(spis_context* c, void* dst, const void* src, int64_t bytes) {
+  ABI_GUARD({
+    if (!c || (bytes > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
+    if (bytes > 0) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) {
+  ABI_GUARD({
+    if (!c || !A || !x || !y) return fail(SPIS_ERR_ARG, "null argument");
+    ST_TRY(exchange(c, A, x));
+    HIP_TRY(launch_spmv(A->view(), kEpiPlain, x, y, nullptr, nullptr, spmv_grid(A->view(), fixed_grid(c)), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_residual_norm(spis_context* c, spis_matrix* A, double* x, const double* b, double* out) {
+  ABI_GUARD({
+    if (!c || !A || !x || !b || !out) return fail(SPIS_ERR_ARG, "null argument");
+    ST_TRY(exchange(c, A, x));
+    const int g = spmv_grid(A->view(), fixed_grid(c));
+    HIP_TRY(launch_spmv(A->view(), kEpiResNorm, x, nullptr, b, c->partA, g, c->stream));
+    ST_TRY(allreduce(c, c->partA, g));
+    HIP_TRY(launch_finalize(c->partA, g, c->dscal, 1, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+static int dot_impl(spis_context* c, int64_t n, const double* x, const double* y, double* out, int op) {
+  const int g = blas_grid(n, fixed_grid(c));
+  HIP_TRY(launch_dot(n, x, y, c->partA, g, c->stream));
+  ST_TRY(allreduce(c, c->partA, g));
+  HIP_TRY(launch_finalize(c->partA, g, c->dscal, op, c->stream));
+  HIP_TRY(hipMemcpyAsync(out, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SPIS_OK;
+}
+
+extern "C" int spis_dot(spis_context* c, int64_t n, const double* x, const double* y, double* out) {
+  ABI_GUARD({
+    if (!c || !x || !y || !out || n < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    return dot_impl(c, n, x, y, out, 0);
+  })
+}
+
+extern "C" int spis_nrm2(spis_context* c, int64_t n, const double* x, double* out) {
+  ABI_GUARD({
+    if (!c || !x || !out || n < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    return dot_impl(c, n, x, x, out, 1);
+  })
+}
+
+extern "C" int spis_axpy(spis_context* c, int64_t n, double h, const double* x, double* y) {
+  ABI_GUARD({
+    if (!c || !x || !y || n < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    HIP_TRY(launch_axpy(n, h, x, y, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_gemv(spis_context* c, int64_t n, int32_t p, const double* Z, int64_t pitch,
+                         const double* y_host, const double* x0, double* x) {
+  ABI_GUARD({
+    if (!c || !Z || !y_host || !x0 || !x || n < 0 || p < 1 || p > kMaxK || pitch < n)
+      return fail(SPIS_ERR_ARG, "bad argument");
+    for (int i = 0; i < p; ++i) c->pinned[i] = y_host[i];
+    HIP_TRY(hipMemcpyAsync(c->dscal, c->pinned, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_gemv(n, p, Z, pitch, c->dscal, x0, x, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_gram(spis_context* c, int64_t n, int32_t nu, const double* const* U, int32_t nv,
+                         const double* const* V, double* G) {
+  ABI_GUARD({
+    if (!c || !U || !V || !G || nu < 1 || nv < 1 || n < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    return gram(c, n, nu, U, nv, V, G);
+  })
+}
+
+// ------------------------------------------------------------------------------------------------
+// constraint terms (class form), solvers.py:21-40
+// ------------------------------------------------------------------------------------------------
+static int constraint_terms(spis_context* c, spis_workspace* ws, ConCache* cc, const spis_constraint_desc& con,
+                            int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                            double* term0, double* term1, double* term2) {
+  const bool mzero = con.M == nullptr || con.M->all_zero;
+  std::vector<const double*> U, V;
+  for (int i = 0; i < p; ++i) U.push_back(Z + static_cast<int64_t>(i) * pitch);
+  U.push_back(x0);
+  int iv = -1, imx = -1;
+  if (!mzero) {
+    if (con.M->n_rows != n) return fail(SPIS_ERR_ARG, "constraint matrix rows %lld != n %lld", (long long)con.M->n_rows, (long long)n);
+    // M z_i, cached across constrained steps of one solve (the basis never changes)
+    for (int i = cc->cols; i < p; ++i)
+      ST_TRY(spmv_local(c, ws, con.M, Z + static_cast<int64_t>(i) * pitch, cc->MZ + static_cast<int64_t>(i) * ws->pitch_n));
+    cc->cols = std::max(cc->cols, p);
+    if (!cc->mx0_done) {
+      ST_TRY(spmv_local(c, ws, con.M, x0, cc->Mx0));
+      cc->mx0_done = true;
+    }
+    for (int i = 0; i < p; ++i) V.push_back(cc->MZ + static_cast<int64_t>(i) * ws->pitch_n);
+  }
+  if (con.v_dev) { iv = static_cast<int>(V.size()); V.push_back(con.v_dev); }
+  if (!mzero) { imx = static_cast<int>(V.size()); V.push_back(cc->Mx0); }
+  const int nu = p + 1, nv = static_cast<int>(V.size());
+  std::vector<double> G(static_cast<size_t>(nu) * std::max(nv, 1), 0.0);
+  if (nv > 0) ST_TRY(gram(c, n, nu, U.data(), nv, V.data(), G.data()));
+  auto g = [&](int a, int b) { return G[static_cast<size_t>(a) * nv + b]; };
+  const double x0Mx0 = imx >= 0 ? g(p, imx) : 0.0;
+  const double vx0 = iv >= 0 ? g(p, iv) : 0.0;
+  *term0 = 0.5 * x0Mx0 + con.c + vx0;  // 0.5*x0@M@x0 + c + v@x0  (solvers.py:34)
+  for (int a = 0; a < p; ++a) {         // v@Z + x0@MZ             (:35)
+    const double vz = iv >= 0 ? g(a, iv) : 0.0;
+    const double xmz = mzero ? 0.0 : g(p, a);
+    term1[a] = vz + xmz;
+  }
+  for (int a = 0; a < p; ++a)           // 0.5*Z.T@MZ              (:36)
+    for (int b = 0; b < p; ++b) term2[static_cast<size_t>(a) * p + b] = mzero ? 0.0 : 0.5 * g(a, b);
+  return SPIS_OK;
+}
+
+static int ensure_con_cache(spis_workspace* ws, size_t ncon, const spis_constraint_desc* cons) {
+  if (ws->con.size() < ncon) ws->con.resize(ncon);
+  for (size_t i = 0; i < ncon; ++i) {
+    ConCache& cc = ws->con[i];
+    cc.cols = 0;
+    cc.mx0_done = false;
+    const bool mzero = cons[i].M == nullptr || cons[i].M->all_zero;
+    if (!mzero && !cc.MZ) {
+      HIP_TRY(hipMalloc(&cc.MZ, sizeof(double) * ws->pitch_n * ws->k));
+      HIP_TRY(hipMalloc(&cc.Mx0, sizeof(double) * ws->pitch_n));
+    }
+  }
+  return SPIS_OK;
+}
+
+extern "C" int spis_constraint_terms(spis_context* c, const spis_constraint_desc* con, int64_t n, int32_t p,
+                                     const double* Z, int64_t pitch, const double* x0, double* term0,
+                                     double* term1, double* term2) {
+  ABI_GUARD({
+    if (!c || !con || !Z || !x0 || !term0 || !term1 || !term2 || p < 1 || n < 0 || pitch < n)
+      return fail(SPIS_ERR_ARG, "bad argument");
+    spis_workspace tmp;
+    tmp.ctx = c;
+    tmp.n = n;
+    tmp.pitch_n = round_up(std::max<int64_t>(n, 1), 64);
+    tmp.k = p;
+    ST_TRY(ensure_con_cache(&tmp, 1, con));
+    int st = constraint_terms(c, &tmp, &tmp.con[0], *con, n, p, Z, pitch, x0, term0, term1, term2);
+    (void)hipStreamSynchronize(c->stream);
+    if (tmp.con[0].MZ) (void)hipFree(tmp.con[0].MZ);
+    if (tmp.con[0].Mx0) (void)hipFree(tmp.con[0].Mx0);
+    if (tmp.ext) (void)hipFree(tmp.ext);
+    return st;
+  })
+}
+
+// ------------------------------------------------------------------------------------------------
+// workspace
+// ------------------------------------------------------------------------------------------------
+static int get_workspace(spis_context* c, int64_t n, int64_t n_ext, int k, bool sep_z, spis_workspace** out) {
+  const int64_t pitch = round_up(std::max<int64_t>(n_ext, 1), 64);
+  for (size_t i = 0; i < c->pool.size(); ++i) {
+    spis_workspace* ws = c->pool[i];
+    if (ws->n == n && ws->pitch == pitch && ws->k == k && ws->sep_z == sep_z) {
+      c->pool.erase(c->pool.begin() + i);
+      *out = ws;
+      return SPIS_OK;
+    }
+  }
+  std::unique_ptr<spis_workspace> ws(new spis_workspace());
+  ws->ctx = c;
+  ws->n = n;
+  ws->pitch = pitch;
+  ws->pitch_n = round_up(std::max<int64_t>(n, 1), 64);
+  ws->k = k;
+  ws->sep_z = sep_z;
+  const size_t basis = sizeof(double) * pitch * (k + 1);
+  HIP_TRY(hipMalloc(&ws->Q, basis));
+  HIP_TRY(hipMemsetAsync(ws->Q, 0, basis, c->stream));
+  if (sep_z) {
+    HIP_TRY(hipMalloc(&ws->Zb, basis));
+    HIP_TRY(hipMemsetAsync(ws->Zb, 0, basis, c->stream));
+  } else {
+    ws->Zb = ws->Q;
+  }
+  for (double** p : {&ws->w, &ws->xj, &ws->r0, &ws->x0}) {
+    HIP_TRY(hipMalloc(p, sizeof(double) * pitch));
+    HIP_TRY(hipMemsetAsync(*p, 0, sizeof(double) * pitch, c->stream));
+  }
+  HIP_TRY(hipMalloc(&ws->ydev, sizeof(double) * (k + 1)));
+  *out = ws.release();
+  return SPIS_OK;
+}
+
+extern "C" int spis_workspace_release(spis_workspace* ws) {
+  ABI_GUARD({
+    if (!ws) return SPIS_OK;
+    spis_context* c = ws->ctx;
+    if (c->pool.size() >= 4) {
+      (void)hipStreamSynchronize(c->stream);
+      free_workspace(c->pool.front());
+      c->pool.erase(c->pool.begin());
+    }
+    c->pool.push_back(ws);
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_workspace_iterate(spis_workspace* ws, int32_t i, double* x_out) {
+  ABI_GUARD({
+    if (!ws || !x_out) return fail(SPIS_ERR_ARG, "null argument");
+    spis_context* c = ws->ctx;
+    if (i < 0 || i > ws->n_iter_y) return fail(SPIS_ERR_ARG, "iterate %d not available (have %d)", i, ws->n_iter_y);
+    if (i == 0) {
+      HIP_TRY(launch_copy(ws->n, ws->r0, x_out, c->stream));
+    } else {
+      const double* y = ws->y_all.data() + static_cast<size_t>(i - 1) * ws->k;
+      for (int a = 0; a < i; ++a) c->pinned[a] = y[a];
+      HIP_TRY(hipMemcpyAsync(ws->ydev, c->pinned, sizeof(double) * i, hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(launch_gemv(ws->n, i, ws->Zb, ws->pitch, ws->ydev, ws->x0, x_out, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_workspace_basis(spis_workspace* ws, int32_t p, double* Z_host) {
+  ABI_GUARD({
+    if (!ws || !Z_host || p < 0 || p > ws->k + 1) return fail(SPIS_ERR_ARG, "bad argument");
+    spis_context* c = ws->ctx;
+    HIP_TRY(hipMemcpy2DAsync(Z_host, sizeof(double) * ws->n, ws->Zb, sizeof(double) * ws->pitch,
+                             sizeof(double) * ws->n, p, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SPIS_OK;
+  })
+}
+
+// ------------------------------------------------------------------------------------------------
+// the solver
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+enum Safety { kSafetyNone = -1, kSafetyFalse = 0, kSafetyTrue = 1 };
+
+struct Solver {
+  spis_context* c;
+  spis_matrix* A;
+  const spis_solve_opts* o;
+  spis_workspace* ws;
+  const double* b;
+  int64_t n;
+  int gs;  // SpMV partial count
+  int gb;  // BLAS-1 partial count
+  std::vector<double> hostq, hostz;
+
+  double* Qv(int i) const { return ws->Q + static_cast<int64_t>(i) * ws->pitch; }
+  double* Zv(int i) const { return ws->Zb + static_cast<int64_t>(i) * ws->pitch; }
+
+  // solvers.py:190-198: z_j = P^-1 q_j ; y = A z_j ; MGS ; h_{j+1,j} = ||y|| ; q_{j+1} = y / h
+  int enqueue_arnoldi(int j) {
+    hipStream_t s = c->stream;
+    double* zj = Zv(j);
+    if (o->pre_matrix) {
+      ST_TRY(spmv_local(c, ws, o->pre_matrix, Qv(j), zj));
+    } else if (o->pre_fn) {
+      hostq.resize(n);
+      hostz.resize(n);
+      HIP_TRY(hipMemcpyAsync(hostq.data(), Qv(j), sizeof(double) * n, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (o->pre_fn(o->pre_user, hostq.data(), hostz.data(), n) != 0)
+        return fail(SPIS_ERR_CALLBACK, "preconditioner callback failed at iteration %d", j);
+      HIP_TRY(hipMemcpyAsync(zj, hostz.data(), sizeof(double) * n, hipMemcpyHostToDevice, s));
+    }
+    ST_TRY(exchange(c, A, zj));
+    {
+      ProfScope ps(c, SPIS_PROF_SPMV);
+      HIP_TRY(launch_spmv(A->view(), kEpiDot, zj, ws->w, Qv(0), c->partA, gs, s));
+    }
+    ST_TRY(allreduce(c, c->partA, gs));
+    {
+      ProfScope pm(c, SPIS_PROF_MGS);
+      double* src = c->partA;
+      double* dst = c->partB;
+      int n_in = gs;
+      for (int i = 0; i <= j; ++i) {
+        const double* qn = i < j ? Qv(i + 1) : nullptr;
+        HIP_TRY(launch_mgs_step(n, ws->w, Qv(i), qn, src, n_in, dst, c->dscal + i, gb, s));
+        ST_TRY(allreduce(c, dst, gb));
+        std::swap(src, dst);
+        n_in = gb;
+      }
+      HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, c->dscal + j + 1, s, gb));
+    }
+    HIP_TRY(hipMemcpyAsync(c->pinned, c->dscal, sizeof(double) * (j + 2), hipMemcpyDeviceToHost, s));
+    return SPIS_OK;
+  }
+
+  // solvers.py:287,290: x_j = Z y + x0 ; partials of ||A x_j - b||^2
+  int enqueue_update(int p, const double* y) {
+    hipStream_t s = c->stream;
+    double* yh = c->pinned + 2 * kMaxK;
+    for (int a = 0; a < p; ++a) yh[a] = y[a];
+    HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
+    {
+      ProfScope pg(c, SPIS_PROF_GEMV);
+      HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, ws->x0, ws->xj, s));
+    }
+    ST_TRY(exchange(c, A, ws->xj));
+    {
+      ProfScope ps(c, SPIS_PROF_SPMV_RES);
+      HIP_TRY(launch_spmv(A->view(), kEpiResNorm, ws->xj, nullptr, b, c->partR, gs, s));
+    }
+    ST_TRY(allreduce(c, c->partR, gs));
+    HIP_TRY(hipMemcpyAsync(c->pinned + 3 * kMaxK, c->partR, sizeof(double) * gs, hipMemcpyDeviceToHost, s));
+    return SPIS_OK;
+  }
+
+  double host_residual() const {
+    const double* p = c->pinned + 3 * kMaxK;
+    double t = 0.0;
+    for (int i = 0; i < gs; ++i) t += p[i];
+    return std::sqrt(t);
+  }
+};
+
+}  // namespace
+
+extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, const double* x0,
+                          const spis_solve_opts* o, spis_solve_out* out, spis_workspace** ws_out) {
+  ABI_GUARD({
+    if (!c || !A || !b || !x0 || !o || !out || !ws_out) return fail(SPIS_ERR_ARG, "null argument");
+    const int k = o->k;
+    if (k < 1 || k > kMaxK) return fail(SPIS_ERR_ARG, "k=%d out of range [1,%d]", k, kMaxK);
+    if (o->method < SPIS_CGMRES || o->method > SPIS_CGMRES_P) return fail(SPIS_ERR_ARG, "bad method");
+    if (o->n_constraints < 0 || (o->n_constraints > 0 && !o->constraints && !o->conls_fn))
+      return fail(SPIS_ERR_ARG, "constraints missing");
+    if (!out->res_host || !out->y_host || !out->branch_host || !out->events_host || !out->msg_host)
+      return fail(SPIS_ERR_ARG, "output arrays missing");
+    const int64_t n = A->n_rows;
+    if (o->pre_matrix && o->pre_matrix->n_rows != n) return fail(SPIS_ERR_ARG, "preconditioner size mismatch");
+    for (int i = 0; i < (o->conls_fn ? 0 : o->n_constraints); ++i)
+      if (o->constraints[i].M && o->constraints[i].M->n_rows != n)
+        return fail(SPIS_ERR_ARG, "constraint %d matrix size mismatch", i);
+    HIP_TRY(hipSetDevice(c->device));
+    const bool sep_z = o->pre_matrix != nullptr || o->pre_fn != nullptr;
+    spis_workspace* ws = nullptr;
+    ST_TRY(get_workspace(c, n, n + A->n_ghost, k, sep_z, &ws));
+    std::unique_ptr<spis_workspace, int (*)(spis_workspace*)> guard(ws, spis_workspace_release);
+    ws->steps = 0;
+    ws->n_iter_y = 0;
+    ws->broke_at_start = false;
+    ws->y_all.assign(static_cast<size_t>(k) * k, 0.0);
+    ws->H.assign(static_cast<size_t>(k + 1) * k, 0.0);
+    const bool use_cb = o->conls_fn != nullptr;
+    if (!use_cb && o->n_constraints > 0) ST_TRY(ensure_con_cache(ws, o->n_constraints, o->constraints));
+    ST_TRY(ensure_pinned(c, 3 * kMaxK + std::max(kSpmvGrid, kRedGrid) + 16));
+
+    Solver S{c, A, o, ws, b, n, spmv_grid(A->view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
+    hipStream_t s = c->stream;
+    double* stamps = out->stamps_host;  // [0,k) iter start, [k,2k) iter end, [2k,3k) con start, [3k,4k) con end
+    const double t_start = now_s();
+    for (int i = 0; i < k; ++i) {
+      out->branch_host[i] = SPIS_BRANCH_UNCON;
+      out->events_host[i] = 0;
+      out->msg_host[i] = SPIS_MSG_SUCCESS;
+    }
+
+    // r0 = b - A x0 ; beta = ||r0|| ; q0 = r0 / beta      (solvers.py:167-177)
+    HIP_TRY(launch_copy(n, x0, ws->x0, s));
+    HIP_TRY(launch_copy(n, x0, ws->xj, s));
+    ST_TRY(exchange(c, A, ws->xj));
+    HIP_TRY(launch_spmv(A->view(), kEpiR0, ws->xj, ws->r0, b, c->partA, S.gs, s));
+    ST_TRY(allreduce(c, c->partA, S.gs));
+    HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->dscal, s, S.gb));
+    HIP_TRY(hipMemcpyAsync(c->pinned, c->dscal, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const double beta = c->pinned[0];
+    int n_res = 0;
+    out->res_host[n_res++] = beta;
+    int steps = 0;
+    int safety = kSafetyNone;
+    const double ctol = 1e-12;  // solvers.py:138
+    GivensQR qr;
+    qr.reset(k, beta);
+    std::vector<double> y(k + 1, 0.0), yk(k + 1, 0.0), y0(k + 1, 0.0), ycon(k + 1, 0.0), hcol(k + 2, 0.0);
+    std::vector<QuadCon> cons(std::max(o->n_constraints, 0));
+    int con_steps = 0;
+    bool have_x = false;  // ws->xj holds x[-1] (else x[-1] = r0)
+    bool pending = false;  // an update (GEMV + residual) of iteration j-1 is in flight
+
+    if (beta == 0.0) {  // x0 solves the system: q0 would be 0/0 (reference: NaNs); report breakdown
+      out->events_host[0] |= SPIS_EV_BREAKDOWN;
+      ws->broke_at_start = true;
+    } else {
+      if (stamps) stamps[0] = now_s();
+      ST_TRY(S.enqueue_arnoldi(0));
+    }
+    for (int j = 0; j < k && !ws->broke_at_start; ++j) {
+      HIP_TRY(hipStreamSynchronize(s));
+      prof_drain(c);
+      if (pending) {  // finish iteration j-1: its true residual + stop test (solvers.py:290-297)
+        out->res_host[n_res++] = S.host_residual();
+        pending = false;
+        if (stamps) stamps[k + j - 1] = now_s();
+        const double r = out->res_host[n_res - 1];
+        const bool stop = o->method == SPIS_GMRES ? (r < o->tol)
+                          : o->method == SPIS_CGMRES ? (r < o->tol && safety == kSafetyTrue)
+                                                     : false;
+        if (stop) break;
+      }
+      steps = j + 1;  // solvers.py:189
+      for (int i = 0; i < j + 2; ++i) hcol[i] = c->pinned[i];
+      for (int i = 0; i < j + 2; ++i) ws->H[static_cast<size_t>(j) * (k + 1) + i] = hcol[i];
+      if (hcol[j + 1] == 0.0 && o->method != SPIS_CGMRES_P) {  // :197-202
+        out->events_host[j] |= SPIS_EV_BREAKDOWN;
+        break;
+      }
+      qr.add_column(j, hcol.data());
+      const int p = j + 1;
+      std::fill(y0.begin(), y0.end(), 0.0);
+      for (int a = 0; a < j; ++a) y0[a] = yk[a];  // warm start (:225-227)
+      int branch = SPIS_BRANCH_UNCON, ev = 0, msg = SPIS_MSG_SUCCESS;
+
+      bool constrained = false;
+      int m_active = 0;
+      if (o->method == SPIS_CGMRES) {
+        const double prev = out->res_host[n_res - 1];
+        constrained = !(prev > o->contol * o->tol && j < k - 1 && safety == kSafetyNone);  // :230
+        m_active = o->n_constraints;
+      } else if (o->method == SPIS_CGMRES_P) {
+        constrained = true;
+        m_active = std::min(j, o->n_constraints);  // clist[:j] (:412)
+      }
+
+      if (!constrained) {
+        qr.solve(p, y.data());
+      } else if (use_cb && m_active > 0) {
+        // dict-form constraints: the host callback runs the constrained LS (and its fallback)
+        std::vector<double> Hc(static_cast<size_t>(p + 1) * p);
+        for (int cc = 0; cc < p; ++cc)
+          for (int r = 0; r <= p; ++r) Hc[static_cast<size_t>(cc) * (p + 1) + r] = ws->H[static_cast<size_t>(cc) * (k + 1) + r];
+        HIP_TRY(hipStreamSynchronize(s));
+        if (o->timing) ++con_steps;
+        if (stamps) stamps[2 * k + j] = now_s();
+        int32_t br = SPIS_BRANCH_CON, evc = 0, msc = SPIS_MSG_SUCCESS;
+        if (o->conls_fn(o->conls_user, ws, j, p, Hc.data(), beta, y0.data(), y.data(), &br, &evc, &msc) != 0)
+          return fail(SPIS_ERR_CALLBACK, "constraint callback failed at iteration %d", j);
+        if (stamps) stamps[3 * k + j] = now_s();
+        branch = br;
+        ev = evc;
+        msg = msc;
+        if (o->method == SPIS_CGMRES) {
+          if (branch == SPIS_BRANCH_CON) safety = kSafetyTrue;
+          else if (ev & SPIS_EV_VIOLATION) safety = kSafetyFalse;
+        }
+        if (branch == SPIS_BRANCH_FALLBACK) qr.solve(p, y.data());
+      } else {
+        // class-form constraints reduced on the device (:242-247), KKT on the host (:251-255)
+        if (o->timing && o->method == SPIS_CGMRES) ++con_steps;
+        if (stamps) stamps[2 * k + j] = now_s();
+        for (int i = 0; i < m_active; ++i) {
+          cons[i].term1.assign(p, 0.0);
+          cons[i].term2.assign(static_cast<size_t>(p) * p, 0.0);
+          ST_TRY(constraint_terms(c, ws, &ws->con[i], o->constraints[i], n, p, ws->Zb, ws->pitch, ws->x0,
+                                  &cons[i].term0, cons[i].term1.data(), cons[i].term2.data()));
+        }
+        if (stamps) stamps[3 * k + j] = now_s();
+        bool failed = false;
+        if (m_active == 0) {
+          qr.solve(p, ycon.data());
+        } else {
+          KKTResult kr = kkt_newton(p, qr.R(), qr.ld(), qr.g(), m_active, cons.data(), y0.data(), ycon.data());
+          msg = kr.message;
+        }
+        bool has_nan = false;
+        for (int a = 0; a < p; ++a) has_nan = has_nan || std::isnan(ycon[a]);
+        if (o->method == SPIS_CGMRES) {
+          if (!o->timing && has_nan) {  // :259-260
+            failed = true;
+            ev |= SPIS_EV_NAN;
+          } else {
+            safety = kSafetyTrue;  // :262
+            if (!o->timing) {
+              double dev = 0.0;  // constraint_checker: signed max from 0 (:14-18)
+              for (int i = 0; i < m_active; ++i) dev = std::max(dev, con_value(cons[i], p, ycon.data()));
+              if (dev > ctol) {  // :267-269 (the warning there raises AttributeError -> except)
+                safety = kSafetyFalse;
+                failed = true;
+                ev |= SPIS_EV_VIOLATION;
+              }
+            }
+          }
+        } else if (has_nan) {  // cgmres_p (:418-424)
+          failed = true;
+          ev |= SPIS_EV_NAN;
+        }
+        if (failed) {  // :271-278
+          ev |= SPIS_EV_FALLBACK;
+          branch = SPIS_BRANCH_FALLBACK;
+          msg = SPIS_MSG_SUCCESS;
+          qr.solve(p, y.data());
+        } else {
+          branch = SPIS_BRANCH_CON;
+          for (int a = 0; a < p; ++a) y[a] = ycon[a];
+        }
+      }
+      if (msg != SPIS_MSG_SUCCESS) ev |= SPIS_EV_LS_MESSAGE;  // :280-284
+      out->branch_host[j] = branch;
+      out->events_host[j] |= ev;
+      out->msg_host[j] = msg;
+      for (int a = 0; a < p; ++a) {
+        yk[a] = y[a];
+        ws->y_all[static_cast<size_t>(j) * k + a] = y[a];
+        out->y_host[static_cast<size_t>(j) * k + a] = y[a];
+      }
+      ws->n_iter_y = j + 1;
+      ST_TRY(S.enqueue_update(p, y.data()));
+      have_x = true;
+      pending = true;
+      if (j + 1 < k) {
+        if (stamps) stamps[j + 1] = now_s();
+        ST_TRY(S.enqueue_arnoldi(j + 1));
+      }
+    }
+    if (pending) {
+      HIP_TRY(hipStreamSynchronize(s));
+      prof_drain(c);
+      out->res_host[n_res++] = S.host_residual();
+      if (stamps) stamps[k + ws->n_iter_y - 1] = now_s();
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    prof_drain(c);
+    if (out->x_final_dev) {
+      if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
+      else HIP_TRY(launch_copy(n, have_x ? ws->xj : ws->r0, out->x_final_dev, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (stamps) {
+      stamps[4 * k] = t_start;
+      stamps[4 * k + 1] = now_s();
+    }
+    (void)con_steps;
+    ws->steps = steps;
+    out->steps = steps;
+    out->n_res = n_res;
+    *ws_out = guard.release();
+    return SPIS_OK;
+  })
+}

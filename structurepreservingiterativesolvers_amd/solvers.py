@@ -1,0 +1,456 @@
+"""Drop-in replacement of the reference ``solvers.py`` on the MI355X.
+
+Same names, signatures, return values and warnings as
+``/root/reference/solvers.py``:
+
+* :func:`cgmres`   — ``solvers.py:131-323`` (constrained FGMRES, the hot path)
+* :func:`gmres`    — ``solvers.py:58-127``  (FGMRES)
+* :func:`cgmres_p` — ``solvers.py:328-445`` (prototypical CGMRES)
+* :class:`constraint_container`, :func:`constraint_checker` — ``:14-53``
+
+Every N-length operation runs in ``libspis.so`` (hand-written HIP kernels for
+gfx950; include/spis.h) on HBM-resident data; the host solves only the small
+(p <= k) least-squares problems.  There is no CPU fallback: without the
+library or a visible MI355X these functions raise
+:class:`~._lib.SpisUnavailable`.
+
+Differences from the reference, by design:
+
+* least squares: the unconstrained step is solved exactly by an incremental
+  Givens QR (the reference runs SLSQP to ``ftol=1e-24``), the constrained step
+  by Newton on the KKT system (the reference: SLSQP with equality
+  constraints).  Iterates agree to ~1e-10 relative; SLSQP-specific failure
+  messages ("Iteration limit reached", "Positive directional derivative ...")
+  are not reproduced, SLSQP's m > p exit (x = initial guess) is.
+* ``dict['x']`` is a lazy sequence (:class:`IterateList`): iterates are
+  rebuilt on the device from the stored ``y`` on first access
+  (``Z[:, :i] y_i + x0``, the same kernel as in the loop).
+* inputs may also be :class:`~.device.DeviceVector` (HBM-resident ``b``/``x0``);
+  then ``x[-1]`` is returned as a DeviceVector too.
+"""
+from __future__ import annotations
+
+import collections.abc
+import ctypes as C
+import logging
+import warnings
+
+import numpy as np
+import scipy.optimize as spo
+import scipy.sparse as sps
+
+from . import _lib
+from .device import DeviceMatrix, DeviceVector, device_matrix, device_vector, get_context
+
+log = logging.getLogger("structurepreservingiterativesolvers_amd")
+
+_ACCEPTED = (
+    "Optimization terminated successfully",
+    "`xtol` termination condition is satisfied.",
+    "`gtol` termination condition is satisfied.",
+)
+
+
+# ------------------------------------------------------------------------------------------------
+# constraint algebra (solvers.py:14-53)
+# ------------------------------------------------------------------------------------------------
+def constraint_checker(x, const_list):
+    """``solvers.py:14-18``: signed running max of the constraint values, from 0."""
+    dev = 0
+    for const in const_list:
+        dev = max(dev, const["fun"](x))
+    return dev
+
+
+class constraint_container:
+    """``solvers.py:21-53``: a quadratic constraint ``1/2 X'MX + v.X + c`` seen
+    through ``X = x0 + Z y``.  Class-form constraints are reduced on the device
+    (SpMM ``M Z`` + tall-skinny Gram, ``spis_constraint_terms``) when ``Z`` is a
+    device basis; with host arrays the reduction runs through the same device
+    entry point after an upload.  Dict-form constraints keep their callables."""
+
+    def __init__(self, const, x0, Z):
+        if hasattr(const, "__dict__"):
+            self.optimise = True
+        elif type(const) is dict:
+            self.optimise = None
+        else:
+            raise NotImplementedError("Constraints must be either dictionaries or classes")
+        if self.optimise:
+            self.term0, self.term1, self.term2 = _reduce_on_device(const, np.asarray(x0), np.asarray(Z))
+        else:
+            self.const, self.x0, self.Z = const, x0, Z
+
+    def constraint_func(self, z):
+        if self.optimise:
+            return self.term0 + self.term1 @ z + z @ self.term2 @ z
+        return self.const["func"](z, self.x0, self.Z)
+
+    def constraint_jac(self, z):
+        if self.optimise:
+            return self.term1 + 2 * z @ self.term2
+        return self.const["jac"](z, self.x0, self.Z)
+
+
+def _reduce_on_device(const, x0, Z):
+    ctx = get_context()
+    n, p = Z.shape
+    Zd = DeviceVector.from_host(np.ascontiguousarray(Z.T).reshape(-1), ctx=ctx)
+    x0d = device_vector(x0, ctx=ctx)
+    desc, keep = _constraint_desc(const, n, ctx)
+    t0 = C.c_double()
+    t1 = np.zeros(p)
+    t2 = np.zeros((p, p))
+    _lib.check(
+        ctx.L.spis_constraint_terms(ctx.handle, C.byref(desc), n, p, C.c_void_p(Zd.ptr), n, C.c_void_p(x0d.ptr),
+                                    C.byref(t0), t1.ctypes.data_as(C.POINTER(C.c_double)),
+                                    t2.ctypes.data_as(C.POINTER(C.c_double))),
+        "spis_constraint_terms",
+    )
+    del keep
+    return t0.value, t1, t2
+
+
+# ------------------------------------------------------------------------------------------------
+# device-side constraint descriptors
+# ------------------------------------------------------------------------------------------------
+_ZERO_CACHE: dict = {}
+
+
+def _is_zero_matrix(M):
+    """O(1) for an empty sparse matrix; O(nnz) (cached per object) otherwise."""
+    if M is None:
+        return True
+    if sps.issparse(M):
+        if M.nnz == 0:
+            return True
+        key = (id(M), M.nnz)
+        hit = _ZERO_CACHE.get(key)
+        if hit is None:
+            hit = not np.any(M.data)
+            _ZERO_CACHE[key] = hit
+        return hit
+    return not np.any(M)
+
+
+def _constraint_desc(const, n, ctx):
+    keep = []
+    M = getattr(const, "M", None)
+    Mh = None
+    if not _is_zero_matrix(M):
+        dm = device_matrix(M if sps.issparse(M) else sps.csr_matrix(M), ctx=ctx)
+        if dm.shape[0] != n:
+            raise ValueError(f"constraint matrix has {dm.shape[0]} rows, expected {n}")
+        keep.append(dm)
+        Mh = dm.handle.value
+    v = getattr(const, "v", None)
+    vh = None
+    if v is not None:
+        v = np.asarray(v, dtype=np.float64).reshape(-1)
+        if np.any(v):
+            vd = device_vector(v, ctx=ctx)
+            keep.append(vd)
+            vh = vd.ptr
+    c = float(np.asarray(getattr(const, "c", 0.0)))
+    return _lib.ConstraintDesc(Mh, vh, c), keep
+
+
+# ------------------------------------------------------------------------------------------------
+# lazy iterate list: dict['x']
+# ------------------------------------------------------------------------------------------------
+class IterateList(collections.abc.Sequence):
+    """``x`` of the reference output dict (``solvers.py:169,287``): ``x[0]`` is
+    ``r0 = b - A x0`` (a reference quirk), ``x[i]`` the i-th iterate.  Entries are
+    materialised on the device on first access and cached on the host."""
+
+    def __init__(self, ctx, ws, n, count, final, as_device=False):
+        self._ctx = ctx
+        self._ws = ws
+        self._n = n
+        self._count = count
+        self._cache = {}
+        self._as_device = as_device
+        if count > 1 and final is not None:
+            self._cache[count - 1] = final
+        self._fin = None
+        if ws:
+            self._fin = __import__("weakref").finalize(self, ctx.L.spis_workspace_release, ws)
+
+    def __len__(self):
+        return self._count
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._count))]
+        if i < 0:
+            i += self._count
+        if not 0 <= i < self._count:
+            raise IndexError("iterate index out of range")
+        hit = self._cache.get(i)
+        if hit is None:
+            buf = DeviceVector(self._ctx, self._n)
+            _lib.check(self._ctx.L.spis_workspace_iterate(self._ws, i, C.c_void_p(buf.ptr)), "spis_workspace_iterate")
+            hit = buf if self._as_device else buf.numpy()
+            self._cache[i] = hit
+        return hit
+
+    def __array__(self, dtype=None, copy=None):
+        a = np.stack([np.asarray(self[i]) for i in range(self._count)]) if self._count else np.zeros((0, self._n))
+        return a if dtype is None else a.astype(dtype)
+
+    def basis(self, p):
+        """The first ``p`` Krylov basis vectors used for the iterates (``Z`` rows, (p, N))."""
+        out = np.empty((p, self._n))
+        _lib.check(self._ctx.L.spis_workspace_basis(self._ws, p, out.ctypes.data_as(C.POINTER(C.c_double))),
+                   "spis_workspace_basis")
+        return out
+
+    def release(self):
+        """Free the device basis now (materialised entries stay available)."""
+        if self._fin is not None:
+            self._fin()
+
+
+# ------------------------------------------------------------------------------------------------
+# preconditioners (solvers.py:149-161)
+# ------------------------------------------------------------------------------------------------
+def _precond_setup(pre, n, ctx, keep):
+    """Returns (pre_matrix handle or None, PRECOND_FN or null)."""
+    if pre is None:
+        return None, _lib.PRECOND_FN()
+    if sps.issparse(pre) and not hasattr(pre, "solve"):
+        dm = device_matrix(pre, ctx=ctx)
+        keep.append(dm)
+        return dm.handle.value, _lib.PRECOND_FN()
+    if hasattr(pre, "solve"):
+        apply = pre.solve
+    else:
+        def apply(vec):
+            try:
+                out = pre @ vec
+            except Exception:
+                raise ValueError("Preconditioner not supported")
+            return out
+
+    err = []
+
+    def cb(_user, q_ptr, z_ptr, nn):
+        try:
+            q = np.ctypeslib.as_array(q_ptr, shape=(nn,)).copy()
+            z = np.asarray(apply(q), dtype=np.float64).reshape(-1)
+            np.ctypeslib.as_array(z_ptr, shape=(nn,))[:] = z
+            return 0
+        except Exception as e:  # re-raised after the C call returns
+            err.append(e)
+            return 1
+
+    fn = _lib.PRECOND_FN(cb)
+    keep.append(fn)
+    keep.append(err)
+    return None, fn
+
+
+# ------------------------------------------------------------------------------------------------
+# dict-form constraints: constrained LS on the host through a callback
+# ------------------------------------------------------------------------------------------------
+def _make_conls(conlist, x0_host, n, timing, method, ctx, keep):
+    ctol = 1e-12
+    err = []
+
+    def cb(_user, ws, j, p, H_ptr, beta, y0_ptr, y_ptr, br_ptr, ev_ptr, msg_ptr):
+        try:
+            H = np.ctypeslib.as_array(H_ptr, shape=(p * (p + 1),)).reshape(p, p + 1).T.copy()
+            y0 = np.ctypeslib.as_array(y0_ptr, shape=(p,)).copy()
+            res = np.zeros(p + 1)
+            res[0] = beta
+
+            def func(z):
+                F = res - H @ z
+                return np.inner(F, F)
+
+            def jac(z):
+                F = res - H @ z
+                return -2 * np.transpose(H) @ F
+
+            Zrows = np.empty((p, n))
+            _lib.check(ctx.L.spis_workspace_basis(C.c_void_p(ws), p, Zrows.ctypes.data_as(C.POINTER(C.c_double))),
+                       "spis_workspace_basis")
+            Z = np.transpose(Zrows)
+            events = 0
+            branch = _lib.BRANCH_CON
+            if method == _lib.CGMRES_P:
+                clist = [_as_slsqp(constraint_container(c, x0_host, Z)) for c in conlist]
+                sol = spo.minimize(func, y0, tol=1e-15, jac=jac, constraints=clist[:j], method="SLSQP",
+                                   options={"ftol": 1e-20, "maxiter": 1e3})
+                if np.isnan(max(sol.x)):
+                    branch, events = _lib.BRANCH_FALLBACK, _lib.EV_NAN | _lib.EV_FALLBACK
+            else:
+                try:
+                    clist = [_as_slsqp(constraint_container(c, x0_host, Z)) for c in conlist]
+                    sol = spo.minimize(func, y0, tol=None, jac=jac, constraints=clist[:], method="SLSQP",
+                                       options={"ftol": ctol ** 2, "maxiter": 1e3})
+                    if not timing and np.isnan(max(sol.x)):
+                        events |= _lib.EV_NAN
+                        raise ValueError
+                    if not timing and constraint_checker(sol.x, clist) > ctol:
+                        events |= _lib.EV_VIOLATION
+                        raise AttributeError("constr_violation")
+                except Exception:
+                    branch = _lib.BRANCH_FALLBACK
+                    events |= _lib.EV_FALLBACK
+            if branch == _lib.BRANCH_CON:
+                np.ctypeslib.as_array(y_ptr, shape=(p,))[:] = sol.x
+                if sol.message not in _ACCEPTED:
+                    events |= _lib.EV_LS_MESSAGE
+                    _SLSQP_MESSAGES[(id(ctx), j)] = str(sol.message)
+            br_ptr[0] = branch
+            ev_ptr[0] = events
+            msg_ptr[0] = 0
+            return 0
+        except Exception as e:
+            err.append(e)
+            return 1
+
+    fn = _lib.CONLS_FN(cb)
+    keep.append(fn)
+    keep.append(err)
+    return fn
+
+
+_SLSQP_MESSAGES: dict = {}
+
+
+def _as_slsqp(cc):
+    return {"type": "eq", "fun": cc.constraint_func, "jac": cc.constraint_jac}
+
+
+# ------------------------------------------------------------------------------------------------
+# the call
+# ------------------------------------------------------------------------------------------------
+def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
+    ctx = get_context()
+    Ad = device_matrix(A, ctx=ctx)
+    n = Ad.shape[0]
+    device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
+    bd = device_vector(b, ctx=ctx)
+    x0d = device_vector(x0, ctx=ctx)
+    if len(bd) != n or len(x0d) != n:
+        raise ValueError(f"b/x0 length ({len(bd)}, {len(x0d)}) does not match A ({n})")
+    k = int(k)
+    if k < 1:
+        raise ValueError("k must be >= 1")
+    keep = []
+    pre_mat, pre_fn = _precond_setup(pre, n, ctx, keep)
+    conlist = list(conlist)
+    descs = None
+    conls = _lib.CONLS_FN()
+    if conlist:
+        kinds = ["class" if hasattr(c, "__dict__") else "dict" if type(c) is dict else "bad" for c in conlist]
+        if all(kd == "class" for kd in kinds):
+            arr = (_lib.ConstraintDesc * len(conlist))()
+            for i, c in enumerate(conlist):
+                arr[i], kp = _constraint_desc(c, n, ctx)
+                keep.extend(kp)
+            descs = arr
+        elif "bad" in kinds and method == _lib.CGMRES_P:
+            raise NotImplementedError("Constraints must be either dictionaries or classes")
+        else:
+            x0_host = np.asarray(x0d.numpy() if isinstance(x0, DeviceVector) else x0, dtype=np.float64)
+            conls = _make_conls(conlist, x0_host, n, timing, method, ctx, keep)
+    opts = _lib.SolveOpts(
+        method=method, k=k, tol=float(tol), contol=float(contol), timing=1 if timing else 0,
+        n_constraints=len(conlist), constraints=descs, pre_matrix=pre_mat, pre_fn=pre_fn, pre_user=None,
+        conls_fn=conls, conls_user=None,
+    )
+    res = np.zeros(k + 1)
+    ys = np.zeros(k * k)
+    br = np.zeros(k, dtype=np.int32)
+    ev = np.zeros(k, dtype=np.int32)
+    msg = np.zeros(k, dtype=np.int32)
+    stamps = np.zeros(4 * k + 2)
+    xf = DeviceVector(ctx, n)
+    out = _lib.SolveOut(
+        steps=0, n_res=0, res_host=res.ctypes.data_as(C.POINTER(C.c_double)),
+        y_host=ys.ctypes.data_as(C.POINTER(C.c_double)), branch_host=br.ctypes.data_as(C.POINTER(C.c_int32)),
+        events_host=ev.ctypes.data_as(C.POINTER(C.c_int32)), msg_host=msg.ctypes.data_as(C.POINTER(C.c_int32)),
+        stamps_host=stamps.ctypes.data_as(C.POINTER(C.c_double)), x_final_dev=xf.ptr,
+    )
+    ws = C.c_void_p()
+    status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
+                              C.byref(out), C.byref(ws))
+    for item in keep:  # a Python exception inside a callback is re-raised as itself
+        if isinstance(item, list) and item:
+            raise item[0]
+    _lib.check(status, "spis_solve")
+    n_iter = out.n_res - 1
+    final = xf if device_io else xf.numpy()
+    xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
+    names = {_lib.BRANCH_UNCON: "uncon", _lib.BRANCH_CON: "con", _lib.BRANCH_FALLBACK: "fallback"}
+    xs.trace = [(j, names[int(br[j])]) for j in range(n_iter)]  # branch per LS step (tests, diagnostics)
+    xs.events = ev[: max(n_iter, out.steps)].copy()
+    xs.y = [ys[j * k: j * k + j + 1].copy() for j in range(n_iter)]
+    return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
+                stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)
+
+
+def _replay_warnings(r, method, timing):
+    """Re-emit, in iteration order, the warnings the reference raises."""
+    n_it = max(r["n_iter"], r["steps"])
+    for j in range(min(n_it, len(r["events"]))):
+        e = int(r["events"][j])
+        if e & _lib.EV_FALLBACK:
+            if method == _lib.CGMRES_P:
+                log.warning("Constrained solve silently failed on iteration %d" % j)
+            else:
+                log.warning("Constrained solve failed, defaulted to standard solve for iteration %d." % j
+                            + " Problem likely overconstrained, a smaller solver tolerance may be required.")
+        if e & _lib.EV_LS_MESSAGE:
+            text = _SLSQP_MESSAGES.pop((id(r["ctx"]), j), None) or _lib.MESSAGES.get(int(r["msg"][j]), "failure")
+            warnings.warn("Iteration %d failed with message '%s'" % (j, text), RuntimeWarning)
+        if e & _lib.EV_BREAKDOWN:
+            warnings.warn("GMRES broke down, either initial guess is exact or" + " , more likely, something has gone wrong.")
+
+
+def _timings(r, k):
+    """Rebuild the reference's timings dict (solvers.py:300-312) from the stamps."""
+    st = r["stamps"]
+    n_it = r["n_iter"]
+    start, end = st[:k][:n_it], st[k:2 * k][:n_it]
+    con_mask = r["branch"][:n_it] != _lib.BRANCH_UNCON
+    cs = int(np.count_nonzero(con_mask))
+    iter_time = np.asarray(end) - np.asarray(start)
+    iter_unconstrained = iter_time[:-cs]
+    assembly = (st[3 * k:4 * k] - st[2 * k:3 * k])[:n_it][con_mask]
+    iter_constrained = iter_time[len(iter_unconstrained):] - assembly
+    return {
+        "runtime": float(st[4 * k + 1] - st[4 * k]),
+        "iter_time_unconstrained": np.mean(iter_unconstrained),
+        "iter_time_constrained": np.mean(iter_constrained),
+        "constraint_building": np.mean(assembly),
+        "constrained_steps": cs,
+    }
+
+
+def gmres(A, b, x0, k, tol=1e-50, pre=None):
+    """FGMRES, ``solvers.py:58-127``."""
+    r = _run(_lib.GMRES, A, b, x0, k, tol, 10, [], pre, None)
+    _replay_warnings(r, _lib.GMRES, None)
+    d = {"name": "gmres", "x": r["x"], "res": list(r["res"][1:]), "steps": r["steps"]}
+    return r["final"], d
+
+
+def cgmres(A, b, x0, k, tol=1e-8, contol=10, conlist=[], pre=None, timing=None):
+    """Constrained FGMRES, ``solvers.py:131-323``."""
+    r = _run(_lib.CGMRES, A, b, x0, k, tol, contol, conlist, pre, timing)
+    _replay_warnings(r, _lib.CGMRES, timing)
+    timings = _timings(r, int(k)) if timing else None
+    d = {"name": "cgmres", "x": r["x"], "res": list(r["res"][1:]), "steps": r["steps"], "timings": timings}
+    return r["final"], d
+
+
+def cgmres_p(A, b, x0, k, conlist=[], pre=None):
+    """Prototypical CGMRES, ``solvers.py:328-445`` (constraint i enforced from step i)."""
+    r = _run(_lib.CGMRES_P, A, b, x0, k, 1e-15, 10, conlist, pre, None)
+    _replay_warnings(r, _lib.CGMRES_P, None)
+    d = {"name": "geosolve", "x": r["x"], "res": list(r["res"][1:])}
+    return r["final"], d

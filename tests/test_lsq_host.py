@@ -1,0 +1,121 @@
+"""Host small-LS (csrc/lsq.cpp, via the host-only liblsq_host.so) against the
+reference's own least-squares solutions: for every golden cgmres run, the
+oracle (bit-exact with the reference) rebuilds H and the constraint terms of
+each iteration, and the Givens / Newton-KKT solutions are compared with the
+``y`` the reference's SLSQP returned (logged in the fixture)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from _golden import Case, names
+from oracle.cgmres_port import ConstraintTerms, _Arnoldi
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "structurepreservingiterativesolvers_amd", "liblsq_host.so")
+PD = C.POINTER(C.c_double)
+
+
+@pytest.fixture(scope="module")
+def lsq():
+    if not os.path.exists(LIB):
+        pytest.skip("liblsq_host.so not built (make)")
+    L = C.CDLL(LIB)
+    L.lsq_givens_solve.argtypes = [C.c_int, PD, C.c_double, PD]
+    L.lsq_kkt_solve.argtypes = [C.c_int, PD, C.c_double, C.c_int, PD, PD, PD, PD, PD, C.POINTER(C.c_int),
+                                C.POINTER(C.c_int)]
+    L.lsq_con_value.argtypes = [C.c_int, C.c_double, PD, PD, PD]
+    L.lsq_con_value.restype = C.c_double
+    return L
+
+
+def _p(a):
+    return np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(PD)
+
+
+def givens(L, Hj, beta):
+    p = Hj.shape[1]
+    y = np.zeros(p)
+    Hc = np.asfortranarray(Hj)
+    L.lsq_givens_solve(p, Hc.ctypes.data_as(PD), beta, y.ctypes.data_as(PD))
+    return y
+
+
+def kkt(L, Hj, beta, terms, y0):
+    p = Hj.shape[1]
+    m = len(terms)
+    t0 = np.array([t[0] for t in terms])
+    t1 = np.concatenate([t[1] for t in terms]) if m else np.zeros(1)
+    t2 = np.concatenate([np.ascontiguousarray(t[2]).ravel() for t in terms]) if m else np.zeros(1)
+    y = np.zeros(p)
+    msg, it = C.c_int(), C.c_int()
+    Hc = np.asfortranarray(Hj)
+    L.lsq_kkt_solve(p, Hc.ctypes.data_as(PD), beta, m, _p(t0), _p(t1), _p(t2), _p(y0), y.ctypes.data_as(PD),
+                    C.byref(msg), C.byref(it))
+    return y, msg.value, it.value
+
+
+CGMRES_CASES = [n for n in names() if Case(n).solver == "cgmres" and Case(n).meta["problem"] not in ("lkdvRK", "edge")]
+
+
+@pytest.mark.parametrize("name", CGMRES_CASES)
+def test_givens_and_kkt_match_reference_slsqp(lsq, name):
+    case = Case(name)
+    st = _Arnoldi(case.A, case.b, case.x0, case.k, case.preconditioner())
+    cons = case.conlist()
+    j = -1
+    prev_y = None
+    checked = 0
+    for i, (p, nc, msg) in enumerate(zip(case.calls_p, case.calls_ncons, case.calls_msg)):
+        while j < p - 1:
+            j += 1
+            st.extend(j)
+        Hj = st.H[: p + 1, :p]
+        yref = case.calls_y[i, :p]
+        scale = max(1.0, np.abs(yref).max())
+        if nc == 0:
+            y = givens(lsq, Hj, st.beta)
+            # SLSQP stops at ftol=1e-24 on ||.||^2: early iterates agree to ~1e-10
+            assert np.abs(y - yref).max() <= 1e-7 * scale, (j, np.abs(y - yref).max())
+        else:
+            Z = st.basis(p - 1)
+            terms = []
+            for c in cons:
+                t = ConstraintTerms(c, case.x0, Z)
+                terms.append((t.term0, t.term1, t.term2))
+            y0 = np.zeros(p)
+            if prev_y is not None:
+                y0[:-1] = prev_y[: p - 1]
+            y, m, it = kkt(lsq, Hj, st.beta, terms, y0)
+            if msg == "More equality constraints than independent variables":
+                assert m == 2 and np.array_equal(y, y0)
+            elif msg == "Optimization terminated successfully":
+                assert m == 0, (j, m)
+                assert np.abs(y - yref).max() <= 1e-8 * scale, (j, np.abs(y - yref).max())
+                # signed checker passes (solvers.py:267): computed values <= ctol
+                for t0, t1, t2 in terms:
+                    assert lsq.lsq_con_value(p, t0, _p(t1), _p(t2), _p(y)) <= 1e-12
+        prev_y = yref
+        checked += 1
+    assert checked > 0
+
+
+def test_givens_matches_lstsq_random(lsq):
+    rng = np.random.default_rng(0)
+    for p in (1, 2, 5, 17, 40):
+        H = np.triu(rng.normal(size=(p + 1, p)), -1) + 4.0 * np.eye(p + 1, p)
+        beta = 3.0
+        rhs = np.zeros(p + 1)
+        rhs[0] = beta
+        y = givens(lsq, H, beta)
+        yref = np.linalg.lstsq(H, rhs, rcond=None)[0]
+        np.testing.assert_allclose(y, yref, rtol=1e-10, atol=1e-12)
+
+
+def test_kkt_overconstrained_returns_initial_guess(lsq):
+    """SLSQP exit mode 2 (m > p) leaves x at the initial guess (fixture lkdv_m50_overconstrained)."""
+    H = np.array([[2.0], [1.0]])
+    terms = [(1.0, np.array([1.0]), np.array([[0.0]]))] * 2
+    y, msg, _ = kkt(lsq, H, 1.0, terms, np.array([0.25]))
+    assert msg == 2 and y[0] == 0.25
