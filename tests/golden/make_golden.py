@@ -107,7 +107,40 @@ def _run(case, fn):
     return x, d, list(FD_WARNINGS), [str(w.message) for w in caught], list(CALLS)
 
 
-def _save(name, meta, inputs, x, d, fdw, pyw, calls):
+def _sensitivity(name, dic, fn, d0, seeds=(1, 2, 3)):
+    """The reference's own roundoff envelope: rerun it with b perturbed by a relative
+    1e-16 (per entry, seeded) and record, per iterate, the largest relative change of x
+    and the largest change of the residual history.  The GPU parity test allows 10x this
+    envelope (floor 1e-8): a different summation order in the dot products is exactly
+    such a perturbation."""
+    x_ref = np.asarray(d0["x"])
+    r_ref = np.asarray(d0["res"])
+    xs = np.zeros(len(x_ref))
+    rs = np.zeros(len(r_ref))
+    steps = [int(d0.get("steps", -1))]
+    b0 = dic["b"]
+    for seed in seeds:
+        rng = np.random.default_rng(1000 + seed)
+        dic["b"] = b0 * (1.0 + 1e-16 * rng.standard_normal(b0.shape))
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                FD_WARNINGS.clear()
+                _, d = fn(dic)
+        finally:
+            dic["b"] = b0
+        xp = np.asarray(d["x"])
+        rp = np.asarray(d["res"])
+        steps.append(int(d.get("steps", -1)))
+        for i in range(min(len(xp), len(x_ref))):
+            den = max(np.linalg.norm(x_ref[i]), 1e-300)
+            xs[i] = max(xs[i], np.linalg.norm(xp[i] - x_ref[i]) / den)
+        for i in range(min(len(rp), len(r_ref))):
+            rs[i] = max(rs[i], abs(rp[i] - r_ref[i]))
+    return {"x_sens": xs, "res_sens": rs, "sens_steps": np.array(steps, dtype=np.int32)}
+
+
+def _save(name, meta, inputs, x, d, fdw, pyw, calls, sens):
     xs = np.asarray(d["x"])
     k = max([c[0] for c in calls], default=1)
     ylog = np.full((len(calls), k), np.nan)
@@ -127,6 +160,7 @@ def _save(name, meta, inputs, x, d, fdw, pyw, calls):
         fd_warnings=np.array(fdw, dtype=object).astype(str) if fdw else np.array([], dtype="<U1"),
         py_warnings=np.array(pyw, dtype=object).astype(str) if pyw else np.array([], dtype="<U1"),
         meta=np.array(repr(meta)),
+        **sens,
     )
     if d.get("timings") is not None:
         out["timing_keys"] = np.array(sorted(d["timings"].keys()))
@@ -134,7 +168,8 @@ def _save(name, meta, inputs, x, d, fdw, pyw, calls):
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **out)
     print(f"{name:28s} N={len(inputs['b']):6d} steps={d.get('steps', '-')!s:>3} res[-1]={(d['res'][-1] if len(d['res']) else float('nan')):.3e} "
-          f"calls={len(calls)} fdw={len(fdw)} pyw={len(pyw)} {os.path.getsize(path) / 1024:.0f} KB")
+          f"calls={len(calls)} fdw={len(fdw)} pyw={len(pyw)} sens={sens['x_sens'].max():.1e} "
+          f"steps={list(sens['sens_steps'])} {os.path.getsize(path) / 1024:.0f} KB")
 
 
 def main():
@@ -145,60 +180,60 @@ def main():
     dh, _ = heat_asm.linforms(M=31)
     x0 = np.zeros_like(dh["b"])
     cases.append(("heat_c1_cgmres", dict(problem="heat", M=31, solver="cgmres", k=50, tol=1e-19), dh, x0,
-                  lambda: W["heat"].cgmresWrapper(dh, x0=x0, k=50, tol=1e-19)))
+                  lambda D: W["heat"].cgmresWrapper(D, x0=x0, k=50, tol=1e-19)))
     cases.append(("heat_c1_gmres", dict(problem="heat", M=31, solver="gmres", k=50, tol=1e-50), dh, x0,
-                  lambda: W["heat"].gmresWrapper(dh, x0=x0, k=50)))
+                  lambda D: W["heat"].gmresWrapper(D, x0=x0, k=50)))
     dh15, _ = heat_asm.linforms(M=15)
     x015 = np.zeros_like(dh15["b"])
     cases.append(("heat_m15_cgmres_p", dict(problem="heat", M=15, solver="cgmres_p", k=20, tol=1e-50), dh15, x015,
-                  lambda: W["heat"].cgmresWrapper(dh15, x0=x015, k=20, tol=1e-50)))
+                  lambda D: W["heat"].cgmresWrapper(D, x0=x015, k=20, tol=1e-50)))
     cases.append(("heat_m15_cgmres_tol1e-3", dict(problem="heat", M=15, solver="cgmres", k=40, tol=1e-3), dh15,
-                  x015, lambda: W["heat"].cgmresWrapper(dh15, x0=x015, k=40, tol=1e-3)))
+                  x015, lambda D: W["heat"].cgmresWrapper(D, x0=x015, k=40, tol=1e-3)))
 
     # ---- lkdv (3 constraints) -----------------------------------------------------
     dl, _ = lkdv_asm.linforms(M=50)
     xl = np.zeros_like(dl["b"])
     cases.append(("lkdv_m50_cgmres_tol1e-6", dict(problem="lkdv", M=50, solver="cgmres", k=30, tol=1e-6), dl, xl,
-                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=30, tol=1e-6)))
+                  lambda D: W["lkdv"].cgmresWrapper(D, x0=xl, k=30, tol=1e-6)))
     cases.append(("lkdv_m50_cgmres_tol1e-19", dict(problem="lkdv", M=50, solver="cgmres", k=30, tol=1e-19), dl,
-                  xl, lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=30, tol=1e-19)))
+                  xl, lambda D: W["lkdv"].cgmresWrapper(D, x0=xl, k=30, tol=1e-19)))
     cases.append(("lkdv_m50_cgmres_p", dict(problem="lkdv", M=50, solver="cgmres_p", k=12, tol=1e-50), dl, xl,
-                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=12, tol=1e-50)))
+                  lambda D: W["lkdv"].cgmresWrapper(D, x0=xl, k=12, tol=1e-50)))
     cases.append(("lkdv_m50_gmres", dict(problem="lkdv", M=50, solver="gmres", k=30, tol=1e-10), dl, xl,
-                  lambda: W["lkdv"].gmresWrapper(dl, x0=xl, k=30, tol=1e-10)))
+                  lambda D: W["lkdv"].gmresWrapper(D, x0=xl, k=30, tol=1e-10)))
     # overconstrained terminal step: p = 2 < 3 constraints -> failure/fallback path
     cases.append(("lkdv_m50_overconstrained", dict(problem="lkdv", M=50, solver="cgmres", k=2, tol=1e-6), dl, xl,
-                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=2, tol=1e-6)))
+                  lambda D: W["lkdv"].cgmresWrapper(D, x0=xl, k=2, tol=1e-6)))
     # left-behind rare path: contol so large that constraints are enforced from j = 0
     cases.append(("lkdv_m50_contol_big", dict(problem="lkdv", M=50, solver="cgmres", k=8, tol=1e-6,
                                               contol=1e12), dl, xl,
-                  lambda: W["lkdv"].cgmresWrapper(dl, x0=xl, k=8, tol=1e-6, contol=1e12)))
+                  lambda D: W["lkdv"].cgmresWrapper(D, x0=xl, k=8, tol=1e-6, contol=1e12)))
     ilu = spla.spilu(dl["A"].tocsc(), drop_tol=1e-2, fill_factor=10)
     cases.append(("lkdv_m50_gmres_spilu", dict(problem="lkdv", M=50, solver="gmres", k=10, tol=1e-12, pre="spilu"),
-                  dl, xl, lambda: solvers.gmres(dl["A"], dl["b"], xl, 10, tol=1e-12, pre=ilu)))
+                  dl, xl, lambda D: solvers.gmres(D["A"], D["b"], xl, 10, tol=1e-12, pre=ilu)))
 
     # ---- swe (2 constraints; + synthetic third) -----------------------------------
     ds, _ = swe_asm.linforms(M=8)
     xs0 = np.zeros_like(ds["b"])
     cases.append(("swe_m8_cgmres_tol1e-19", dict(problem="swe", M=8, solver="cgmres", k=30, tol=1e-19), ds, xs0,
-                  lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=30, tol=1e-19)))
+                  lambda D: W["swe"].cgmresWrapper(D, x0=xs0, k=30, tol=1e-19)))
     cases.append(("swe_m8_cgmres_tol1e-7", dict(problem="swe", M=8, solver="cgmres", k=30, tol=1e-7), ds, xs0,
-                  lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=30, tol=1e-7)))
+                  lambda D: W["swe"].cgmresWrapper(D, x0=xs0, k=30, tol=1e-7)))
     cases.append(("swe_m8_gmres", dict(problem="swe", M=8, solver="gmres", k=30, tol=1e-50), ds, xs0,
-                  lambda: W["swe"].gmresWrapper(ds, x0=xs0, k=30)))
+                  lambda D: W["swe"].gmresWrapper(D, x0=xs0, k=30)))
     ds6, _ = swe_asm.linforms(M=6)
     x6 = np.zeros_like(ds6["b"])
     cases.append(("swe_m6_cgmres_p", dict(problem="swe", M=6, solver="cgmres_p", k=15, tol=1e-50), ds6, x6,
-                  lambda: W["swe"].cgmresWrapper(ds6, x0=x6, k=15, tol=1e-50)))
+                  lambda D: W["swe"].cgmresWrapper(D, x0=x6, k=15, tol=1e-50)))
     cases.append(("swe_m8_cgmres_timing", dict(problem="swe", M=8, solver="cgmres", k=12, tol=1e-7, timing=True),
-                  ds, xs0, lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=12, tol=1e-7, timing=True)))
+                  ds, xs0, lambda D: W["swe"].cgmresWrapper(D, x0=xs0, k=12, tol=1e-7, timing=True)))
     jac = sps.diags(1.0 / ds["A"].diagonal(), format="csr")
     cases.append(("swe_m8_cgmres_jacobi", dict(problem="swe", M=8, solver="cgmres", k=20, tol=1e-19, pre="jacobi"),
-                  ds, xs0, lambda: W["swe"].cgmresWrapper(ds, x0=xs0, k=20, tol=1e-19, pre=jac)))
+                  ds, xs0, lambda D: W["swe"].cgmresWrapper(D, x0=xs0, k=20, tol=1e-19, pre=jac)))
     rng = np.random.default_rng(5)
     xr = rng.normal(size=ds["b"].shape)
     cases.append(("swe_m8_cgmres_x0", dict(problem="swe", M=8, solver="cgmres", k=20, tol=1e-19, x0="random5"),
-                  ds, xr, lambda: W["swe"].cgmresWrapper(ds, x0=xr, k=20, tol=1e-19)))
+                  ds, xr, lambda D: W["swe"].cgmresWrapper(D, x0=xr, k=20, tol=1e-19)))
     D3, c3 = swe_asm.extra_constraint(len(ds["b"]), ds["z0"], seed=2)
 
     class _Mass:
@@ -217,10 +252,10 @@ def main():
     ds3["D3"] = D3
     ds3["c3"] = c3
     cases.append(("swe_m8_cgmres_3cons", dict(problem="swe3", M=8, solver="cgmres", k=30, tol=1e-19), ds3, xs0,
-                  lambda: solvers.cgmres(ds["A"], ds["b"], xs0, 30, tol=1e-19,
+                  lambda D: solvers.cgmres(D["A"], D["b"], xs0, 30, tol=1e-19,
                                          conlist=[_Mass(), _Energy(), _Extra()])))
     cases.append(("swe_m8_cgmres_nocons", dict(problem="swe", M=8, solver="cgmres", k=15, tol=1e-19, cons="none"),
-                  ds, xs0, lambda: solvers.cgmres(ds["A"], ds["b"], xs0, 15, tol=1e-19, conlist=[])))
+                  ds, xs0, lambda D: solvers.cgmres(D["A"], D["b"], xs0, 15, tol=1e-19, conlist=[])))
 
     # ---- lkdvRK (dict-form constraints through the reference wrapper) --------------
     dr, pr = rk_asm.linforms(M=20, tstages=2)
@@ -229,10 +264,10 @@ def main():
     drk["dt"] = pr.dt
     drk["butcher_b"] = pr.butcher_tableau.b
     cases.append(("lkdvrk_m20_s2_cgmres", dict(problem="lkdvRK", M=20, s=2, solver="cgmres", k=30, tol=1e-6),
-                  drk, xr0, lambda: W["lkdvRK"].cgmresWrapper(dr, x0=xr0, k=30, prob=pr, tol=1e-6)))
+                  drk, xr0, lambda D: W["lkdvRK"].cgmresWrapper(D, x0=xr0, k=30, prob=pr, tol=1e-6)))
     cases.append(("lkdvrk_m20_s2_cgmres_tight", dict(problem="lkdvRK", M=20, s=2, solver="cgmres", k=25,
                                                      tol=1e-19), drk, xr0,
-                  lambda: W["lkdvRK"].cgmresWrapper(dr, x0=xr0, k=25, prob=pr, tol=1e-19)))
+                  lambda D: W["lkdvRK"].cgmresWrapper(D, x0=xr0, k=25, prob=pr, tol=1e-19)))
 
     # ---- edge: exact breakdown at j = 0 (returns r0 as the "solution") -------------
     n = 64
@@ -243,16 +278,17 @@ def main():
     dbk = {"A": A2, "b": e0v}
     xb = np.zeros(n)
     cases.append(("edge_breakdown_cgmres", dict(problem="edge", solver="cgmres", k=5, tol=1e-8, cons="none"), dbk,
-                  xb, lambda: solvers.cgmres(A2, e0v, xb, 5, tol=1e-8, conlist=[])))
+                  xb, lambda D: solvers.cgmres(D["A"], D["b"], xb, 5, tol=1e-8, conlist=[])))
     cases.append(("edge_breakdown_gmres", dict(problem="edge", solver="gmres", k=5, tol=1e-50), dbk, xb,
-                  lambda: solvers.gmres(A2, e0v, xb, 5)))
+                  lambda D: solvers.gmres(D["A"], D["b"], xb, 5)))
 
     for name, meta, dic, x0c, fn in cases:
         inputs = _dic_fields(dic)
         inputs["b"] = np.asarray(dic["b"])
         inputs["x0"] = x0c
-        x, d, fdw, pyw, calls = _run(name, fn)
-        _save(name, meta, inputs, x, d, fdw, pyw, calls)
+        x, d, fdw, pyw, calls = _run(name, lambda: fn(dic))
+        sens = _sensitivity(name, dic, fn, d)
+        _save(name, meta, inputs, x, d, fdw, pyw, calls, sens)
 
 
 if __name__ == "__main__":

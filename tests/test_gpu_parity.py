@@ -5,11 +5,15 @@ Tolerances (fp64):
 * SpMV: bit-exact vs SciPy ``A @ x`` (rows <= 2048 nnz), since the kernel sums
   the rounded products of each row left to right as ``csr_matvec`` does;
 * MGS ``y - h q``: bit-exact vs NumPy; dots / norms / GEMV / Gram: 1e-13 rel;
-* solver iterates: ||x_i - x_i^ref|| <= 1e-8 ||x_i^ref|| (reference LS is SLSQP
-  to ftol 1e-24, ours is exact Givens / Newton-KKT: early iterates differ by
-  <= ~1e-10 rel); residual history: |r - r_ref| <= 1e-8 r_0 +
-  1e-6 r_ref; steps, branch sequence and warnings identical except where the
-  reference's SLSQP itself failed numerically (listed per case below);
+* solver iterates: ||x_i - x_i^ref|| <= max(1e-8, 10 s_i) ||x_i^ref||, where s_i is
+  the reference's OWN roundoff envelope at iterate i — the largest relative change
+  of its x_i when b is perturbed by 1e-16 (3 seeds, recorded in the fixture by
+  make_golden.py).  A different summation order of the dots is such a
+  perturbation; on the roundoff-sensitive KdV problems s_i reaches 3e-7 (lkdv)
+  and 3.5e-3 (lkdvRK), on swe/heat 1e-15..1e-8.  Residual history:
+  |r_i - r_i^ref| <= 1e-10 r_0 + 1e-8 r_i^ref + 10 rs_i (rs_i the same envelope);
+  steps, branch sequence and warnings identical except where the reference's
+  SLSQP itself failed numerically (listed per case below);
 * constraint deviation of the CGMRES solution: |c_i(x)| <= 1e-12 * scale.
 """
 import logging
@@ -169,19 +173,21 @@ def test_golden(spis, name, caplog):
         assert len(xs) == len(ref), (len(xs), len(ref))
         if "steps" in d:
             assert d["steps"] == case.steps
+    xsens = case.z["x_sens"]
+    rsens = case.z["res_sens"]
     for i in range(min(nx, len(xs))):
         scale = max(np.linalg.norm(ref[i]), 1e-300)
         err = np.linalg.norm(xs[i] - ref[i]) / scale
-        assert err <= 1e-8, (i, err)
+        assert err <= max(1e-8, 10 * xsens[i]), (i, err, xsens[i])
     res = np.asarray(d["res"])
     rres = case.res
     r0 = np.linalg.norm(case.b - case.A @ case.x0)
     nr = len(rres) if upto is None else min(len(rres), upto)
     for i in range(nr):
-        assert abs(res[i] - rres[i]) <= 1e-8 * r0 + 1e-6 * rres[i], (i, res[i], rres[i])
+        assert abs(res[i] - rres[i]) <= 1e-10 * r0 + 1e-8 * rres[i] + 10 * rsens[i], (i, res[i], rres[i])
     if upto is None:
         np.testing.assert_allclose(np.asarray(x), case.x_final, rtol=0,
-                                   atol=1e-8 * max(np.linalg.norm(case.x_final), 1e-300))
+                                   atol=max(1e-8, 10 * xsens[-1]) * max(np.linalg.norm(case.x_final), 1e-300))
         trace = d["x"].trace
         exp = expected_trace(case)
         if case.solver != "gmres":
@@ -205,7 +211,8 @@ def test_lkdvrk_dict_form_through_callback(spis):
     case = Case("lkdvrk_m20_s2_cgmres")
     x, d = rk_ls.cgmresWrapper(case.dic(), x0=case.x0, k=case.k, prob=case.prob(), tol=case.tol, lift=False)
     assert d["steps"] == case.steps
-    np.testing.assert_allclose(x, case.x_final, atol=1e-8 * np.linalg.norm(case.x_final))
+    tol = max(1e-8, 10 * case.z["x_sens"][-1])
+    np.testing.assert_allclose(x, case.x_final, atol=tol * np.linalg.norm(case.x_final))
 
 
 # ------------------------------------------------------------------------------------------------
