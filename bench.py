@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--tol", type=float, default=1e-19)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prof-period", type=int, default=5,
+                    help="time every n-th iteration's kernels with HIP events inside the timed region")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,7 +129,7 @@ def main():
     L = ctx.L
     import ctypes as C
 
-    _lib.check(L.spis_profile_enable(ctx.handle, 1), "spis_profile_enable")
+    _lib.check(L.spis_profile_enable(ctx.handle, args.prof_period), "spis_profile_enable")
     ctx.synchronize()
     t0 = time.perf_counter()
     iters = 0

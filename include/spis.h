@@ -94,10 +94,13 @@ int spis_context_synchronize(spis_context* ctx);
 int spis_context_stream(spis_context* ctx, void** stream_out);
 
 /* ---- live kernel timing ------------------------------------------------------
- * When enabled, spis_solve records HIP events on the context stream around the
- * Arnoldi SpMV, the MGS chain (+ normalise), the GEMV and the true-residual
- * SpMV of every iteration; totals (ms) and launch counts accumulate until the
- * next spis_profile_enable.  Used by bench.py for the roofline numbers. */
+ * spis_profile_enable(ctx, period): period > 0 makes spis_solve record HIP
+ * events on the context stream around the Arnoldi SpMV, the MGS chain
+ * (+ normalise), the GEMV and the true-residual SpMV of every period-th
+ * iteration (an event pair costs a few us of queue time, so bench.py samples);
+ * totals (ms) and launch counts accumulate until the next call.  period = 0
+ * disables; a negative value (tests) additionally routes the constraint
+ * reduction through the generic Gram path instead of the fused kernel. */
 enum spis_prof_kind {
   SPIS_PROF_SPMV = 0,      /* Arnoldi SpMV, solvers.py:191            */
   SPIS_PROF_MGS = 1,       /* MGS chain + normalise, :193-198          */

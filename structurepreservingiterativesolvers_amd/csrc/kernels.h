@@ -14,8 +14,14 @@ constexpr int kItemCap = 2048;   // merge items (rows + nnz) per row block
 constexpr int kSpmvGrid = 2048;  // max SpMV workgroups (= max epilogue partials)
 constexpr int kRedGrid = 1024;   // max BLAS-1 workgroups (= max reduction partials)
 constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's LDS copy of y
-constexpr int kGramChunk = 64;   // vector elements staged per Gram tile
-constexpr int kGramMaxVec = 72;  // max vectors on either side of a Gram product
+constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
+constexpr int kGramMaxVec = 64;  // max vectors on either side of one Gram launch (<= 256 4x4 tiles)
+constexpr int kYArg = 128;
+constexpr int kConGramGrid = 512;  // workgroups of the fused constraint Gram (4 waves each)       // GEMV coefficients passed by value up to this p
+
+struct YArg {
+  double v[kYArg];
+};
 
 // SpMV epilogues (fused into the row reduction of the same launch)
 enum Epilogue : int {
@@ -47,9 +53,21 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // h = sqrt(sum(part_in)); q_next = y / h (if h != 0)
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid);
-// x = Z[:, :p] y + x0
+// x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
-                       const double* x0, double* x, hipStream_t s);
+                       bool y_on_host, const double* x0, double* x, hipStream_t s);
+// W[c] = M Z[c] for c < nvec (vectors at stride ldx / ldy)
+hipError_t launch_spmm(const CsrView& A, const double* X, int64_t ldx, int nvec, double* Y,
+                       int64_t ldy, hipStream_t s);
+size_t gram_lds_bytes(int nu, int nv);
+// Ut (n x (p+1), row-major) = [Z[:, :p], x0]^T
+hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                  double* Ut, hipStream_t s);
+// G = [U^T M U | U^T v_0 .. U^T v_{nvv-1}] from Ut (M may be null: linear terms only);
+// partials: constraint_gram_waves() x (np1*np1 + nvv*np1) doubles
+int constraint_gram_waves();
+hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
+                                  const double* const* v, double* partials, double* G, hipStream_t s);
 // partial dot / sum of squares
 hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_out, int grid,
                       hipStream_t s);

@@ -155,17 +155,39 @@ __global__ __launch_bounds__(kBlock) void mgs_step_kernel(int64_t n, double* __r
                                                           double* __restrict__ h_out) {
 #pragma clang fp contract(off)
   __shared__ double s_wave[4];
-  const double h = sum_partials(part_in, n_in, s_wave);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
-  double part = 0.0;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  double part = 0.0;
   if (VEC) {
     const int64_t npair = n >> 1;
     double2* y2 = reinterpret_cast<double2*>(y);
     const double2* q2 = reinterpret_cast<const double2*>(qi);
     const double2* n2 = reinterpret_cast<const double2*>(qn);
-    for (int64_t p = tid; p < npair; p += stride) {
+    // issue this thread's first 16-B loads BEFORE the partial reduction (a barrier + a
+    // latency-bound read of n_in partials): the stream is in flight while h_i is formed
+    const bool have = tid < npair;
+    double2 yv0 = make_double2(0.0, 0.0), qv0 = yv0, nv0 = yv0;
+    if (have) {
+      qv0 = q2[tid];
+      yv0 = y2[tid];
+      if (qn) nv0 = n2[tid];
+    }
+    const double h = sum_partials(part_in, n_in, s_wave);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+    if (have) {
+      const double a0 = h * qv0.x, a1 = h * qv0.y;
+      yv0.x = yv0.x - a0;
+      yv0.y = yv0.y - a1;
+      y2[tid] = yv0;
+      if (qn) {
+        part += nv0.x * yv0.x;
+        part += nv0.y * yv0.y;
+      } else {
+        part += yv0.x * yv0.x;
+        part += yv0.y * yv0.y;
+      }
+    }
+    for (int64_t p = tid + stride; p < npair; p += stride) {
       const double2 qv = q2[p];
       double2 yv = y2[p];
       const double a0 = h * qv.x, a1 = h * qv.y;
@@ -189,6 +211,8 @@ __global__ __launch_bounds__(kBlock) void mgs_step_kernel(int64_t n, double* __r
       part += qn ? qn[e] * yv : yv * yv;
     }
   } else {
+    const double h = sum_partials(part_in, n_in, s_wave);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
     for (int64_t e = tid; e < n; e += stride) {
       const double a = h * qi[e];
       const double yv = y[e] - a;
@@ -240,19 +264,24 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4: x = Z[:, :p] y + x0 (solvers.py:287).  y is copied to LDS once per workgroup; each lane
-// streams one (VEC: two) element(s) of every basis vector.  Sum in basis order, then + x0.
+// K4: x = Z[:, :p] y + x0 (solvers.py:287).  For p <= kYArg the coefficients travel in the
+// kernel-argument segment (scalar loads, no H2D copy in front of the launch); otherwise they
+// are copied to LDS from a device buffer.  Each lane streams one (VEC: two) element(s) of every
+// basis vector; sum in basis order, then + x0 (numpy's ``Z @ yk + x0`` adds x0 afterwards).
 // ---------------------------------------------------------------------------------------------
-template <bool VEC>
+template <bool VEC, bool ARG>
 __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
                                                       const double* __restrict__ Z, int64_t pitch,
-                                                      const double* __restrict__ ycoef,
+                                                      YArg yarg, const double* __restrict__ ycoef,
                                                       const double* __restrict__ x0,
                                                       double* __restrict__ x) {
 #pragma clang fp contract(off)
-  __shared__ double s_y[kMaxK];
-  for (int i = threadIdx.x; i < p; i += kBlock) s_y[i] = ycoef[i];
-  __syncthreads();
+  __shared__ double s_y[ARG ? 1 : kMaxK];
+  if (!ARG) {
+    for (int i = threadIdx.x; i < p; i += kBlock) s_y[i] = ycoef[i];
+    __syncthreads();
+  }
+  const double* yc = ARG ? yarg.v : s_y;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (VEC) {
@@ -261,8 +290,9 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
       double a0 = 0.0, a1 = 0.0;
       for (int i = 0; i < p; ++i) {
         const double2 z = reinterpret_cast<const double2*>(Z + i * pitch)[q];
-        a0 += z.x * s_y[i];
-        a1 += z.y * s_y[i];
+        const double c = yc[i];
+        a0 += z.x * c;
+        a1 += z.y * c;
       }
       const double2 b = reinterpret_cast<const double2*>(x0)[q];
       reinterpret_cast<double2*>(x)[q] = make_double2(a0 + b.x, a1 + b.y);
@@ -270,29 +300,101 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
     if ((n & 1) && tid == 0) {
       const int64_t e = n - 1;
       double a = 0.0;
-      for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * s_y[i];
+      for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * yc[i];
       x[e] = a + x0[e];
     }
   } else {
     for (int64_t e = tid; e < n; e += stride) {
       double a = 0.0;
-      for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * s_y[i];
+      for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * yc[i];
       x[e] = a + x0[e];
     }
   }
 }
 
-hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
-                       const double* x0, double* x, hipStream_t s) {
-  if (p > kMaxK) return hipErrorInvalidValue;
+hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y_host_or_dev,
+                       bool y_on_host, const double* x0, double* x, hipStream_t s) {
+  if (p > kMaxK || p < 1) return hipErrorInvalidValue;
   const bool vec = aligned16(Z) && (pitch % 2 == 0) && aligned16(x0) && aligned16(x);
   int64_t g = (n / (vec ? 2 : 1) + kBlock - 1) / kBlock;
   if (g > 4 * kRedGrid) g = 4 * kRedGrid;
   if (g < 1) g = 1;
-  if (vec)
-    hipLaunchKernelGGL(gemv_kernel<true>, dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, y, x0, x);
+  YArg ya;
+  const bool arg = y_on_host && p <= kYArg;
+  if (y_on_host && !arg) return hipErrorInvalidValue;  // caller stages larger y in HBM
+  if (arg)
+    for (int i = 0; i < p; ++i) ya.v[i] = y_host_or_dev[i];
+  const double* yd = arg ? nullptr : y_host_or_dev;
+  if (vec && arg)
+    hipLaunchKernelGGL((gemv_kernel<true, true>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+  else if (vec)
+    hipLaunchKernelGGL((gemv_kernel<true, false>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+  else if (arg)
+    hipLaunchKernelGGL((gemv_kernel<false, true>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
   else
-    hipLaunchKernelGGL(gemv_kernel<false>, dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, y, x0, x);
+    hipLaunchKernelGGL((gemv_kernel<false, false>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5: multi-vector SpMV W[:, c] = M Z[:, c], c < nvec (constraint operators, solvers.py:33):
+// one launch for all basis vectors; the row block's values and columns are staged in LDS once
+// and reused for every vector.  Same product/sum order as K1 (bit-identical to SciPy per
+// column).  Long rows: workgroup reduction per vector.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void spmm_rowblock_kernel(
+    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
+    const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ X, int64_t ldx,
+    int nvec, double* __restrict__ Y, int64_t ldy) {
+  __shared__ double s_val[kNnzCap];
+  __shared__ int32_t s_col[kNnzCap];
+  __shared__ double s_prod[kNnzCap];
+  __shared__ double s_wave[4];
+  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int r0 = blk_row[blk];
+    const int r1 = blk_row[blk + 1];
+    const int nz0 = rp[r0];
+    const int nnz = rp[r1] - nz0;
+    if (nnz > kNnzCap) {
+      for (int c = 0; c < nvec; ++c) {
+        const double* xc = X + c * ldx;
+        double acc = 0.0;
+        for (int i = nz0 + threadIdx.x; i < nz0 + nnz; i += kBlock) acc += va[i] * xc[ci[i]];
+        const double sum = block_sum(acc, s_wave);
+        if (threadIdx.x == 0) Y[c * ldy + r0] = sum;
+      }
+      continue;
+    }
+    for (int i = threadIdx.x; i < nnz; i += kBlock) {
+      s_val[i] = va[nz0 + i];
+      s_col[i] = ci[nz0 + i];
+    }
+    __syncthreads();
+    const int r = r0 + threadIdx.x;
+    const int s0 = r < r1 ? rp[r] - nz0 : 0;
+    const int e0 = r < r1 ? rp[r + 1] - nz0 : 0;
+    for (int c = 0; c < nvec; ++c) {
+      const double* xc = X + c * ldx;
+#pragma unroll 4
+      for (int i = threadIdx.x; i < nnz; i += kBlock) s_prod[i] = s_val[i] * xc[s_col[i]];
+      __syncthreads();
+      if (r < r1) {
+        double sum = 0.0;
+        for (int t = s0; t < e0; ++t) sum += s_prod[t];
+        Y[c * ldy + r] = sum;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+hipError_t launch_spmm(const CsrView& A, const double* X, int64_t ldx, int nvec, double* Y,
+                       int64_t ldy, hipStream_t s) {
+  if (nvec <= 0) return hipSuccess;
+  int g = A.n_blk < kSpmvGrid ? A.n_blk : kSpmvGrid;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(spmm_rowblock_kernel, dim3(g), dim3(kBlock), 0, s, A.indptr, A.indices, A.vals,
+                     A.blk_row, A.n_blk, X, ldx, nvec, Y, ldy);
   return hipGetLastError();
 }
 
@@ -381,13 +483,17 @@ hipError_t launch_gather(int64_t m, const int32_t* idx, const double* x, double*
 }
 
 // ---------------------------------------------------------------------------------------------
-// K6: tall-skinny Gram G = U^T V (constraint terms, solvers.py:33-36).  Each workgroup stages
-// kGramChunk elements of all nu + nv vectors in LDS (rows padded by one to spread banks), every
-// thread owns up to kPairsPerThread (a, b) pairs in registers across its chunks; per-workgroup
-// partials are then summed in workgroup order by gram_reduce_kernel (deterministic).
+// K6: tall-skinny Gram G = U^T V (constraint terms, solvers.py:33-36; K = N is huge, nu, nv <=
+// kGramMaxVec).  Each workgroup stages kGramChunk elements of the nu + nv vectors in LDS (rows
+// padded to a multiple of 4 with zeros, leading dim kGramChunk + 1).  Thread t owns a 4 x 4
+// register tile of G (tile = t % ntiles) and the elements e = t / ntiles (mod ksplit) of every
+// chunk, so each 8 LDS reads feed 16 FMAs.  At the end the ksplit partial tiles are summed in
+// a fixed order through LDS and the workgroup's partial G is written; gram_reduce_kernel sums
+// the workgroup partials in workgroup order (4 waves x strided subsets, fixed combine):
+// deterministic, independent of placement.
 // ---------------------------------------------------------------------------------------------
-constexpr int kPairsPerThread = (kGramMaxVec * kGramMaxVec + kBlock - 1) / kBlock;
 constexpr int kGramLd = kGramChunk + 1;
+constexpr int kTile = 4;
 
 __global__ __launch_bounds__(kBlock) void gram_partial_kernel(int64_t n, int nu,
                                                               const double* const* __restrict__ U,
@@ -395,68 +501,224 @@ __global__ __launch_bounds__(kBlock) void gram_partial_kernel(int64_t n, int nu,
                                                               const double* const* __restrict__ V,
                                                               double* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nup = (nu + kTile - 1) / kTile * kTile;
+  const int nvp = (nv + kTile - 1) / kTile * kTile;
   double* sU = smem;
-  double* sV = smem + nu * kGramLd;
-  const int npairs = nu * nv;
-  double acc[kPairsPerThread];
+  double* sV = smem + nup * kGramLd;
+  const int ta = nup / kTile, tb = nvp / kTile, ntiles = ta * tb;
+  const int ksplit = kBlock / ntiles;  // >= 1 since ntiles <= 256
+  const int t = threadIdx.x;
+  const int tile = t % ntiles;
+  const int ks = t / ntiles;
+  const bool active = ks < ksplit;
+  const int a0 = (tile / tb) * kTile, b0 = (tile % tb) * kTile;
+  double acc[kTile][kTile];
 #pragma unroll
-  for (int t = 0; t < kPairsPerThread; ++t) acc[t] = 0.0;
-  const int nload = (nu + nv) * kGramChunk;
+  for (int i = 0; i < kTile; ++i)
+#pragma unroll
+    for (int j = 0; j < kTile; ++j) acc[i][j] = 0.0;
+  const int nload = (nup + nvp) * kGramChunk;
   for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * kGramChunk; c0 < n;
        c0 += static_cast<int64_t>(gridDim.x) * kGramChunk) {
-    for (int idx = threadIdx.x; idx < nload; idx += kBlock) {
+    for (int idx = t; idx < nload; idx += kBlock) {
       const int vec = idx / kGramChunk;
       const int e = idx - vec * kGramChunk;
       const int64_t g = c0 + e;
-      if (vec < nu)
-        sU[vec * kGramLd + e] = g < n ? U[vec][g] : 0.0;
+      if (vec < nup)
+        sU[vec * kGramLd + e] = (vec < nu && g < n) ? U[vec][g] : 0.0;
       else
-        sV[(vec - nu) * kGramLd + e] = g < n ? V[vec - nu][g] : 0.0;
+        sV[(vec - nup) * kGramLd + e] = (vec - nup < nv && g < n) ? V[vec - nup][g] : 0.0;
     }
     __syncthreads();
+    if (active) {
+      for (int e = ks; e < kGramChunk; e += ksplit) {
+        double u[kTile], v[kTile];
 #pragma unroll
-    for (int t = 0; t < kPairsPerThread; ++t) {
-      const int pr = threadIdx.x + t * kBlock;
-      if (pr < npairs) {
-        const int a = pr / nv;
-        const int b = pr - a * nv;
-        const double* ua = sU + a * kGramLd;
-        const double* vb = sV + b * kGramLd;
-        double s = 0.0;
-        for (int e = 0; e < kGramChunk; ++e) s += ua[e] * vb[e];
-        acc[t] += s;
+        for (int i = 0; i < kTile; ++i) u[i] = sU[(a0 + i) * kGramLd + e];
+#pragma unroll
+        for (int j = 0; j < kTile; ++j) v[j] = sV[(b0 + j) * kGramLd + e];
+#pragma unroll
+        for (int i = 0; i < kTile; ++i)
+#pragma unroll
+          for (int j = 0; j < kTile; ++j) acc[i][j] += u[i] * v[j];
       }
     }
     __syncthreads();
   }
+  // fixed-order reduction of the ksplit partial tiles: slot [ks][tile][16]
+  double* red = smem;
+  if (active)
 #pragma unroll
-  for (int t = 0; t < kPairsPerThread; ++t) {
-    const int pr = threadIdx.x + t * kBlock;
-    if (pr < npairs) partials[static_cast<int64_t>(blockIdx.x) * npairs + pr] = acc[t];
+    for (int i = 0; i < kTile; ++i)
+#pragma unroll
+      for (int j = 0; j < kTile; ++j) red[(ks * ntiles + tile) * 16 + i * kTile + j] = acc[i][j];
+  __syncthreads();
+  const int npairs = nu * nv;
+  for (int pr = t; pr < npairs; pr += kBlock) {
+    const int a = pr / nv, b = pr - (pr / nv) * nv;
+    const int tl = (a / kTile) * tb + (b / kTile);
+    const int slot = (a % kTile) * kTile + (b % kTile);
+    double sum = 0.0;
+    for (int k = 0; k < ksplit; ++k) sum += red[(k * ntiles + tl) * 16 + slot];
+    partials[static_cast<int64_t>(blockIdx.x) * npairs + pr] = sum;
   }
 }
 
 __global__ __launch_bounds__(kBlock) void gram_reduce_kernel(int npairs, int grid,
                                                              const double* __restrict__ partials,
                                                              double* __restrict__ G) {
-  const int pr = blockIdx.x * kBlock + threadIdx.x;
-  if (pr >= npairs) return;
+  __shared__ double s_acc[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pr = blockIdx.x * 64 + lane;
   double s = 0.0;
-  for (int b = 0; b < grid; ++b) s += partials[static_cast<int64_t>(b) * npairs + pr];
-  G[pr] = s;
+  if (pr < npairs) {
+#pragma unroll 8
+    for (int b = w; b < grid; b += 4) s += partials[static_cast<int64_t>(b) * npairs + pr];
+  }
+  s_acc[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && pr < npairs) G[pr] = ((s_acc[0][lane] + s_acc[1][lane]) + s_acc[2][lane]) + s_acc[3][lane];
+}
+
+size_t gram_lds_bytes(int nu, int nv) {
+  const int nup = (nu + kTile - 1) / kTile * kTile;
+  const int nvp = (nv + kTile - 1) / kTile * kTile;
+  const size_t tiles = static_cast<size_t>(nup + nvp) * kGramLd * sizeof(double);
+  const size_t red = static_cast<size_t>(kBlock) * 16 * sizeof(double);
+  return tiles > red ? tiles : red;
 }
 
 hipError_t launch_gram(int64_t n, int nu, const double* const* U, int nv, const double* const* V,
                        double* partials, int grid, double* G, hipStream_t s) {
   if (nu > kGramMaxVec || nv > kGramMaxVec || nu < 1 || nv < 1) return hipErrorInvalidValue;
-  const size_t lds = static_cast<size_t>(nu + nv) * kGramLd * sizeof(double);
-  hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(kBlock), lds, s, n, nu, U, nv, V,
-                     partials);
+  hipLaunchKernelGGL(gram_partial_kernel, dim3(grid), dim3(kBlock), gram_lds_bytes(nu, nv), s, n, nu, U,
+                     nv, V, partials);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int npairs = nu * nv;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     npairs, grid, partials, G);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs, grid,
+                     partials, G);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K7: fused constraint reduction (solvers.py:33-36 for all constraints of a step at once).
+//   U = [z_0 .. z_{p-1}, x0]           (np1 = p + 1 columns)
+//   transpose_basis_kernel:  Ut (N x np1, row-major) = U^T, via LDS tiles of 64 rows
+//   constraint_gram_kernel:  one wave per row r (contiguous row chunks per wave, banded
+//     gathers stay in L1/L2); lane a < np1 forms w_a = (M U)_{r,a} = sum_nz M_rc Ut[c][a]
+//     with one coalesced 8*np1-byte gather per nonzero, then accumulates
+//       G[a][b] += Ut[r][a] * w_b          (w_b broadcast by v_readlane: scalar, no LDS)
+//       Gv[c][a] += Ut[r][a] * v_c[r]      (up to 4 linear terms v_c)
+//     and writes one partial per wave; the partials are summed by gram_reduce_kernel in wave
+//     order (deterministic).  G = U^T M U gives term2 = G[:p,:p]/2, x0'MZ = G[p,:p],
+//     x0'Mx0 = G[p,p]; Gv gives v'Z and v.x0.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int p,
+                                                                 const double* __restrict__ Z,
+                                                                 int64_t pitch,
+                                                                 const double* __restrict__ x0,
+                                                                 double* __restrict__ Ut) {
+  extern __shared__ __attribute__((aligned(16))) double tile[];  // np1 x 65
+  const int np1 = p + 1;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int rows = static_cast<int>(n - r0 < 64 ? n - r0 : 64);
+  for (int idx = threadIdx.x; idx < np1 * 64; idx += kBlock) {
+    const int a = idx >> 6, r = idx & 63;
+    if (r < rows) tile[a * 65 + r] = a < p ? Z[a * pitch + r0 + r] : x0[r0 + r];
+  }
+  __syncthreads();
+  double* out = Ut + r0 * np1;
+  for (int idx = threadIdx.x; idx < rows * np1; idx += kBlock) {
+    const int r = idx / np1, a = idx - (idx / np1) * np1;
+    out[idx] = tile[a * 65 + r];
+  }
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const unsigned long long bits = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane(static_cast<unsigned>(bits), lane);
+  const unsigned hi = __builtin_amdgcn_readlane(static_cast<unsigned>(bits >> 32), lane);
+  return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+
+template <int NP>
+__global__ __launch_bounds__(kBlock) void constraint_gram_kernel(
+    int64_t n, int np1, const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+    const double* __restrict__ va, const double* __restrict__ Ut, int nvv,
+    const double* __restrict__ v0, const double* __restrict__ v1, const double* __restrict__ v2,
+    const double* __restrict__ v3, double* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kBlock / 64);
+  const int64_t per = (n + nwaves - 1) / nwaves;
+  const int64_t rbeg = wave * per;
+  const int64_t rend = rbeg + per < n ? rbeg + per : n;
+  const bool on = lane < np1;
+  const int la = on ? lane : 0;
+  double acc[NP];
+#pragma unroll
+  for (int b = 0; b < NP; ++b) acc[b] = 0.0;
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool has_m = rp != nullptr;
+  for (int64_t r = rbeg; r < rend; ++r) {
+    const double u = on ? Ut[r * np1 + la] : 0.0;
+    if (has_m) {
+      double w = 0.0;
+      const int s = rp[r], e = rp[r + 1];
+      for (int t = s; t < e; ++t) w += va[t] * Ut[static_cast<int64_t>(ci[t]) * np1 + la];
+      if (!on) w = 0.0;
+#pragma unroll
+      for (int b = 0; b < NP; ++b) acc[b] += u * readlane_f64(w, b);
+    }
+    if (nvv > 0) gv[0] += u * v0[r];
+    if (nvv > 1) gv[1] += u * v1[r];
+    if (nvv > 2) gv[2] += u * v2[r];
+    if (nvv > 3) gv[3] += u * v3[r];
+  }
+  // partial layout per wave: [np1 x np1 G | nvv x np1 Gv]
+  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
+  double* out = partials + wave * stride;
+  if (on) {
+    if (has_m)
+#pragma unroll
+      for (int b = 0; b < NP; ++b)
+        if (b < np1) out[lane * np1 + b] = acc[b];
+    for (int c = 0; c < nvv; ++c) out[np1 * np1 + c * np1 + lane] = gv[c];
+  }
+}
+
+hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                  double* Ut, hipStream_t s) {
+  const int np1 = p + 1;
+  if (np1 > 64) return hipErrorInvalidValue;
+  const int64_t g = (n + 63) / 64;
+  hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
+                     static_cast<size_t>(np1) * 65 * sizeof(double), s, n, p, Z, pitch, x0, Ut);
+  return hipGetLastError();
+}
+
+int constraint_gram_waves() { return kConGramGrid * (kBlock / 64); }
+
+hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
+                                  const double* const* v, double* partials, double* G, hipStream_t s) {
+  if (np1 > 64 || nvv > 4 || (M == nullptr && nvv == 0)) return hipErrorInvalidValue;
+  const int32_t* rp = M ? M->indptr : nullptr;
+  const int32_t* ci = M ? M->indices : nullptr;
+  const double* va = M ? M->vals : nullptr;
+  const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int c = 0; c < nvv; ++c) vv[c] = v[c];
+  if (np1 <= 32)
+    hipLaunchKernelGGL(constraint_gram_kernel<32>, dim3(kConGramGrid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
+                       nvv, vv[0], vv[1], vv[2], vv[3], partials);
+  else
+    hipLaunchKernelGGL(constraint_gram_kernel<64>, dim3(kConGramGrid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
+                       nvv, vv[0], vv[1], vv[2], vv[3], partials);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int npairs = np1 * np1 + nvv * np1;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs,
+                     constraint_gram_waves(), partials, G);
   return hipGetLastError();
 }
 

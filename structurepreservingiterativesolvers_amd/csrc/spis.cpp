@@ -90,18 +90,26 @@ struct spis_context {
   double* partB = nullptr;  // reduction partials, pong
   double* partR = nullptr;  // true-residual partials
   double* dscal = nullptr;  // small device scalars (kMaxK + 8)
-  double* pinned = nullptr;  // pinned host staging
+  double* pinned = nullptr;  // pinned, device-mapped host staging (kernels write h / partials here)
+  double* pinned_dev = nullptr;  // the same memory as seen from the device
   size_t pinned_len = 0;     // doubles
+  hipEvent_t ev_arn = nullptr, ev_upd[2] = {nullptr, nullptr};  // solver pipeline events
   double* gram_part = nullptr;
   size_t gram_part_len = 0;
   double* gram_G = nullptr;
   const double** gram_ptrs = nullptr;  // device array of 2 * kGramMaxVec pointers
   double* gram_pinned = nullptr;       // host staging of Gram tiles + pointer lists
+  double* cg_part = nullptr;           // fused constraint-Gram partials (per wave)
+  size_t cg_part_len = 0;
+  double* cg_G = nullptr;              // its reduced output (64*64 + 4*64)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   std::vector<spis_workspace*> pool;
   // live kernel timing (spis_profile_*): HIP events on this stream around each timed launch
   bool prof = false;
+  int prof_period = 1;            // time every prof_period-th Arnoldi iteration
+  int prof_iter = 0;              // iteration counter for the sampling
+  bool force_generic_gram = false;  // tests: take the MZ + tiled-Gram path
   std::vector<hipEvent_t> ev_free;
   struct Pending { int kind; hipEvent_t a, b; };
   std::vector<Pending> ev_pending;
@@ -147,6 +155,7 @@ struct spis_workspace {
   double* x0 = nullptr;  // copy of x0 (n)
   double* ext = nullptr;  // scratch SpMV input with ghost space (constraint / preconditioner halos)
   double* ydev = nullptr;
+  double* Ut = nullptr;  // transposed [Z, x0] for the fused constraint reduction (n x (p+1))
   int32_t ext_len = 0;
   std::vector<ConCache> con;
   std::vector<double> y_all;  // k*k host copy of every iteration's y
@@ -178,7 +187,7 @@ struct ProfScope {  // records [a, b] around the launches issued in its lifetime
   int kind;
   hipEvent_t a = nullptr;
   ProfScope(spis_context* c_, int kind_) : c(c_), kind(kind_) {
-    if (c->prof) {
+    if (c->prof && (c->prof_iter % c->prof_period) == 0) {
       a = prof_event(c);
       (void)hipEventRecord(a, c->stream);
     }
@@ -194,7 +203,13 @@ struct ProfScope {  // records [a, b] around the launches issued in its lifetime
 
 // after a stream synchronisation: fold completed event pairs into the totals
 static void prof_drain(spis_context* c) {
-  for (auto& p : c->ev_pending) {
+  size_t keep = 0;
+  for (size_t i = 0; i < c->ev_pending.size(); ++i) {
+    auto& p = c->ev_pending[i];
+    if (hipEventQuery(p.b) != hipSuccess) {  // still in flight (speculative Arnoldi step)
+      c->ev_pending[keep++] = p;
+      continue;
+    }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
       c->prof_ms[p.kind] += ms;
@@ -203,7 +218,7 @@ static void prof_drain(spis_context* c) {
     c->ev_free.push_back(p.a);
     c->ev_free.push_back(p.b);
   }
-  c->ev_pending.clear();
+  c->ev_pending.resize(keep);
 }
 
 static int allreduce(spis_context* c, double* buf, int64_t count) {
@@ -228,11 +243,28 @@ static int exchange(spis_context* c, const spis_matrix* M, double* x) {
 
 static int ensure_pinned(spis_context* c, size_t len) {
   if (c->pinned_len >= len) return SPIS_OK;
-  if (c->pinned) HIP_TRY(hipHostFree(c->pinned));
+  if (c->pinned) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipHostFree(c->pinned));
+  }
   c->pinned = nullptr;
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double), hipHostMallocMapped));
+  void* dp = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
+  c->pinned_dev = static_cast<double*>(dp);
   c->pinned_len = len;
   return SPIS_OK;
+}
+
+// spin on an event (the solver's one host wait per iteration: lower wake-up latency than a
+// blocking synchronize; the host thread has nothing else to do meanwhile)
+static int wait_event(hipEvent_t e) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return SPIS_OK;
+    if (r != hipErrorNotReady) return fail(SPIS_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(r));
+    __builtin_ia32_pause();
+  }
 }
 
 // y = M x where x is a local vector (owned part valid); ghosts gathered through scratch if needed
@@ -324,6 +356,9 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->partR, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_arn, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], hipEventDisableTiming));
     *out = c.release();
     return SPIS_OK;
   })
@@ -366,6 +401,8 @@ extern "C" int spis_context_destroy(spis_context* c) {
       (void)hipEventDestroy(p.b);
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1]})
+      if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SPIS_OK;
@@ -391,7 +428,10 @@ extern "C" int spis_profile_enable(spis_context* c, int32_t on) {
     if (!c) return fail(SPIS_ERR_ARG, "null context");
     HIP_TRY(hipStreamSynchronize(c->stream));
     prof_drain(c);
-    c->prof = on != 0;
+    c->prof = on > 0;
+    c->prof_period = on > 0 ? on : 1;
+    c->prof_iter = 0;
+    c->force_generic_gram = on < 0;  // (negative: test hook selecting the generic Gram path)
     for (int i = 0; i < SPIS_PROF_KINDS; ++i) {
       c->prof_ms[i] = 0.0;
       c->prof_n[i] = 0;
@@ -692,9 +732,13 @@ extern "C" int spis_gemv(spis_context* c, int64_t n, int32_t p, const double* Z,
   ABI_GUARD({
     if (!c || !Z || !y_host || !x0 || !x || n < 0 || p < 1 || p > kMaxK || pitch < n)
       return fail(SPIS_ERR_ARG, "bad argument");
-    for (int i = 0; i < p; ++i) c->pinned[i] = y_host[i];
-    HIP_TRY(hipMemcpyAsync(c->dscal, c->pinned, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(launch_gemv(n, p, Z, pitch, c->dscal, x0, x, c->stream));
+    if (p <= kYArg) {
+      HIP_TRY(launch_gemv(n, p, Z, pitch, y_host, true, x0, x, c->stream));
+    } else {
+      for (int i = 0; i < p; ++i) c->pinned[i] = y_host[i];
+      HIP_TRY(hipMemcpyAsync(c->dscal, c->pinned, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(launch_gemv(n, p, Z, pitch, c->dscal, false, x0, x, c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SPIS_OK;
   })
@@ -709,44 +753,147 @@ extern "C" int spis_gram(spis_context* c, int64_t n, int32_t nu, const double* c
 }
 
 // ------------------------------------------------------------------------------------------------
-// constraint terms (class form), solvers.py:21-40
+// constraint terms (class form), solvers.py:21-40, all constraints of a step at once:
+//   MZ = M Z (one multi-vector SpMM launch per matrix, columns cached across the constrained
+//   steps of a solve because the basis never changes), then ONE Gram
+//   G = [z_0 .. z_{p-1}, x0]^T [M_1 Z, v_1, M_1 x0, M_2 Z, v_2, M_2 x0, ...]
+// from which term0 / term1 / term2 of every constraint are read off.
 // ------------------------------------------------------------------------------------------------
-static int constraint_terms(spis_context* c, spis_workspace* ws, ConCache* cc, const spis_constraint_desc& con,
-                            int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
-                            double* term0, double* term1, double* term2) {
-  const bool mzero = con.M == nullptr || con.M->all_zero;
+// fused path (single GPU, p + 1 <= 64, <= 4 linear terms): transpose [Z, x0] once, then one
+// wave-per-row pass per constraint matrix (K7) — no M Z columns are materialised
+static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
+                                  int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                  QuadCon* out) {
+  const int np1 = p + 1;
+  if (!ws->Ut) HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * std::max<int64_t>(n, 1) * 64));
+  const size_t need = static_cast<size_t>(constraint_gram_waves()) * (np1 * np1 + 4 * np1);
+  if (c->cg_part_len < need) {
+    if (c->cg_part) HIP_TRY(hipFree(c->cg_part));
+    HIP_TRY(hipMalloc(&c->cg_part, need * sizeof(double)));
+    c->cg_part_len = need;
+  }
+  if (!c->cg_G) HIP_TRY(hipMalloc(&c->cg_G, sizeof(double) * (64 * 64 + 4 * 64)));
+  if (!c->gram_pinned)
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->gram_pinned), sizeof(double) * (64 * 64 + 2 * kGramMaxVec),
+                          hipHostMallocDefault));
+  HIP_TRY(launch_transpose_basis(n, p, Z, pitch, x0, ws->Ut, c->stream));
+  std::vector<const double*> vlist;
+  std::vector<int> vidx(m, -1);
+  for (int ci = 0; ci < m; ++ci)
+    if (cons[ci].v_dev) {
+      vidx[ci] = static_cast<int>(vlist.size());
+      vlist.push_back(cons[ci].v_dev);
+    }
+  std::vector<double> Gv(static_cast<size_t>(vlist.size()) * np1, 0.0);
+  std::vector<std::vector<double>> Gm(m);
+  bool v_done = vlist.empty();
+  for (int ci = 0; ci < m; ++ci) {
+    const bool mzero = cons[ci].M == nullptr || cons[ci].M->all_zero;
+    if (mzero) continue;
+    const CsrView mv = cons[ci].M->view();
+    const int nvv = v_done ? 0 : static_cast<int>(vlist.size());
+    HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
+    const int cnt = np1 * np1 + nvv * np1;
+    HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    Gm[ci].assign(c->gram_pinned, c->gram_pinned + np1 * np1);
+    if (!v_done) {
+      std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + cnt, Gv.begin());
+      v_done = true;
+    }
+  }
+  if (!v_done) {
+    const int nvv = static_cast<int>(vlist.size());
+    HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * (np1 * np1 + nvv * np1), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + np1 * np1 + nvv * np1, Gv.begin());
+  }
+  for (int ci = 0; ci < m; ++ci) {
+    QuadCon& q = out[ci];
+    q.term1.assign(p, 0.0);
+    q.term2.assign(static_cast<size_t>(p) * p, 0.0);
+    const std::vector<double>& G = Gm[ci];
+    const bool hasM = !G.empty();
+    const double* gv = vidx[ci] >= 0 ? Gv.data() + static_cast<size_t>(vidx[ci]) * np1 : nullptr;
+    const double x0Mx0 = hasM ? G[static_cast<size_t>(p) * np1 + p] : 0.0;
+    const double vx0 = gv ? gv[p] : 0.0;
+    q.term0 = 0.5 * x0Mx0 + cons[ci].c + vx0;  // solvers.py:34
+    for (int a = 0; a < p; ++a)                // :35
+      q.term1[a] = (gv ? gv[a] : 0.0) + (hasM ? G[static_cast<size_t>(p) * np1 + a] : 0.0);
+    if (hasM)                                  // :36
+      for (int a = 0; a < p; ++a)
+        for (int b = 0; b < p; ++b) q.term2[static_cast<size_t>(a) * p + b] = 0.5 * G[static_cast<size_t>(a) * np1 + b];
+  }
+  return SPIS_OK;
+}
+
+static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
+                                int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                QuadCon* out) {
+  int nlin = 0;
+  for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
+  if (!c->comm && p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram)
+    return constraint_terms_fused(c, ws, m, cons, n, p, Z, pitch, x0, out);
   std::vector<const double*> U, V;
   for (int i = 0; i < p; ++i) U.push_back(Z + static_cast<int64_t>(i) * pitch);
   U.push_back(x0);
-  int iv = -1, imx = -1;
-  if (!mzero) {
-    if (con.M->n_rows != n) return fail(SPIS_ERR_ARG, "constraint matrix rows %lld != n %lld", (long long)con.M->n_rows, (long long)n);
-    // M z_i, cached across constrained steps of one solve (the basis never changes)
-    for (int i = cc->cols; i < p; ++i)
-      ST_TRY(spmv_local(c, ws, con.M, Z + static_cast<int64_t>(i) * pitch, cc->MZ + static_cast<int64_t>(i) * ws->pitch_n));
-    cc->cols = std::max(cc->cols, p);
-    if (!cc->mx0_done) {
-      ST_TRY(spmv_local(c, ws, con.M, x0, cc->Mx0));
-      cc->mx0_done = true;
+  struct Idx {
+    int mz0 = -1, iv = -1, imx = -1;
+  };
+  std::vector<Idx> idx(m);
+  for (int ci = 0; ci < m; ++ci) {
+    const spis_constraint_desc& con = cons[ci];
+    ConCache& cc = ws->con[ci];
+    const bool mzero = con.M == nullptr || con.M->all_zero;
+    if (!mzero) {
+      if (con.M->n_rows != n) return fail(SPIS_ERR_ARG, "constraint matrix rows != n");
+      if (cc.cols < p) {
+        if (!c->comm || con.M->n_ghost == 0) {
+          HIP_TRY(launch_spmm(con.M->view(), Z + static_cast<int64_t>(cc.cols) * pitch, pitch, p - cc.cols,
+                              cc.MZ + static_cast<int64_t>(cc.cols) * ws->pitch_n, ws->pitch_n, c->stream));
+        } else {
+          for (int i = cc.cols; i < p; ++i)
+            ST_TRY(spmv_local(c, ws, con.M, Z + static_cast<int64_t>(i) * pitch,
+                              cc.MZ + static_cast<int64_t>(i) * ws->pitch_n));
+        }
+        cc.cols = p;
+      }
+      if (!cc.mx0_done) {
+        ST_TRY(spmv_local(c, ws, con.M, x0, cc.Mx0));
+        cc.mx0_done = true;
+      }
+      idx[ci].mz0 = static_cast<int>(V.size());
+      for (int i = 0; i < p; ++i) V.push_back(cc.MZ + static_cast<int64_t>(i) * ws->pitch_n);
     }
-    for (int i = 0; i < p; ++i) V.push_back(cc->MZ + static_cast<int64_t>(i) * ws->pitch_n);
+    if (con.v_dev) {
+      idx[ci].iv = static_cast<int>(V.size());
+      V.push_back(con.v_dev);
+    }
+    if (!mzero) {
+      idx[ci].imx = static_cast<int>(V.size());
+      V.push_back(cc.Mx0);
+    }
   }
-  if (con.v_dev) { iv = static_cast<int>(V.size()); V.push_back(con.v_dev); }
-  if (!mzero) { imx = static_cast<int>(V.size()); V.push_back(cc->Mx0); }
   const int nu = p + 1, nv = static_cast<int>(V.size());
   std::vector<double> G(static_cast<size_t>(nu) * std::max(nv, 1), 0.0);
   if (nv > 0) ST_TRY(gram(c, n, nu, U.data(), nv, V.data(), G.data()));
   auto g = [&](int a, int b) { return G[static_cast<size_t>(a) * nv + b]; };
-  const double x0Mx0 = imx >= 0 ? g(p, imx) : 0.0;
-  const double vx0 = iv >= 0 ? g(p, iv) : 0.0;
-  *term0 = 0.5 * x0Mx0 + con.c + vx0;  // 0.5*x0@M@x0 + c + v@x0  (solvers.py:34)
-  for (int a = 0; a < p; ++a) {         // v@Z + x0@MZ             (:35)
-    const double vz = iv >= 0 ? g(a, iv) : 0.0;
-    const double xmz = mzero ? 0.0 : g(p, a);
-    term1[a] = vz + xmz;
+  for (int ci = 0; ci < m; ++ci) {
+    const Idx& d = idx[ci];
+    QuadCon& q = out[ci];
+    q.term1.assign(p, 0.0);
+    q.term2.assign(static_cast<size_t>(p) * p, 0.0);
+    const double x0Mx0 = d.imx >= 0 ? g(p, d.imx) : 0.0;
+    const double vx0 = d.iv >= 0 ? g(p, d.iv) : 0.0;
+    q.term0 = 0.5 * x0Mx0 + cons[ci].c + vx0;  // 0.5*x0@M@x0 + c + v@x0  (solvers.py:34)
+    for (int a = 0; a < p; ++a)                // v@Z + x0@MZ             (:35)
+      q.term1[a] = (d.iv >= 0 ? g(a, d.iv) : 0.0) + (d.mz0 >= 0 ? g(p, d.mz0 + a) : 0.0);
+    if (d.mz0 >= 0)                            // 0.5*Z.T@MZ              (:36)
+      for (int a = 0; a < p; ++a)
+        for (int b = 0; b < p; ++b) q.term2[static_cast<size_t>(a) * p + b] = 0.5 * g(a, d.mz0 + b);
   }
-  for (int a = 0; a < p; ++a)           // 0.5*Z.T@MZ              (:36)
-    for (int b = 0; b < p; ++b) term2[static_cast<size_t>(a) * p + b] = mzero ? 0.0 : 0.5 * g(a, b);
   return SPIS_OK;
 }
 
@@ -776,13 +923,19 @@ extern "C" int spis_constraint_terms(spis_context* c, const spis_constraint_desc
     tmp.n = n;
     tmp.pitch_n = round_up(std::max<int64_t>(n, 1), 64);
     tmp.k = p;
-    ST_TRY(ensure_con_cache(&tmp, 1, con));
-    int st = constraint_terms(c, &tmp, &tmp.con[0], *con, n, p, Z, pitch, x0, term0, term1, term2);
+    int st = ensure_con_cache(&tmp, 1, con);
+    QuadCon q;
+    if (st == SPIS_OK) st = constraint_terms_all(c, &tmp, 1, con, n, p, Z, pitch, x0, &q);
     (void)hipStreamSynchronize(c->stream);
     if (tmp.con[0].MZ) (void)hipFree(tmp.con[0].MZ);
     if (tmp.con[0].Mx0) (void)hipFree(tmp.con[0].Mx0);
     if (tmp.ext) (void)hipFree(tmp.ext);
-    return st;
+    if (tmp.Ut) (void)hipFree(tmp.Ut);
+    if (st != SPIS_OK) return st;
+    *term0 = q.term0;
+    std::copy(q.term1.begin(), q.term1.end(), term1);
+    std::copy(q.term2.begin(), q.term2.end(), term2);
+    return SPIS_OK;
   })
 }
 
@@ -847,9 +1000,14 @@ extern "C" int spis_workspace_iterate(spis_workspace* ws, int32_t i, double* x_o
       HIP_TRY(launch_copy(ws->n, ws->r0, x_out, c->stream));
     } else {
       const double* y = ws->y_all.data() + static_cast<size_t>(i - 1) * ws->k;
-      for (int a = 0; a < i; ++a) c->pinned[a] = y[a];
-      HIP_TRY(hipMemcpyAsync(ws->ydev, c->pinned, sizeof(double) * i, hipMemcpyHostToDevice, c->stream));
-      HIP_TRY(launch_gemv(ws->n, i, ws->Zb, ws->pitch, ws->ydev, ws->x0, x_out, c->stream));
+      if (i <= kYArg) {
+        HIP_TRY(launch_gemv(ws->n, i, ws->Zb, ws->pitch, y, true, ws->x0, x_out, c->stream));
+      } else {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int a = 0; a < i; ++a) c->pinned[a] = y[a];
+        HIP_TRY(hipMemcpyAsync(ws->ydev, c->pinned, sizeof(double) * i, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(launch_gemv(ws->n, i, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, x_out, c->stream));
+      }
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SPIS_OK;
@@ -874,6 +1032,14 @@ namespace {
 
 enum Safety { kSafetyNone = -1, kSafetyFalse = 0, kSafetyTrue = 1 };
 
+// Pipeline (one host wait per iteration, GPU never idle while the host solves the LS):
+//   stream order  A_0, A_1, U_0, A_2, U_1, A_3, U_2, ...
+//   A_j = Arnoldi step j (SpMV + MGS chain + normalise; h column j -> mapped pinned slot j)
+//   U_j = update of step j (GEMV x_j = Z y_j + x0, true-residual SpMV; partials -> slot j%2)
+// At iteration j the host waits for U_{j-1} (which also covers A_j), reads res_{j-1} (stop test
+// of iteration j-1, as solvers.py:296) and h column j, solves LS_j, enqueues U_j and A_{j+2}.
+// A_{j+1} was enqueued an iteration earlier, so the GPU works on it during LS_j; a stop or
+// breakdown discards at most the speculative A_{j+1}, A_{j+2} (they never touch x / res).
 struct Solver {
   spis_context* c;
   spis_matrix* A;
@@ -881,16 +1047,22 @@ struct Solver {
   spis_workspace* ws;
   const double* b;
   int64_t n;
+  int k;
   int gs;  // SpMV partial count
   int gb;  // BLAS-1 partial count
   std::vector<double> hostq, hostz;
 
   double* Qv(int i) const { return ws->Q + static_cast<int64_t>(i) * ws->pitch; }
   double* Zv(int i) const { return ws->Zb + static_cast<int64_t>(i) * ws->pitch; }
+  // mapped pinned layout: [k slots of (k+2) h values][2 residual-partial slots][y staging]
+  size_t hoff(int j) const { return static_cast<size_t>(j) * (k + 2); }
+  size_t roff(int j) const { return static_cast<size_t>(k) * (k + 2) + static_cast<size_t>(j & 1) * kSpmvGrid; }
+  size_t yoff() const { return static_cast<size_t>(k) * (k + 2) + 2 * kSpmvGrid; }
+  size_t pinned_need() const { return yoff() + kMaxK + 16; }
 
-  // solvers.py:190-198: z_j = P^-1 q_j ; y = A z_j ; MGS ; h_{j+1,j} = ||y|| ; q_{j+1} = y / h
-  int enqueue_arnoldi(int j) {
+  int enqueue_arnoldi(int j) {  // solvers.py:190-198
     hipStream_t s = c->stream;
+    c->prof_iter = j;
     double* zj = Zv(j);
     if (o->pre_matrix) {
       ST_TRY(spmv_local(c, ws, o->pre_matrix, Qv(j), zj));
@@ -909,6 +1081,7 @@ struct Solver {
       HIP_TRY(launch_spmv(A->view(), kEpiDot, zj, ws->w, Qv(0), c->partA, gs, s));
     }
     ST_TRY(allreduce(c, c->partA, gs));
+    double* hcol = c->pinned_dev + hoff(j);  // the kernels write H[:, j] straight to host memory
     {
       ProfScope pm(c, SPIS_PROF_MGS);
       double* src = c->partA;
@@ -916,41 +1089,48 @@ struct Solver {
       int n_in = gs;
       for (int i = 0; i <= j; ++i) {
         const double* qn = i < j ? Qv(i + 1) : nullptr;
-        HIP_TRY(launch_mgs_step(n, ws->w, Qv(i), qn, src, n_in, dst, c->dscal + i, gb, s));
+        HIP_TRY(launch_mgs_step(n, ws->w, Qv(i), qn, src, n_in, dst, hcol + i, gb, s));
         ST_TRY(allreduce(c, dst, gb));
         std::swap(src, dst);
         n_in = gb;
       }
-      HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, c->dscal + j + 1, s, gb));
+      HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, hcol + j + 1, s, gb));
     }
-    HIP_TRY(hipMemcpyAsync(c->pinned, c->dscal, sizeof(double) * (j + 2), hipMemcpyDeviceToHost, s));
     return SPIS_OK;
   }
 
-  // solvers.py:287,290: x_j = Z y + x0 ; partials of ||A x_j - b||^2
-  int enqueue_update(int p, const double* y) {
+  int enqueue_update(int j, int p, const double* y) {  // solvers.py:287,290
     hipStream_t s = c->stream;
-    double* yh = c->pinned + 2 * kMaxK;
-    for (int a = 0; a < p; ++a) yh[a] = y[a];
-    HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
+    c->prof_iter = j;
     {
       ProfScope pg(c, SPIS_PROF_GEMV);
-      HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, ws->x0, ws->xj, s));
+      if (p <= kYArg) {
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, ws->xj, s));
+      } else {
+        double* yh = c->pinned + yoff();
+        for (int a = 0; a < p; ++a) yh[a] = y[a];
+        HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, ws->xj, s));
+      }
     }
     ST_TRY(exchange(c, A, ws->xj));
+    double* rpart = c->comm ? c->partR : c->pinned_dev + roff(j);
     {
       ProfScope ps(c, SPIS_PROF_SPMV_RES);
-      HIP_TRY(launch_spmv(A->view(), kEpiResNorm, ws->xj, nullptr, b, c->partR, gs, s));
+      HIP_TRY(launch_spmv(A->view(), kEpiResNorm, ws->xj, nullptr, b, rpart, gs, s));
     }
-    ST_TRY(allreduce(c, c->partR, gs));
-    HIP_TRY(hipMemcpyAsync(c->pinned + 3 * kMaxK, c->partR, sizeof(double) * gs, hipMemcpyDeviceToHost, s));
+    if (c->comm) {
+      ST_TRY(allreduce(c, c->partR, gs));
+      HIP_TRY(hipMemcpyAsync(c->pinned + roff(j), c->partR, sizeof(double) * gs, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipEventRecord(c->ev_upd[j & 1], s));
     return SPIS_OK;
   }
 
-  double host_residual() const {
-    const double* p = c->pinned + 3 * kMaxK;
+  double residual(int j) const {  // fixed-order host sum of the partials of U_j
+    const double* q = c->pinned + roff(j);
     double t = 0.0;
-    for (int i = 0; i < gs; ++i) t += p[i];
+    for (int i = 0; i < gs; ++i) t += q[i];
     return std::sqrt(t);
   }
 };
@@ -985,9 +1165,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ws->H.assign(static_cast<size_t>(k + 1) * k, 0.0);
     const bool use_cb = o->conls_fn != nullptr;
     if (!use_cb && o->n_constraints > 0) ST_TRY(ensure_con_cache(ws, o->n_constraints, o->constraints));
-    ST_TRY(ensure_pinned(c, 3 * kMaxK + std::max(kSpmvGrid, kRedGrid) + 16));
 
-    Solver S{c, A, o, ws, b, n, spmv_grid(A->view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
+    Solver S{c, A, o, ws, b, n, k, spmv_grid(A->view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
+    ST_TRY(ensure_pinned(c, S.pinned_need()));
     hipStream_t s = c->stream;
     double* stamps = out->stamps_host;  // [0,k) iter start, [k,2k) iter end, [2k,3k) con start, [3k,4k) con end
     const double t_start = now_s();
@@ -1003,10 +1183,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ST_TRY(exchange(c, A, ws->xj));
     HIP_TRY(launch_spmv(A->view(), kEpiR0, ws->xj, ws->r0, b, c->partA, S.gs, s));
     ST_TRY(allreduce(c, c->partA, S.gs));
-    HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->dscal, s, S.gb));
-    HIP_TRY(hipMemcpyAsync(c->pinned, c->dscal, sizeof(double), hipMemcpyDeviceToHost, s));
+    double* beta_slot = c->pinned + S.yoff() + kMaxK;
+    HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
     HIP_TRY(hipStreamSynchronize(s));
-    const double beta = c->pinned[0];
+    const double beta = *beta_slot;
     int n_res = 0;
     out->res_host[n_res++] = beta;
     int steps = 0;
@@ -1016,9 +1196,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     qr.reset(k, beta);
     std::vector<double> y(k + 1, 0.0), yk(k + 1, 0.0), y0(k + 1, 0.0), ycon(k + 1, 0.0), hcol(k + 2, 0.0);
     std::vector<QuadCon> cons(std::max(o->n_constraints, 0));
-    int con_steps = 0;
-    bool have_x = false;  // ws->xj holds x[-1] (else x[-1] = r0)
-    bool pending = false;  // an update (GEMV + residual) of iteration j-1 is in flight
+    bool have_x = false;   // ws->xj holds x[-1] (else x[-1] = r0)
+    int pending = -1;      // iteration whose update U_j is in flight and not yet read
 
     if (beta == 0.0) {  // x0 solves the system: q0 would be 0/0 (reference: NaNs); report breakdown
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
@@ -1026,14 +1205,19 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     } else {
       if (stamps) stamps[0] = now_s();
       ST_TRY(S.enqueue_arnoldi(0));
+      HIP_TRY(hipEventRecord(c->ev_arn, s));
+      if (k > 1) {
+        if (stamps) stamps[1] = now_s();
+        ST_TRY(S.enqueue_arnoldi(1));
+      }
     }
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
-      HIP_TRY(hipStreamSynchronize(s));
+      ST_TRY(wait_event(j == 0 ? c->ev_arn : c->ev_upd[(j - 1) & 1]));
       prof_drain(c);
-      if (pending) {  // finish iteration j-1: its true residual + stop test (solvers.py:290-297)
-        out->res_host[n_res++] = S.host_residual();
-        pending = false;
-        if (stamps) stamps[k + j - 1] = now_s();
+      if (pending >= 0) {  // finish iteration j-1: true residual + stop test (solvers.py:290-297)
+        out->res_host[n_res++] = S.residual(pending);
+        if (stamps) stamps[k + pending] = now_s();
+        pending = -1;
         const double r = out->res_host[n_res - 1];
         const bool stop = o->method == SPIS_GMRES ? (r < o->tol)
                           : o->method == SPIS_CGMRES ? (r < o->tol && safety == kSafetyTrue)
@@ -1041,7 +1225,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (stop) break;
       }
       steps = j + 1;  // solvers.py:189
-      for (int i = 0; i < j + 2; ++i) hcol[i] = c->pinned[i];
+      const double* hp = c->pinned + S.hoff(j);
+      for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
       for (int i = 0; i < j + 2; ++i) ws->H[static_cast<size_t>(j) * (k + 1) + i] = hcol[i];
       if (hcol[j + 1] == 0.0 && o->method != SPIS_CGMRES_P) {  // :197-202
         out->events_host[j] |= SPIS_EV_BREAKDOWN;
@@ -1072,7 +1257,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         for (int cc = 0; cc < p; ++cc)
           for (int r = 0; r <= p; ++r) Hc[static_cast<size_t>(cc) * (p + 1) + r] = ws->H[static_cast<size_t>(cc) * (k + 1) + r];
         HIP_TRY(hipStreamSynchronize(s));
-        if (o->timing) ++con_steps;
         if (stamps) stamps[2 * k + j] = now_s();
         int32_t br = SPIS_BRANCH_CON, evc = 0, msc = SPIS_MSG_SUCCESS;
         if (o->conls_fn(o->conls_user, ws, j, p, Hc.data(), beta, y0.data(), y.data(), &br, &evc, &msc) != 0)
@@ -1088,14 +1272,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (branch == SPIS_BRANCH_FALLBACK) qr.solve(p, y.data());
       } else {
         // class-form constraints reduced on the device (:242-247), KKT on the host (:251-255)
-        if (o->timing && o->method == SPIS_CGMRES) ++con_steps;
         if (stamps) stamps[2 * k + j] = now_s();
-        for (int i = 0; i < m_active; ++i) {
-          cons[i].term1.assign(p, 0.0);
-          cons[i].term2.assign(static_cast<size_t>(p) * p, 0.0);
-          ST_TRY(constraint_terms(c, ws, &ws->con[i], o->constraints[i], n, p, ws->Zb, ws->pitch, ws->x0,
-                                  &cons[i].term0, cons[i].term1.data(), cons[i].term2.data()));
-        }
+        if (m_active > 0)
+          ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
+                                      cons.data()));
         if (stamps) stamps[3 * k + j] = now_s();
         bool failed = false;
         if (m_active == 0) {
@@ -1146,21 +1326,20 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         out->y_host[static_cast<size_t>(j) * k + a] = y[a];
       }
       ws->n_iter_y = j + 1;
-      ST_TRY(S.enqueue_update(p, y.data()));
+      ST_TRY(S.enqueue_update(j, p, y.data()));
       have_x = true;
-      pending = true;
-      if (j + 1 < k) {
-        if (stamps) stamps[j + 1] = now_s();
-        ST_TRY(S.enqueue_arnoldi(j + 1));
+      pending = j;
+      if (j + 2 < k) {
+        if (stamps) stamps[j + 2] = now_s();
+        ST_TRY(S.enqueue_arnoldi(j + 2));
       }
     }
-    if (pending) {
-      HIP_TRY(hipStreamSynchronize(s));
-      prof_drain(c);
-      out->res_host[n_res++] = S.host_residual();
-      if (stamps) stamps[k + ws->n_iter_y - 1] = now_s();
+    if (pending >= 0) {
+      ST_TRY(wait_event(c->ev_upd[pending & 1]));
+      out->res_host[n_res++] = S.residual(pending);
+      if (stamps) stamps[k + pending] = now_s();
     }
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipStreamSynchronize(s));  // speculative Arnoldi steps finish before x / ws are used
     prof_drain(c);
     if (out->x_final_dev) {
       if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
@@ -1171,7 +1350,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       stamps[4 * k] = t_start;
       stamps[4 * k + 1] = now_s();
     }
-    (void)con_steps;
     ws->steps = steps;
     out->steps = steps;
     out->n_res = n_res;

@@ -203,6 +203,27 @@ def test_golden(spis, name, caplog):
         assert d["timings"]["constrained_steps"] == int(case.z["timing_constrained_steps"])
 
 
+def test_fused_and_generic_constraint_reduction_agree(spis):
+    """The fused transpose + wave-per-row kernel (K7) and the generic M Z + tiled Gram path
+    (K5 + K6) give the same constrained solve."""
+    from structurepreservingiterativesolvers_amd import _lib
+    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=20)
+    x0 = np.random.default_rng(4).normal(size=dic["b"].shape)  # non-zero x0: all term0/term1 parts
+    ctx = get_context()
+    xf, df = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
+    _lib.check(ctx.L.spis_profile_enable(ctx.handle, -1), "spis_profile_enable")
+    try:
+        xg, dg = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
+    finally:
+        _lib.check(ctx.L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
+    assert df["x"].trace == dg["x"].trace
+    np.testing.assert_allclose(xf, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
+
+
 def test_lkdvrk_dict_form_through_callback(spis):
     """lift=False keeps the reference's dict-form constraints (host SLSQP through
     the constrained-LS callback of spis_solve)."""
@@ -285,7 +306,10 @@ def test_full_size_swe_properties(spis):
     assert np.all(np.diff(res[:-1]) <= 1e-12 * res[0])
     Q = d["x"].basis(30)
     G = Q @ Q.T
-    assert np.abs(G - np.eye(30)).max() < 1e-10
+    # MGS orthogonality loss is inherent here (h_{j+1,j} / ||A q_j|| ~ 2e-4): the reference's own
+    # basis (oracle, same NumPy ops) shows max|Q'Q - I| between 2.3e-7 and 3.8e-6 across 1e-16
+    # perturbations of b at this size; require the same order
+    assert np.abs(G - np.eye(30)).max() < 1e-5
     assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-12 * abs(dic["m0"])
     assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
     np.testing.assert_allclose(res[-1], np.linalg.norm(A @ x - dic["b"]), rtol=1e-10)
