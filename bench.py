@@ -146,10 +146,11 @@ def main():
 
     S = spmv_bytes(n, A.nnz)
     spmv_ms = ms[_lib.PROF_SPMV] / max(cnt[_lib.PROF_SPMV], 1)
-    spmv_gbs = S / (spmv_ms * 1e-3) / 1e9
-    p_mean = (args.k + 1) / 2.0
+    spmv_gbs = S / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
+    sampled = [j + 1 for j in range(0, args.k, max(args.prof_period, 1))]
+    p_mean = float(np.mean(sampled))  # basis size of the sampled (timed) MGS chains
     mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
-    mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9
+    mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
     traffic = load_traffic()

@@ -17,7 +17,8 @@ constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's L
 constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
 constexpr int kGramMaxVec = 64;  // max vectors on either side of one Gram launch (<= 256 4x4 tiles)
 constexpr int kYArg = 128;
-constexpr int kConGramGrid = 512;  // workgroups of the fused constraint Gram (4 waves each)       // GEMV coefficients passed by value up to this p
+constexpr int kMgsPer = 4;       // 16-B pairs per lane per round in MGS / normalise (loads issued first)
+constexpr int kConGramGrid = 1024;  // workgroups of the fused constraint Gram (4 waves each)       // GEMV coefficients passed by value up to this p
 
 struct YArg {
   double v[kYArg];
@@ -64,8 +65,8 @@ size_t gram_lds_bytes(int nu, int nv);
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   double* Ut, hipStream_t s);
 // G = [U^T M U | U^T v_0 .. U^T v_{nvv-1}] from Ut (M may be null: linear terms only);
-// partials: constraint_gram_waves() x (np1*np1 + nvv*np1) doubles
-int constraint_gram_waves();
+// partials: constraint_gram_partials() x (np1*np1 + nvv*np1) doubles
+int constraint_gram_partials();
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
                                   const double* const* v, double* partials, double* G, hipStream_t s);
 // partial dot / sum of squares

@@ -77,10 +77,25 @@ __global__ __launch_bounds__(kBlock) void spmv_rowblock_kernel(
       }
       continue;
     }
-    const double* __restrict__ vb = va + nz0;
-    const int32_t* __restrict__ cb = ci + nz0;
-#pragma unroll 4
-    for (int i = threadIdx.x; i < nnz; i += kBlock) s_prod[i] = vb[i] * x[cb[i]];
+    // all of the block's val/col loads first (kNnzCap / kBlock per lane, coalesced), then the
+    // x gathers, then the rounded products to LDS: maximal loads in flight per lane
+    constexpr int kPer = kNnzCap / kBlock;
+    int cols[kPer];
+    double vals[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      cols[u] = i < nnz ? ci[nz0 + i] : 0;
+      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+    }
+    double xs[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) xs[u] = x[cols[u]];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < nnz) s_prod[i] = vals[u] * xs[u];
+    }
     __syncthreads();
     const int r = r0 + threadIdx.x;
     if (r < r1) {
@@ -109,7 +124,7 @@ int spmv_grid(const CsrView& A, bool fixed) {
 
 int blas_grid(int64_t n, bool fixed) {
   if (fixed) return kRedGrid;
-  int64_t g = (n + 2 * kBlock * 2 - 1) / (2 * kBlock * 2);  // >= 2 pairs per thread
+  int64_t g = (n / 2 + kBlock * kMgsPer - 1) / (kBlock * kMgsPer);  // kMgsPer 16-B pairs per lane
   if (g > kRedGrid) g = kRedGrid;
   return g < 1 ? 1 : static_cast<int>(g);
 }
@@ -155,69 +170,68 @@ __global__ __launch_bounds__(kBlock) void mgs_step_kernel(int64_t n, double* __r
                                                           double* __restrict__ h_out) {
 #pragma clang fp contract(off)
   __shared__ double s_wave[4];
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   double part = 0.0;
   if (VEC) {
     const int64_t npair = n >> 1;
     double2* y2 = reinterpret_cast<double2*>(y);
     const double2* q2 = reinterpret_cast<const double2*>(qi);
     const double2* n2 = reinterpret_cast<const double2*>(qn);
-    // issue this thread's first 16-B loads BEFORE the partial reduction (a barrier + a
-    // latency-bound read of n_in partials): the stream is in flight while h_i is formed
-    const bool have = tid < npair;
-    double2 yv0 = make_double2(0.0, 0.0), qv0 = yv0, nv0 = yv0;
-    if (have) {
-      qv0 = q2[tid];
-      yv0 = y2[tid];
-      if (qn) nv0 = n2[tid];
-    }
+    const int64_t round = static_cast<int64_t>(gridDim.x) * kBlock * kMgsPer;
+    int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * kMgsPer + threadIdx.x;
+    double2 yv[kMgsPer], qv[kMgsPer], nv[kMgsPer];
+    auto load = [&](int64_t b0) {
+#pragma unroll
+      for (int u = 0; u < kMgsPer; ++u) {
+        const int64_t p = b0 + u * kBlock;
+        if (p < npair) {
+          qv[u] = q2[p];
+          yv[u] = y2[p];
+          if (qn) nv[u] = n2[p];
+        }
+      }
+    };
+    // the first round's loads are in flight while h_i is formed (barrier + partial reads)
+    load(base);
     const double h = sum_partials(part_in, n_in, s_wave);
     if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
-    if (have) {
-      const double a0 = h * qv0.x, a1 = h * qv0.y;
-      yv0.x = yv0.x - a0;
-      yv0.y = yv0.y - a1;
-      y2[tid] = yv0;
-      if (qn) {
-        part += nv0.x * yv0.x;
-        part += nv0.y * yv0.y;
-      } else {
-        part += yv0.x * yv0.x;
-        part += yv0.y * yv0.y;
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < kMgsPer; ++u) {
+        const int64_t p = base + u * kBlock;
+        if (p < npair) {
+          const double a0 = h * qv[u].x, a1 = h * qv[u].y;
+          yv[u].x = yv[u].x - a0;
+          yv[u].y = yv[u].y - a1;
+          y2[p] = yv[u];
+          if (qn) {
+            part += nv[u].x * yv[u].x;
+            part += nv[u].y * yv[u].y;
+          } else {
+            part += yv[u].x * yv[u].x;
+            part += yv[u].y * yv[u].y;
+          }
+        }
       }
+      base += round;
+      if (base - threadIdx.x >= npair) break;
+      load(base);
     }
-    for (int64_t p = tid + stride; p < npair; p += stride) {
-      const double2 qv = q2[p];
-      double2 yv = y2[p];
-      const double a0 = h * qv.x, a1 = h * qv.y;
-      yv.x = yv.x - a0;
-      yv.y = yv.y - a1;
-      y2[p] = yv;
-      if (qn) {
-        const double2 nv = n2[p];
-        part += nv.x * yv.x;
-        part += nv.y * yv.y;
-      } else {
-        part += yv.x * yv.x;
-        part += yv.y * yv.y;
-      }
-    }
-    if ((n & 1) && tid == 0) {
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
       const int64_t e = n - 1;
       const double a = h * qi[e];
-      const double yv = y[e] - a;
-      y[e] = yv;
-      part += qn ? qn[e] * yv : yv * yv;
+      const double yv1 = y[e] - a;
+      y[e] = yv1;
+      part += qn ? qn[e] * yv1 : yv1 * yv1;
     }
   } else {
     const double h = sum_partials(part_in, n_in, s_wave);
     if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
-    for (int64_t e = tid; e < n; e += stride) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
       const double a = h * qi[e];
-      const double yv = y[e] - a;
-      y[e] = yv;
-      part += qn ? qn[e] * yv : yv * yv;
+      const double yv1 = y[e] - a;
+      y[e] = yv1;
+      part += qn ? qn[e] * yv1 : yv1 * yv1;
     }
   }
   const double tot = block_sum(part, s_wave);
@@ -247,12 +261,33 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
                                                            const double* __restrict__ part_in,
                                                            int n_in, double* __restrict__ h_out) {
   __shared__ double s_wave[4];
+  const bool vec = ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(qn)) & 15) == 0;
+  const int64_t npair = vec ? (n >> 1) : 0;
+  const double2* y2 = reinterpret_cast<const double2*>(y);
+  double2* q2 = reinterpret_cast<double2*>(qn);
+  const int64_t round = static_cast<int64_t>(gridDim.x) * kBlock * kMgsPer;
+  int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * kMgsPer + threadIdx.x;
+  double2 yv[kMgsPer];
+#pragma unroll
+  for (int u = 0; u < kMgsPer; ++u)
+    if (base + u * kBlock < npair) yv[u] = y2[base + u * kBlock];
   const double h = sqrt(sum_partials(part_in, n_in, s_wave));
   if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
   // breakdown (h == 0): cgmres/gmres stop (solvers.py:199-202); cgmres_p carries on with the
   // q[j+1] row it never wrote, i.e. zeros (solvers.py:172,376-377) — reproduce that here
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride)
+  while (base - threadIdx.x < npair) {
+#pragma unroll
+    for (int u = 0; u < kMgsPer; ++u) {
+      const int64_t p = base + u * kBlock;
+      if (p < npair) q2[p] = h == 0.0 ? make_double2(0.0, 0.0) : make_double2(yv[u].x / h, yv[u].y / h);
+    }
+    base += round;
+#pragma unroll
+    for (int u = 0; u < kMgsPer; ++u)
+      if (base + u * kBlock < npair) yv[u] = y2[base + u * kBlock];
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;  // scalar tail / unaligned
+  for (int64_t e = 2 * npair + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride)
     qn[e] = h == 0.0 ? 0.0 : y[e] / h;
 }
 
@@ -648,8 +683,10 @@ __global__ __launch_bounds__(kBlock) void constraint_gram_kernel(
     const double* __restrict__ va, const double* __restrict__ Ut, int nvv,
     const double* __restrict__ v0, const double* __restrict__ v1, const double* __restrict__ v2,
     const double* __restrict__ v3, double* __restrict__ partials) {
+  __shared__ double s_acc[64 * (NP + 4)];  // fixed-order wave combine: [lane][NP G | 4 Gv]
   const int lane = threadIdx.x & 63;
-  const int64_t wave = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wid;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kBlock / 64);
   const int64_t per = (n + nwaves - 1) / nwaves;
   const int64_t rbeg = wave * per;
@@ -664,9 +701,27 @@ __global__ __launch_bounds__(kBlock) void constraint_gram_kernel(
   for (int64_t r = rbeg; r < rend; ++r) {
     const double u = on ? Ut[r * np1 + la] : 0.0;
     if (has_m) {
+      // the row's (col, val) pairs: one coalesced load per 64 entries, then broadcast by
+      // readlane so that every gather of the row is independent and in flight together
+      const int s = __builtin_amdgcn_readfirstlane(rp[r]);
+      const int e = __builtin_amdgcn_readfirstlane(rp[r + 1]);
       double w = 0.0;
-      const int s = rp[r], e = rp[r + 1];
-      for (int t = s; t < e; ++t) w += va[t] * Ut[static_cast<int64_t>(ci[t]) * np1 + la];
+      for (int c0 = s; c0 < e; c0 += 64) {
+        const int len = e - c0 < 64 ? e - c0 : 64;
+        const int mc = lane < len ? ci[c0 + lane] : 0;
+        const double mv = lane < len ? va[c0 + lane] : 0.0;
+        for (int t0 = 0; t0 < len; t0 += 8) {
+          double g[8];
+#pragma unroll
+          for (int u8 = 0; u8 < 8; ++u8) {
+            const int col = __builtin_amdgcn_readlane(mc, t0 + u8 < len ? t0 + u8 : 0);
+            g[u8] = t0 + u8 < len ? Ut[static_cast<int64_t>(col) * np1 + la] : 0.0;
+          }
+#pragma unroll
+          for (int u8 = 0; u8 < 8; ++u8)
+            if (t0 + u8 < len) w += readlane_f64(mv, t0 + u8) * g[u8];
+        }
+      }
       if (!on) w = 0.0;
 #pragma unroll
       for (int b = 0; b < NP; ++b) acc[b] += u * readlane_f64(w, b);
@@ -676,15 +731,29 @@ __global__ __launch_bounds__(kBlock) void constraint_gram_kernel(
     if (nvv > 2) gv[2] += u * v2[r];
     if (nvv > 3) gv[3] += u * v3[r];
   }
-  // partial layout per wave: [np1 x np1 G | nvv x np1 Gv]
-  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
-  double* out = partials + wave * stride;
-  if (on) {
-    if (has_m)
+  // combine the block's 4 waves in wave order through LDS (deterministic), one partial per block
+  for (int w = 0; w < kBlock / 64; ++w) {
+    if (wid == w) {
 #pragma unroll
-      for (int b = 0; b < NP; ++b)
-        if (b < np1) out[lane * np1 + b] = acc[b];
-    for (int c = 0; c < nvv; ++c) out[np1 * np1 + c * np1 + lane] = gv[c];
+      for (int b = 0; b < NP; ++b) s_acc[lane * (NP + 4) + b] = (w == 0 ? 0.0 : s_acc[lane * (NP + 4) + b]) + acc[b];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        s_acc[lane * (NP + 4) + NP + c] = (w == 0 ? 0.0 : s_acc[lane * (NP + 4) + NP + c]) + gv[c];
+    }
+    __syncthreads();
+  }
+  // partial layout per block: [np1 x np1 G | nvv x np1 Gv]
+  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
+  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
+  for (int idx = threadIdx.x; idx < stride; idx += kBlock) {
+    if (idx < np1 * np1) {
+      const int a = idx / np1, b = idx - (idx / np1) * np1;
+      out[idx] = has_m ? s_acc[a * (NP + 4) + b] : 0.0;
+    } else {
+      const int k2 = idx - np1 * np1;
+      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
+      out[idx] = s_acc[a * (NP + 4) + NP + c];
+    }
   }
 }
 
@@ -698,7 +767,7 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
   return hipGetLastError();
 }
 
-int constraint_gram_waves() { return kConGramGrid * (kBlock / 64); }
+int constraint_gram_partials() { return kConGramGrid; }
 
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
                                   const double* const* v, double* partials, double* G, hipStream_t s) {
@@ -718,7 +787,7 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
   if (e != hipSuccess) return e;
   const int npairs = np1 * np1 + nvv * np1;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs,
-                     constraint_gram_waves(), partials, G);
+                     constraint_gram_partials(), partials, G);
   return hipGetLastError();
 }
 

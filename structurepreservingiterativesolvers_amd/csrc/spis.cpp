@@ -766,7 +766,7 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                   QuadCon* out) {
   const int np1 = p + 1;
   if (!ws->Ut) HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * std::max<int64_t>(n, 1) * 64));
-  const size_t need = static_cast<size_t>(constraint_gram_waves()) * (np1 * np1 + 4 * np1);
+  const size_t need = static_cast<size_t>(constraint_gram_partials()) * (np1 * np1 + 4 * np1);
   if (c->cg_part_len < need) {
     if (c->cg_part) HIP_TRY(hipFree(c->cg_part));
     HIP_TRY(hipMalloc(&c->cg_part, need * sizeof(double)));

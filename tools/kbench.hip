@@ -1,0 +1,285 @@
+// kbench.hip — kernel-variant micro-benchmark (tuning tool, not part of libspis).
+// Times SpMV and MGS-step variants on the real bench matrix (tools/dump_matrix.py) with HIP
+// events, back-to-back launches like the solver issues them.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
+
+using namespace spis;
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+template <typename T>
+std::vector<T> load(const std::string& p, size_t n) {
+  std::vector<T> v(n);
+  FILE* f = fopen(p.c_str(), "rb");
+  if (!f || fread(v.data(), sizeof(T), n, f) != n) {
+    fprintf(stderr, "cannot read %s\n", p.c_str());
+    exit(1);
+  }
+  fclose(f);
+  return v;
+}
+
+static void blocks(int64_t n, const int32_t* rp, int item_cap, int row_cap, int nnz_cap, std::vector<int32_t>& blk) {
+  blk.clear();
+  blk.push_back(0);
+  int64_t rows = 0, nnz = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t len = rp[r + 1] - rp[r];
+    if (rows > 0 && (rows + 1 > row_cap || nnz + len > nnz_cap || rows + 1 + nnz + len > item_cap)) {
+      blk.push_back(static_cast<int32_t>(r));
+      rows = nnz = 0;
+    }
+    ++rows;
+    nnz += len;
+  }
+  blk.push_back(static_cast<int32_t>(n));
+}
+
+// ---- SpMV variant: all val/col loads of the block issued first (fixed trip count) ------------
+template <int EPI, int PER>
+__global__ __launch_bounds__(kBlock) void spmv_v1(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                  const double* __restrict__ va, const int32_t* __restrict__ blk_row,
+                                                  int n_blk, const double* __restrict__ x, double* __restrict__ y,
+                                                  const double* __restrict__ aux, double* __restrict__ partials) {
+  __shared__ double s_prod[kBlock * PER];
+  __shared__ double s_wave[4];
+  double part = 0.0;
+  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int r0 = blk_row[blk];
+    const int r1 = blk_row[blk + 1];
+    const int nz0 = rp[r0];
+    const int nnz = rp[r1] - nz0;
+    int cols[PER];
+    double vals[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      cols[u] = i < nnz ? ci[nz0 + i] : 0;
+      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+    }
+    double xs[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) xs[u] = x[cols[u]];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < nnz) s_prod[i] = vals[u] * xs[u];
+    }
+    __syncthreads();
+    const int r = r0 + threadIdx.x;
+    if (r < r1) {
+      const int s = rp[r] - nz0;
+      const int e = rp[r + 1] - nz0;
+      double sum = 0.0;
+      for (int t = s; t < e; ++t) sum += s_prod[t];
+      if (EPI == kEpiDot) {
+        y[r] = sum;
+        part += aux[r] * sum;
+      } else {
+        y[r] = sum;
+      }
+    }
+    __syncthreads();
+  }
+  if (EPI != kEpiPlain) {
+    const double tot = block_sum(part, s_wave);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+  }
+}
+
+// ---- MGS variant: PER pairs per thread, all loads first ---------------------------------------
+template <int PER>
+__global__ __launch_bounds__(kBlock) void mgs_v1(int64_t n, double* __restrict__ y, const double* __restrict__ qi,
+                                                 const double* __restrict__ qn, const double* __restrict__ part_in,
+                                                 int n_in, double* __restrict__ part_out, double* __restrict__ h_out) {
+#pragma clang fp contract(off)
+  __shared__ double s_wave[4];
+  const int64_t npair = n >> 1;
+  double2* y2 = reinterpret_cast<double2*>(y);
+  const double2* q2 = reinterpret_cast<const double2*>(qi);
+  const double2* n2 = reinterpret_cast<const double2*>(qn);
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock * PER + threadIdx.x;
+  double2 yv[PER], qv[PER], nv[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int64_t p = base + u * kBlock;
+    if (p < npair) {
+      qv[u] = q2[p];
+      yv[u] = y2[p];
+      nv[u] = n2[p];
+    }
+  }
+  const double h = sum_partials(part_in, n_in, s_wave);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+  double part = 0.0;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int64_t p = base + u * kBlock;
+    if (p < npair) {
+      const double a0 = h * qv[u].x, a1 = h * qv[u].y;
+      yv[u].x = yv[u].x - a0;
+      yv[u].y = yv[u].y - a1;
+      y2[p] = yv[u];
+      part += nv[u].x * yv[u].x;
+      part += nv[u].y * yv[u].y;
+    }
+  }
+  const double tot = block_sum(part, s_wave);
+  if (threadIdx.x == 0) part_out[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void copy2_kernel(int64_t m, const double2* __restrict__ x, double2* __restrict__ y) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += static_cast<int64_t>(gridDim.x) * kBlock)
+    y[i] = x[i];
+}
+__global__ __launch_bounds__(kBlock) void read2_kernel(int64_t m, const double2* __restrict__ x, double* __restrict__ out) {
+  double a = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const double2 v = x[i];
+    a += v.x + v.y;
+  }
+  if (a == 12345.678) out[0] = a;
+}
+
+int main(int argc, char** argv) {
+  const std::string dir = argc > 1 ? argv[1] : "/tmp/kbench_mat";
+  auto shp = load<int64_t>(dir + "/shape.bin", 2);
+  const int64_t n = shp[0], nnz = shp[1];
+  auto rp = load<int32_t>(dir + "/indptr.bin", n + 1);
+  auto ci = load<int32_t>(dir + "/indices.bin", nnz);
+  auto va = load<double>(dir + "/data.bin", nnz);
+  int32_t *drp, *dci, *dblk;
+  double *dva, *dx, *dy, *dpart, *dpart2, *dh;
+  CK(hipMalloc(&drp, 4 * (n + 1)));
+  CK(hipMalloc(&dci, 4 * nnz));
+  CK(hipMalloc(&dva, 8 * nnz));
+  CK(hipMemcpy(drp, rp.data(), 4 * (n + 1), hipMemcpyHostToDevice));
+  CK(hipMemcpy(dci, ci.data(), 4 * nnz, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dva, va.data(), 8 * nnz, hipMemcpyHostToDevice));
+  const int64_t pitch = (n + 63) / 64 * 64;
+  const int K = 31;
+  double* dQ;
+  CK(hipMalloc(&dQ, 8 * pitch * K));
+  CK(hipMalloc(&dx, 8 * pitch));
+  CK(hipMalloc(&dy, 8 * pitch));
+  CK(hipMalloc(&dpart, 8 * 8192));
+  CK(hipMalloc(&dpart2, 8 * 8192));
+  CK(hipMalloc(&dh, 8 * 64));
+  std::vector<double> hx(pitch);
+  for (int64_t i = 0; i < pitch; ++i) hx[i] = i < n ? 1e-3 * ((i * 7919) % 1000) : 0.0;
+  for (int k = 0; k < K; ++k) CK(hipMemcpy(dQ + k * pitch, hx.data(), 8 * pitch, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dx, hx.data(), 8 * pitch, hipMemcpyHostToDevice));
+  CK(hipMemset(dpart, 0, 8 * 8192));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double S = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
+  auto timeit = [&](const char* name, int reps, double bytes, auto&& fn) {
+    for (int i = 0; i < 3; ++i) fn();
+    CK(hipStreamSynchronize(s));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps; ++i) fn();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / reps;
+    printf("%-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
+           100.0 * bytes / (us * 1e-6) / 8e12);
+  };
+  // ---- SpMV
+  for (int cap : {1024, 2048}) {
+    std::vector<int32_t> blk;
+    blocks(n, rp.data(), cap, 256, 2048, blk);
+    CK(hipMalloc(&dblk, 4 * blk.size()));
+    CK(hipMemcpy(dblk, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+    const int nb = static_cast<int>(blk.size()) - 1;
+    CsrView A{n, drp, dci, dva, dblk, nb};
+    char nm[128];
+    for (int g : {1024, 2048, 4096, nb}) {
+      const int gg = g < nb ? g : nb;
+      snprintf(nm, sizeof nm, "spmv cur  items=%d grid=%d", cap, gg);
+      timeit(nm, 50, S, [&] { (void)launch_spmv(A, kEpiDot, dx, dy, dQ, dpart, gg, s); });
+      if (cap == 2048) {
+        snprintf(nm, sizeof nm, "spmv v1<8> items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 8>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+      } else {
+        snprintf(nm, sizeof nm, "spmv v1<4> items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 4>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+      }
+    }
+    CK(hipFree(dblk));
+  }
+  // ---- MGS chain of 30 steps (y, q_i, q_{i+1})
+  const double mgsB = 32.0 * n;
+  for (int g : {512, 1024, 2048}) {
+    char nm[128];
+    snprintf(nm, sizeof nm, "mgs cur grid=%d (per step)", g);
+    timeit(nm, 1, mgsB * 30, [&] {
+      for (int i = 0; i < 30; ++i)
+        (void)launch_mgs_step(n, dy, dQ + i * pitch, dQ + (i + 1) * pitch, (i & 1) ? dpart2 : dpart, g,
+                              (i & 1) ? dpart : dpart2, dh + i, g, s);
+    });
+  }
+  const int64_t npair = n / 2;
+  {
+    const int g2 = static_cast<int>((npair + 256 * 2 - 1) / (256 * 2));
+    const int g4 = static_cast<int>((npair + 256 * 4 - 1) / (256 * 4));
+    const int g1 = static_cast<int>((npair + 256 - 1) / 256);
+    timeit("mgs v1<1> (per step x30)", 1, mgsB * 30, [&] {
+      for (int i = 0; i < 30; ++i)
+        hipLaunchKernelGGL(mgs_v1<1>, dim3(g1), dim3(kBlock), 0, s, n, dy, dQ + i * pitch, dQ + (i + 1) * pitch,
+                           (i & 1) ? dpart2 : dpart, 1024, (i & 1) ? dpart : dpart2, dh + i);
+    });
+    timeit("mgs v1<2> (per step x30)", 1, mgsB * 30, [&] {
+      for (int i = 0; i < 30; ++i)
+        hipLaunchKernelGGL(mgs_v1<2>, dim3(g2), dim3(kBlock), 0, s, n, dy, dQ + i * pitch, dQ + (i + 1) * pitch,
+                           (i & 1) ? dpart2 : dpart, 1024, (i & 1) ? dpart : dpart2, dh + i);
+    });
+    timeit("mgs v1<4> (per step x30)", 1, mgsB * 30, [&] {
+      for (int i = 0; i < 30; ++i)
+        hipLaunchKernelGGL(mgs_v1<4>, dim3(g4), dim3(kBlock), 0, s, n, dy, dQ + i * pitch, dQ + (i + 1) * pitch,
+                           (i & 1) ? dpart2 : dpart, 1024, (i & 1) ? dpart : dpart2, dh + i);
+    });
+  }
+  // streaming copy ceiling on 2 GiB (far beyond the 256 MiB Infinity Cache), 16 B/lane
+  {
+    const int64_t big = int64_t(1) << 27;  // doubles per buffer (1 GiB)
+    double *bx, *by;
+    CK(hipMalloc(&bx, 8 * big));
+    CK(hipMalloc(&by, 8 * big));
+    CK(hipMemset(bx, 0, 8 * big));
+    timeit("copy ceiling 1 GiB -> 1 GiB (double2)", 10, 16.0 * big, [&] {
+      hipLaunchKernelGGL(copy2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                         reinterpret_cast<const double2*>(bx), reinterpret_cast<double2*>(by));
+    });
+    timeit("read ceiling 1 GiB (double2, sum)", 10, 8.0 * big, [&] {
+      hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                         reinterpret_cast<const double2*>(bx), dpart);
+    });
+    CK(hipFree(bx));
+    CK(hipFree(by));
+  }
+  printf("n=%lld nnz=%lld S=%.1f MB\n", (long long)n, (long long)nnz, S / 1e6);
+  return 0;
+}
