@@ -95,12 +95,14 @@ def main():
     ap.add_argument("--tol", type=float, default=1e-19)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-distributed", action="store_true",
+                    help="use the row-partitioned RCCL path even for one rank (plumbing check)")
     ap.add_argument("--prof-period", type=int, default=5,
                     help="time every n-th iteration's kernels with HIP events inside the timed region")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
+    if args.gpus > 1 or world > 1 or args.force_distributed:
         from structurepreservingiterativesolvers_amd import distributed
 
         return distributed.bench_main(args, METRIC)

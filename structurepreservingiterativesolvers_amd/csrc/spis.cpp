@@ -469,7 +469,9 @@ extern "C" int spis_comm_unique_id(uint8_t id_out[128]) {
 extern "C" int spis_comm_init(spis_context* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
   ABI_GUARD({
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPIS_ERR_ARG, "bad comm args");
-    if (nranks == 1) return SPIS_OK;  // single rank: no collectives
+    if (c->comm) return fail(SPIS_ERR_STATE, "context already has a communicator");
+    // a 1-rank communicator is created too: it switches the context to the distributed code
+    // path (fixed grids, all-reduces, halo exchanges — e.g. to itself), which tests use
     HIP_TRY(hipSetDevice(c->device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, 128);

@@ -39,9 +39,17 @@ class Context:
         _lib.check(self.L.spis_context_synchronize(self.handle), "spis_context_synchronize")
 
     def close(self):
+        """Destroy the context; device objects still alive become inert (their finalizers
+        see the closed context and do nothing)."""
         if self.handle:
             self.L.spis_context_destroy(self.handle)
             self.handle = None
+
+
+def _release(ctx, fn_name, handle):
+    """Finalizer: release a device object unless its context was already destroyed."""
+    if ctx.handle:
+        getattr(ctx.L, fn_name)(*([ctx.handle] if fn_name == "spis_free" else []), handle)
 
 
 _CONTEXTS: dict[int, Context] = {}
@@ -72,7 +80,7 @@ class DeviceBuffer:
         p = C.c_void_p()
         _lib.check(ctx.L.spis_malloc(ctx.handle, 8 * max(self.n, 1), C.byref(p)), "spis_malloc")
         self.ptr = p.value
-        self._fin = weakref.finalize(self, ctx.L.spis_free, ctx.handle, C.c_void_p(self.ptr))
+        self._fin = weakref.finalize(self, _release, ctx, "spis_free", C.c_void_p(self.ptr))
 
     def upload(self, arr):
         a = np.ascontiguousarray(arr, dtype=np.float64)
@@ -140,7 +148,7 @@ class DeviceMatrix:
             "spis_csr_upload",
         )
         self.handle = h
-        self._fin = weakref.finalize(self, ctx.L.spis_matrix_destroy, h)
+        self._fin = weakref.finalize(self, _release, ctx, "spis_matrix_destroy", h)
         info = (C.c_int64 * 8)()
         _lib.check(ctx.L.spis_matrix_info(h, info), "spis_matrix_info")
         self.n_blocks = int(info[3])

@@ -118,9 +118,11 @@ _ZERO_CACHE: dict = {}
 
 
 def _is_zero_matrix(M):
-    """O(1) for an empty sparse matrix; O(nnz) (cached per object) otherwise."""
+    """O(1) for an empty sparse matrix or a device matrix; O(nnz) (cached per object) otherwise."""
     if M is None:
         return True
+    if isinstance(M, DeviceMatrix):
+        return M.all_zero or M.nnz == 0
     if sps.issparse(M):
         if M.nnz == 0:
             return True
@@ -138,14 +140,19 @@ def _constraint_desc(const, n, ctx):
     M = getattr(const, "M", None)
     Mh = None
     if not _is_zero_matrix(M):
-        dm = device_matrix(M if sps.issparse(M) else sps.csr_matrix(M), ctx=ctx)
+        dm = M if isinstance(M, DeviceMatrix) else device_matrix(M if sps.issparse(M) else sps.csr_matrix(M), ctx=ctx)
         if dm.shape[0] != n:
             raise ValueError(f"constraint matrix has {dm.shape[0]} rows, expected {n}")
         keep.append(dm)
         Mh = dm.handle.value
     v = getattr(const, "v", None)
     vh = None
-    if v is not None:
+    if isinstance(v, DeviceVector):
+        if len(v) != n:
+            raise ValueError(f"constraint vector has {len(v)} entries, expected {n}")
+        keep.append(v)
+        vh = v.ptr
+    elif v is not None:
         v = np.asarray(v, dtype=np.float64).reshape(-1)
         if np.any(v):
             vd = device_vector(v, ctx=ctx)
@@ -174,7 +181,9 @@ class IterateList(collections.abc.Sequence):
             self._cache[count - 1] = final
         self._fin = None
         if ws:
-            self._fin = __import__("weakref").finalize(self, ctx.L.spis_workspace_release, ws)
+            from .device import _release
+
+            self._fin = __import__("weakref").finalize(self, _release, ctx, "spis_workspace_release", C.c_void_p(ws))
 
     def __len__(self):
         return self._count
@@ -328,7 +337,8 @@ def _as_slsqp(cc):
 # the call
 # ------------------------------------------------------------------------------------------------
 def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
-    ctx = get_context()
+    # a device matrix carries its context (distributed rank / communicator); else the default one
+    ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
     Ad = device_matrix(A, ctx=ctx)
     n = Ad.shape[0]
     device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)

@@ -313,3 +313,56 @@ def test_full_size_swe_properties(spis):
     assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-12 * abs(dic["m0"])
     assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
     np.testing.assert_allclose(res[-1], np.linalg.norm(A @ x - dic["b"]), rtol=1e-10)
+
+
+def test_distributed_code_path_self_halo(spis):
+    """The RCCL data path on one GPU: a 1-rank communicator (fixed-size partial arrays +
+    ncclAllReduce) and an operator whose last ~20% columns are declared ghosts received from
+    rank 0 itself (gather + grouped ncclSend/ncclRecv), constraints through the generic
+    per-column halo path.  Must reproduce the single-GPU solve."""
+    import ctypes as C
+
+    from structurepreservingiterativesolvers_amd import _lib, solvers
+    from structurepreservingiterativesolvers_amd.device import Context, DeviceMatrix, DeviceVector
+    from structurepreservingiterativesolvers_amd.distributed import HaloPlan, _DevCon
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=16)
+    A = dic["A"].tocsr()
+    n = A.shape[0]
+    x0 = np.zeros(n)
+    xs, ds = swe_ls.cgmresWrapper(dic, x0=x0, k=20, tol=1e-19)
+
+    ctx = Context(0)
+    uid = (C.c_uint8 * 128)()
+    _lib.check(ctx.L.spis_comm_unique_id(uid), "spis_comm_unique_id")
+    _lib.check(ctx.L.spis_comm_init(ctx.handle, 1, 0, uid), "spis_comm_init")
+
+    def self_halo(M):
+        M = M.tocsr()
+        cut = int(0.8 * n)
+        ghost_cols = np.unique(M.indices[M.indices >= cut])
+        idx = M.indices.astype(np.int64).copy()
+        g = idx >= cut
+        idx[g] = n + np.searchsorted(ghost_cols, idx[g])
+        loc = sps.csr_matrix((M.data, idx.astype(np.int32), M.indptr.astype(np.int32)), shape=(n, n + len(ghost_cols)))
+        plan = HaloPlan([0], [len(ghost_cols)], ghost_cols.astype(np.int32), [len(ghost_cols)], len(ghost_cols))
+        return DeviceMatrix(ctx, loc, halo=plan)
+
+    Ad = self_halo(A)
+    assert Ad.n_ghost > 0
+    bd = DeviceVector.from_host(dic["b"], ctx=ctx)
+    x0d = DeviceVector.from_host(x0, ctx=ctx)
+    cons = [_DevCon(None, DeviceVector.from_host(dic["omega"], ctx=ctx), -dic["m0"]),
+            _DevCon(self_halo(dic["L"]), None, -dic["e0"])]
+    r = solvers._run(_lib.CGMRES, Ad, bd, x0d, 20, 1e-19, 10, cons, None, None)
+    x = r["final"].numpy()
+    assert r["steps"] == ds["steps"]
+    assert r["x"].trace == ds["x"].trace
+    np.testing.assert_allclose(x, xs, rtol=0, atol=1e-10 * np.linalg.norm(xs))
+    # fixed-size partial arrays change the summation order: late residuals (~1e-11) differ in
+    # their last digits, i.e. at ~1e-14 of r0
+    np.testing.assert_allclose(r["res"][1:], ds["res"], rtol=1e-8, atol=1e-12 * r["res"][0])
+    del r, Ad, bd, x0d, cons  # release device objects before the context goes
+    ctx.close()
