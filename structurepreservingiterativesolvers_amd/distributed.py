@@ -246,9 +246,15 @@ class DistributedSystem:
         return self.part.from_locals(parts)
 
 
-class _DevCon:
+class DeviceConstraint:
+    """A class-form constraint ``1/2 X'MX + v.X + c`` whose ``M`` is a (distributed)
+    DeviceMatrix or None and ``v`` a DeviceVector or None (solvers.py:22-36)."""
+
     def __init__(self, M, v, c):
         self.M, self.v, self.c = M, v, c
+
+
+_DevCon = DeviceConstraint
 
 
 def swe_fields(M):
@@ -276,8 +282,8 @@ def bench_main(args, metric):
     bd = sysd.vector(dic["b"])
     x0d = DeviceVector.from_host(np.zeros(sysd.n_local), ctx=ctx)
     conlist = [
-        _DevCon(None, sysd.vector(dic["omega"]), -dic["m0"]),
-        _DevCon(sysd.matrix(dic["L"]), None, -dic["e0"]),
+        DeviceConstraint(None, sysd.vector(dic["omega"]), -dic["m0"]),
+        DeviceConstraint(sysd.matrix(dic["L"]), None, -dic["e0"]),
     ]
     del dic
 
