@@ -50,7 +50,9 @@ static void blocks(int64_t n, const int32_t* rp, int item_cap, int row_cap, int 
 }
 
 // ---- SpMV variant: all val/col loads of the block issued first (fixed trip count) ------------
-template <int EPI, int PER>
+// SWZ 0: blk = blockIdx (grid-stride); 1: XCD-swizzled logical id (grid-stride); 2: swizzled id,
+// contiguous chunk of row blocks per workgroup.  NT: nontemporal val/col loads.
+template <int EPI, int PER, int SWZ = 0, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmv_v1(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                                   const double* __restrict__ va, const int32_t* __restrict__ blk_row,
                                                   int n_blk, const double* __restrict__ x, double* __restrict__ y,
@@ -58,7 +60,17 @@ __global__ __launch_bounds__(kBlock) void spmv_v1(const int32_t* __restrict__ rp
   __shared__ double s_prod[kBlock * PER];
   __shared__ double s_wave[4];
   double part = 0.0;
-  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+  const int G = gridDim.x;
+  int L = blockIdx.x;
+  if (SWZ && (G & 7) == 0) L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  int b0 = L, b1 = n_blk, bs = G;
+  if (SWZ == 2) {
+    const int c = (n_blk + G - 1) / G;
+    b0 = L * c;
+    b1 = min(n_blk, b0 + c);
+    bs = 1;
+  }
+  for (int blk = b0; blk < b1; blk += bs) {
     const int r0 = blk_row[blk];
     const int r1 = blk_row[blk + 1];
     const int nz0 = rp[r0];
@@ -68,8 +80,13 @@ __global__ __launch_bounds__(kBlock) void spmv_v1(const int32_t* __restrict__ rp
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int i = threadIdx.x + u * kBlock;
-      cols[u] = i < nnz ? ci[nz0 + i] : 0;
-      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+      if (NT) {
+        cols[u] = i < nnz ? __builtin_nontemporal_load(ci + nz0 + i) : 0;
+        vals[u] = i < nnz ? __builtin_nontemporal_load(va + nz0 + i) : 0.0;
+      } else {
+        cols[u] = i < nnz ? ci[nz0 + i] : 0;
+        vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+      }
     }
     double xs[PER];
 #pragma unroll
@@ -155,6 +172,24 @@ __global__ __launch_bounds__(kBlock) void read2_kernel(int64_t m, const double2*
   if (a == 12345.678) out[0] = a;
 }
 
+// calibration streams for PMC byte counters: known bytes, fixed access width per lane
+__global__ __launch_bounds__(kBlock) void calib_read8(int64_t m, const double* __restrict__ x, double* __restrict__ out) {
+  double a = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += static_cast<int64_t>(gridDim.x) * kBlock)
+    a += x[i];
+  if (a == 12345.678) out[0] = a;
+}
+__global__ __launch_bounds__(kBlock) void calib_read4(int64_t m, const int32_t* __restrict__ x, double* __restrict__ out) {
+  int64_t a = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += static_cast<int64_t>(gridDim.x) * kBlock)
+    a += x[i];
+  if (a == 1234567) out[0] = 1.0;
+}
+__global__ __launch_bounds__(kBlock) void calib_write8(int64_t m, double* __restrict__ y) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += static_cast<int64_t>(gridDim.x) * kBlock)
+    y[i] = 1.0;
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp/kbench_mat";
   auto shp = load<int64_t>(dir + "/shape.bin", 2);
@@ -190,6 +225,34 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double S = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
+  if (argc > 2 && std::string(argv[2]) == "pmc") {
+    // PMC mode: 3 calibration streams of 1 GiB each (known bytes), then 5 Arnoldi SpMVs
+    const int64_t m8 = int64_t(1) << 27;
+    double* big;
+    CK(hipMalloc(&big, 8 * m8));
+    CK(hipMemset(big, 0, 8 * m8));
+    hipLaunchKernelGGL(calib_read8, dim3(4096), dim3(kBlock), 0, s, m8, big, dpart);
+    hipLaunchKernelGGL(calib_read4, dim3(4096), dim3(kBlock), 0, s, 2 * m8, reinterpret_cast<const int32_t*>(big), dpart);
+    hipLaunchKernelGGL(calib_write8, dim3(4096), dim3(kBlock), 0, s, m8, big);
+    CK(hipStreamSynchronize(s));
+    std::vector<int32_t> blk;
+    blocks(n, rp.data(), 2048, 256, 2048, blk);
+    CK(hipMalloc(&dblk, 4 * blk.size()));
+    CK(hipMemcpy(dblk, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+    CsrView A{n, drp, dci, dva, dblk, static_cast<int>(blk.size()) - 1};
+    const int g = A.n_blk < 2048 ? A.n_blk : 2048;
+    for (int i = 0; i < 5; ++i) CK(launch_spmv(A, kEpiDot, dx, dy, dQ, dpart, g, s));
+    const int nb = A.n_blk;
+    for (int i = 0; i < 5; ++i)
+      hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1, false>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+    for (int i = 0; i < 5; ++i)
+      hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 2, false>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+    for (int i = 0; i < 5; ++i)
+      hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1, true>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+    CK(hipStreamSynchronize(s));
+    printf("pmc mode: calib 1 GiB read8 / read4 / write8, then 5 x spmv (S = %.1f MB)\n", S / 1e6);
+    return 0;
+  }
   auto timeit = [&](const char* name, int reps, double bytes, auto&& fn) {
     for (int i = 0; i < 3; ++i) fn();
     CK(hipStreamSynchronize(s));
@@ -220,6 +283,22 @@ int main(int argc, char** argv) {
         snprintf(nm, sizeof nm, "spmv v1<8> items=%d grid=%d", cap, gg);
         timeit(nm, 50, S, [&] {
           hipLaunchKernelGGL((spmv_v1<kEpiDot, 8>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+        snprintf(nm, sizeof nm, "spmv v1<8> swz1 items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+        snprintf(nm, sizeof nm, "spmv v1<8> swz2 items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 2>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+        snprintf(nm, sizeof nm, "spmv v1<8> swz1 nt items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1, true>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
+        });
+        snprintf(nm, sizeof nm, "spmv v1<8> nt items=%d grid=%d", cap, gg);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 0, true>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
         });
       } else {
         snprintf(nm, sizeof nm, "spmv v1<4> items=%d grid=%d", cap, gg);
