@@ -143,6 +143,9 @@ int spis_matrix_destroy(spis_matrix* A);
 int spis_matrix_info(spis_matrix* A, int64_t info[8]);
 
 /* ---- vectors / BLAS-1 primitives (device pointers, n = local length) -------- */
+/* spis_malloc: zero-filled block, ordered on the context stream (no host wait); blocks come from
+ * a per-context stream-ordered cache.  spis_free returns a block to that cache (it must come
+ * from spis_malloc of the same context); blocks are released at spis_context_destroy. */
 int spis_malloc(spis_context* ctx, int64_t bytes, void** dev_out);
 int spis_free(spis_context* ctx, void* dev);
 int spis_memcpy_h2d(spis_context* ctx, void* dst_dev, const void* src_host, int64_t bytes);

@@ -18,7 +18,7 @@ constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
 constexpr int kGramMaxVec = 64;  // max vectors on either side of one Gram launch (<= 256 4x4 tiles)
 constexpr int kYArg = 128;
 constexpr int kMgsPer = 4;       // 16-B pairs per lane per round in MGS / normalise (loads issued first)
-constexpr int kConGramGrid = 1024;  // workgroups of the fused constraint Gram (4 waves each)       // GEMV coefficients passed by value up to this p
+constexpr int kConGramGrid = 1024;  // max workgroups (partial slots) of the fused constraint Gram      // GEMV coefficients passed by value up to this p
 
 struct YArg {
   double v[kYArg];

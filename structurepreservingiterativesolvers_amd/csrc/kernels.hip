@@ -640,13 +640,14 @@ hipError_t launch_gram(int64_t n, int nu, const double* const* U, int nv, const 
 // K7: fused constraint reduction (solvers.py:33-36 for all constraints of a step at once).
 //   U = [z_0 .. z_{p-1}, x0]           (np1 = p + 1 columns)
 //   transpose_basis_kernel:  Ut (N x np1, row-major) = U^T, via LDS tiles of 64 rows
-//   constraint_gram_kernel:  one wave per row r (contiguous row chunks per wave, banded
-//     gathers stay in L1/L2); lane a < np1 forms w_a = (M U)_{r,a} = sum_nz M_rc Ut[c][a]
-//     with one coalesced 8*np1-byte gather per nonzero, then accumulates
-//       G[a][b] += Ut[r][a] * w_b          (w_b broadcast by v_readlane: scalar, no LDS)
-//       Gv[c][a] += Ut[r][a] * v_c[r]      (up to 4 linear terms v_c)
-//     and writes one partial per wave; the partials are summed by gram_reduce_kernel in wave
-//     order (deterministic).  G = U^T M U gives term2 = G[:p,:p]/2, x0'MZ = G[p,:p],
+//   constraint_gram_kernel:  16-row chunks; XCD group g = blockIdx % 8 owns a contiguous eighth
+//     of the rows and deals its chunks round-robin to its waves (compact L2 window).  Per chunk
+//     the wave streams the contiguous nonzeros with 16 independent 8*np1-byte Ut-row gathers in
+//     flight (lane a < np1 forms w_a = (M U)_{r,a}), stores each row's w to an LDS tile, then
+//       G[a][b] += sum_i Ut[r0+i][a] * W[i][b]     (W rows read by LDS broadcast)
+//       Gv[c][a] += Ut[r][a] * v_c[r]             (up to 4 linear terms v_c)
+//     and each block writes one partial (its 4 waves combined in wave order); gram_reduce_kernel
+//     sums the block partials in block order (deterministic).  G = U^T M U gives term2 = G[:p,:p]/2, x0'MZ = G[p,:p],
 //     x0'Mx0 = G[p,p]; Gv gives v'Z and v.x0.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int p,
@@ -677,82 +678,195 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
 }
 
+constexpr int kConRows = 16;   // rows per chunk of the fused constraint Gram
+constexpr int kConBatch = 16;  // gather instructions in flight per wave (x P nonzeros each)
+constexpr int kConWin = 256;   // nonzeros staged in LDS per window
+
+// NP = column slots (32 or 64); P = 64 / NP nonzeros gathered per wave instruction (lane half h
+// takes nonzero t = P*q + h of a batch); each lane keeps SEG = NP / P entries of its G row.
 template <int NP>
-__global__ __launch_bounds__(kBlock) void constraint_gram_kernel(
+__global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kernel(
     int64_t n, int np1, const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
     const double* __restrict__ va, const double* __restrict__ Ut, int nvv,
     const double* __restrict__ v0, const double* __restrict__ v1, const double* __restrict__ v2,
     const double* __restrict__ v3, double* __restrict__ partials) {
-  __shared__ double s_acc[64 * (NP + 4)];  // fixed-order wave combine: [lane][NP G | 4 Gv]
+  constexpr int P = 64 / NP;
+  constexpr int SEG = NP / P;
+  constexpr int NW = kBlock / 64;
+  __shared__ __attribute__((aligned(16))) double s_w[NW][kConRows][NP];  // per-wave W tile
+  __shared__ double s_val[NW][kConWin];
+  __shared__ int s_col[NW][kConWin];
+  __shared__ double s_acc[64 * (SEG + 4)];  // fixed-order wave combine: [lane][SEG G | 4 Gv]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wave = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wid;
-  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kBlock / 64);
-  const int64_t per = (n + nwaves - 1) / nwaves;
-  const int64_t rbeg = wave * per;
-  const int64_t rend = rbeg + per < n ? rbeg + per : n;
-  const bool on = lane < np1;
-  const int la = on ? lane : 0;
-  double acc[NP];
-#pragma unroll
-  for (int b = 0; b < NP; ++b) acc[b] = 0.0;
-  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  const int la = lane % NP;  // column a of U this lane gathers / owns
+  const int h = lane / NP;   // nonzero slot within a gather instruction
+  const bool on = la < np1;
+  const int lac = on ? la : 0;
+  // XCD group = blockIdx % 8 (dispatch order; speed only, never correctness): each group owns a
+  // contiguous eighth of the rows, its waves take 16-row chunks round-robin, so the group's
+  // active window of Ut rows (and their banded column neighbourhood) stays in its own L2
+  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int grp = blockIdx.x % ngrp;
+  const int64_t wpg = static_cast<int64_t>(gridDim.x / ngrp) * NW;  // waves per group
+  const int64_t gw = static_cast<int64_t>(blockIdx.x / ngrp) * NW + wid;
+  const int64_t rpg = (n + ngrp - 1) / ngrp;
+  const int64_t g0 = grp * rpg;
+  const int64_t g1 = g0 + rpg < n ? g0 + rpg : n;
+  const int64_t nch = g1 > g0 ? (g1 - g0 + kConRows - 1) / kConRows : 0;
   const bool has_m = rp != nullptr;
-  for (int64_t r = rbeg; r < rend; ++r) {
-    const double u = on ? Ut[r * np1 + la] : 0.0;
-    if (has_m) {
-      // the row's (col, val) pairs: one coalesced load per 64 entries, then broadcast by
-      // readlane so that every gather of the row is independent and in flight together
-      const int s = __builtin_amdgcn_readfirstlane(rp[r]);
-      const int e = __builtin_amdgcn_readfirstlane(rp[r + 1]);
-      double w = 0.0;
-      for (int c0 = s; c0 < e; c0 += 64) {
-        const int len = e - c0 < 64 ? e - c0 : 64;
-        const int mc = lane < len ? ci[c0 + lane] : 0;
-        const double mv = lane < len ? va[c0 + lane] : 0.0;
-        for (int t0 = 0; t0 < len; t0 += 8) {
-          double g[8];
+  double acc[SEG];
 #pragma unroll
-          for (int u8 = 0; u8 < 8; ++u8) {
-            const int col = __builtin_amdgcn_readlane(mc, t0 + u8 < len ? t0 + u8 : 0);
-            g[u8] = t0 + u8 < len ? Ut[static_cast<int64_t>(col) * np1 + la] : 0.0;
+  for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double (*W)[NP] = s_w[wid];
+  double* sv = s_val[wid];
+  int* sc = s_col[wid];
+  auto chunk_rows = [&](int64_t ch) { return static_cast<int>(g1 - (g0 + ch * kConRows) < kConRows ? g1 - (g0 + ch * kConRows) : kConRows); };
+  // row pointers of the wave's first chunk; later chunks' are prefetched one chunk ahead
+  int rpl_next = 0;
+  if (has_m && gw < nch) {
+    const int nr = chunk_rows(gw);
+    rpl_next = rp[g0 + gw * kConRows + (lane <= nr ? lane : nr)];
+  }
+  for (int64_t ch = gw; ch < nch; ch += wpg) {
+    const int64_t r0 = g0 + ch * kConRows;
+    const int nr = chunk_rows(ch);
+    const int rpl = rpl_next;
+    if (has_m && ch + wpg < nch) {  // next chunk's row pointers (issued before anything else)
+      const int nr2 = chunk_rows(ch + wpg);
+      rpl_next = rp[r0 + wpg * kConRows + (lane <= nr2 ? lane : nr2)];
+    }
+    const int nz0 = has_m ? __builtin_amdgcn_readlane(rpl, 0) : 0;
+    const int nz1 = has_m ? __builtin_amdgcn_readlane(rpl, nr) : 0;
+    // the first window's (col, val) loads go out first (vmcnt retires in order), clamped and
+    // unconditional so the compiler keeps them in flight together
+    constexpr int kStage = kConWin / 64;
+    int cst[kStage];
+    double vst[kStage];
+    auto stage = [&](int wb, int wl) {
+#pragma unroll
+      for (int q = 0; q < kStage; ++q) {
+        const int e = q * 64 + lane;
+        const int idx = wb + (e < wl ? e : 0);
+        cst[q] = ci[idx];
+        vst[q] = va[idx];
+      }
+    };
+    auto commit = [&]() {
+#pragma unroll
+      for (int q = 0; q < kStage; ++q) {
+        sc[q * 64 + lane] = cst[q];
+        sv[q * 64 + lane] = vst[q];
+      }
+      __builtin_amdgcn_wave_barrier();
+    };
+    if (nz1 > nz0) stage(nz0, nz1 - nz0 < kConWin ? nz1 - nz0 : kConWin);
+    // rows of U for the update (unconditional, clamped: in flight during the gathers)
+    double u[kConRows];
+#pragma unroll
+    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * np1 + lac];
+    double vc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (lane < nr) {
+      if (nvv > 0) vc[0] = v0[r0 + lane];
+      if (nvv > 1) vc[1] = v1[r0 + lane];
+      if (nvv > 2) vc[2] = v2[r0 + lane];
+      if (nvv > 3) vc[3] = v3[r0 + lane];
+    }
+    if (has_m) {
+      // phase 1: w_a = sum_c M_rc Ut[c][a] per row over the chunk's contiguous nonzeros;
+      // each row's w goes to the wave's LDS tile at the row end (empty rows store 0)
+      int row = 0;
+      int row_end = __builtin_amdgcn_readlane(rpl, 1);
+      double w = 0.0;
+      auto flush = [&]() {
+        double wt = w;
+        if (P == 2) wt += __shfl_xor(w, 32);
+        if (h == 0) W[row][la] = wt;
+        w = 0.0;
+        ++row;
+        row_end = __builtin_amdgcn_readlane(rpl, row + 1 <= kConRows ? row + 1 : kConRows);
+      };
+      if (nz1 > nz0) commit();  // first window: straight-line, waits for its own loads only
+      for (int wb = nz0; wb < nz1; wb += kConWin) {
+        const int wl = nz1 - wb < kConWin ? nz1 - wb : kConWin;
+        if (wb != nz0) {  // chunks longer than one window (rare)
+          stage(wb, wl);
+          commit();
+        }
+        for (int tb = 0; tb < wl; tb += kConBatch * P) {
+          double g[kConBatch];
+#pragma unroll
+          for (int q = 0; q < kConBatch; ++q) {
+            const int t = tb + P * q + h;
+            const int col = sc[t < wl ? t : 0];
+            g[q] = Ut[static_cast<int64_t>(col) * np1 + lac];  // valid address for every lane
           }
 #pragma unroll
-          for (int u8 = 0; u8 < 8; ++u8)
-            if (t0 + u8 < len) w += readlane_f64(mv, t0 + u8) * g[u8];
+          for (int q = 0; q < kConBatch; ++q) {
+            const int tA = tb + P * q;  // wave-uniform position of slot 0
+            if (tA >= wl) break;
+            while (wb + tA >= row_end) flush();
+            const double gq = on ? g[q] : 0.0;
+            if (h == 0) w += sv[tA] * gq;
+            if (P == 2 && tA + 1 < wl) {
+              while (wb + tA + 1 >= row_end) flush();
+              if (h == 1) w += sv[tA + 1] * gq;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      while (row < kConRows) flush();  // last row with nonzeros, then empty / absent rows
+      __builtin_amdgcn_wave_barrier();
+      // phase 2: rank-16 update G[a][b] += sum_i Ut[r0+i][a] * W[i][b], b in this lane's
+      // segment [SEG*h, SEG*h + SEG) (LDS broadcast reads)
+#pragma unroll
+      for (int i = 0; i < kConRows; ++i) {
+        const double ui = (on && i < nr) ? u[i] : 0.0;
+        const double2* wr = reinterpret_cast<const double2*>(&W[i][SEG * h]);
+#pragma unroll
+        for (int j = 0; j < SEG; j += 2) {
+          const double2 x2 = wr[j >> 1];
+          acc[j] += ui * x2.x;
+          acc[j + 1] += ui * x2.y;
         }
       }
-      if (!on) w = 0.0;
-#pragma unroll
-      for (int b = 0; b < NP; ++b) acc[b] += u * readlane_f64(w, b);
+      __builtin_amdgcn_wave_barrier();
     }
-    if (nvv > 0) gv[0] += u * v0[r];
-    if (nvv > 1) gv[1] += u * v1[r];
-    if (nvv > 2) gv[2] += u * v2[r];
-    if (nvv > 3) gv[3] += u * v3[r];
+    if (h == 0) {
+#pragma unroll
+      for (int i = 0; i < kConRows; ++i) {  // Gv[c][a] += Ut[r][a] * v_c[r]
+        const double ui = (on && i < nr) ? u[i] : 0.0;
+        if (nvv > 0) gv[0] += ui * readlane_f64(vc[0], i);
+        if (nvv > 1) gv[1] += ui * readlane_f64(vc[1], i);
+        if (nvv > 2) gv[2] += ui * readlane_f64(vc[2], i);
+        if (nvv > 3) gv[3] += ui * readlane_f64(vc[3], i);
+      }
+    }
   }
-  // combine the block's 4 waves in wave order through LDS (deterministic), one partial per block
-  for (int w = 0; w < kBlock / 64; ++w) {
+  // combine the block's waves in wave order through LDS (deterministic), one partial per block
+  for (int w = 0; w < NW; ++w) {
     if (wid == w) {
 #pragma unroll
-      for (int b = 0; b < NP; ++b) s_acc[lane * (NP + 4) + b] = (w == 0 ? 0.0 : s_acc[lane * (NP + 4) + b]) + acc[b];
+      for (int j = 0; j < SEG; ++j) s_acc[lane * (SEG + 4) + j] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + j]) + acc[j];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        s_acc[lane * (NP + 4) + NP + c] = (w == 0 ? 0.0 : s_acc[lane * (NP + 4) + NP + c]) + gv[c];
+        s_acc[lane * (SEG + 4) + SEG + c] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + SEG + c]) + gv[c];
     }
     __syncthreads();
   }
-  // partial layout per block: [np1 x np1 G | nvv x np1 Gv]
+  // partial layout per block: [np1 x np1 G | nvv x np1 Gv]; G[a][b] lives in lane a + NP*(b/SEG)
   const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
   double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
   for (int idx = threadIdx.x; idx < stride; idx += kBlock) {
     if (idx < np1 * np1) {
       const int a = idx / np1, b = idx - (idx / np1) * np1;
-      out[idx] = has_m ? s_acc[a * (NP + 4) + b] : 0.0;
+      out[idx] = has_m ? s_acc[(a + NP * (b / SEG)) * (SEG + 4) + (b % SEG)] : 0.0;
     } else {
       const int k2 = idx - np1 * np1;
       const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
-      out[idx] = s_acc[a * (NP + 4) + NP + c];
+      out[idx] = s_acc[a * (SEG + 4) + SEG + c];
     }
   }
 }
@@ -777,17 +891,20 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
   const double* va = M ? M->vals : nullptr;
   const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int c = 0; c < nvv; ++c) vv[c] = v[c];
+  // one resident wave-set (256 CUs x blocks per CU at the kernel's occupancy): every group's
+  // waves sweep their row range together; a multiple of 8 and <= constraint_gram_partials()
+  const int grid = np1 <= 32 ? 256 * 3 : 256 * 2;
   if (np1 <= 32)
-    hipLaunchKernelGGL(constraint_gram_kernel<32>, dim3(kConGramGrid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
+    hipLaunchKernelGGL(constraint_gram_kernel<32>, dim3(grid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
                        nvv, vv[0], vv[1], vv[2], vv[3], partials);
   else
-    hipLaunchKernelGGL(constraint_gram_kernel<64>, dim3(kConGramGrid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
+    hipLaunchKernelGGL(constraint_gram_kernel<64>, dim3(grid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
                        nvv, vv[0], vv[1], vv[2], vv[3], partials);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int npairs = np1 * np1 + nvv * np1;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs,
-                     constraint_gram_partials(), partials, G);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs, grid,
+                     partials, G);
   return hipGetLastError();
 }
 

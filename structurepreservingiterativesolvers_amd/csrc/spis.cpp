@@ -16,9 +16,12 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kernels.h"
@@ -115,6 +118,12 @@ struct spis_context {
   std::vector<Pending> ev_pending;
   double prof_ms[SPIS_PROF_KINDS] = {0};
   int64_t prof_n[SPIS_PROF_KINDS] = {0};
+  // stream-ordered caching allocator behind spis_malloc / spis_free: freed blocks go to a
+  // size-keyed free list and are handed out again in stream order (every user of a block runs on
+  // this context's stream), so a steady-state solve loop makes no hipMalloc / hipFree calls
+  std::multimap<size_t, void*> free_blocks;
+  std::unordered_map<void*, size_t> live_blocks;
+  size_t cached_bytes = 0;
 };
 
 struct spis_matrix {
@@ -178,7 +187,7 @@ static hipEvent_t prof_event(spis_context* c) {
     return e;
   }
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only: no L2 flush
   return e;
 }
 
@@ -248,7 +257,10 @@ static int ensure_pinned(spis_context* c, size_t len) {
     HIP_TRY(hipHostFree(c->pinned));
   }
   c->pinned = nullptr;
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double), hipHostMallocMapped));
+  // fine-grained (coherent) and mapped: kernels store h columns / residual partials straight
+  // into host memory, uncached on the GPU side, so a device-scope event release suffices
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double),
+                        hipHostMallocMapped | hipHostMallocCoherent));
   void* dp = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
   c->pinned_dev = static_cast<double*>(dp);
@@ -356,12 +368,23 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->partR, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_arn, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], hipEventDisableTiming));
+    // pipeline events only order host reads of the coherent pinned slots: device-scope release
+    // (a system-scope one writes back and invalidates L2 at every iteration, ~8 us each);
+    // SPIS_SYSTEM_EVENTS=1 restores the system-scope release
+    const char* se = std::getenv("SPIS_SYSTEM_EVENTS");
+    const unsigned evf = hipEventDisableTiming | ((se && se[0] == '1') ? 0u : hipEventReleaseToDevice);
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_arn, evf));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
     *out = c.release();
     return SPIS_OK;
   })
+}
+
+static void release_cache(spis_context* c) {
+  for (auto& kv : c->free_blocks) (void)hipFree(kv.second);
+  c->free_blocks.clear();
+  c->cached_bytes = 0;
 }
 
 static void free_workspace(spis_workspace* ws) {
@@ -386,6 +409,8 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto* ws : c->pool) free_workspace(ws);
+    release_cache(c);
+    for (auto& kv : c->live_blocks) (void)hipFree(kv.first);
     (void)hipFree(c->partA);
     (void)hipFree(c->partB);
     (void)hipFree(c->partR);
@@ -634,13 +659,37 @@ extern "C" int spis_matrix_info(spis_matrix* M, int64_t info[8]) {
 // ------------------------------------------------------------------------------------------------
 // memory + primitives
 // ------------------------------------------------------------------------------------------------
+static size_t alloc_class(int64_t bytes) {  // 256-B classes below 1 MiB, 64 KiB classes above
+  const size_t b = static_cast<size_t>(std::max<int64_t>(bytes, 16));
+  return b < (1u << 20) ? (b + 255) / 256 * 256 : (b + 65535) / 65536 * 65536;
+}
+
+static constexpr size_t kCacheLimit = size_t(16) << 30;  // bytes kept on the free list
+
 extern "C" int spis_malloc(spis_context* c, int64_t bytes, void** out) {
   ABI_GUARD({
     if (!c || !out || bytes < 0) return fail(SPIS_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMalloc(out, std::max<int64_t>(bytes, 16)));
-    HIP_TRY(hipMemsetAsync(*out, 0, std::max<int64_t>(bytes, 16), c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    const size_t sz = alloc_class(bytes);
+    void* p = nullptr;
+    auto it = c->free_blocks.find(sz);
+    if (it != c->free_blocks.end()) {
+      p = it->second;
+      c->free_blocks.erase(it);
+      c->cached_bytes -= sz;
+    } else {
+      hipError_t e = hipMalloc(&p, sz);
+      if (e != hipSuccess) {  // give the cached blocks back and retry once
+        (void)hipGetLastError();
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        release_cache(c);
+        HIP_TRY(hipMalloc(&p, sz));
+      }
+    }
+    c->live_blocks[p] = sz;
+    // zero-filled, ordered before every later use of the block on this stream (no host wait)
+    HIP_TRY(hipMemsetAsync(p, 0, sz, c->stream));
+    *out = p;
     return SPIS_OK;
   })
 }
@@ -648,8 +697,18 @@ extern "C" int spis_malloc(spis_context* c, int64_t bytes, void** out) {
 extern "C" int spis_free(spis_context* c, void* p) {
   ABI_GUARD({
     if (!c) return fail(SPIS_ERR_ARG, "null context");
+    if (!p) return SPIS_OK;
+    auto it = c->live_blocks.find(p);
+    if (it == c->live_blocks.end()) return fail(SPIS_ERR_ARG, "spis_free: pointer not from spis_malloc");
+    const size_t sz = it->second;
+    c->live_blocks.erase(it);
+    if (c->cached_bytes + sz <= kCacheLimit) {  // reusable in stream order: no wait
+      c->free_blocks.emplace(sz, p);
+      c->cached_bytes += sz;
+      return SPIS_OK;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (p) HIP_TRY(hipFree(p));
+    HIP_TRY(hipFree(p));
     return SPIS_OK;
   })
 }
@@ -1336,6 +1395,12 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         ST_TRY(S.enqueue_arnoldi(j + 2));
       }
     }
+    // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
+    // Arnoldi step, which never touches xj / r0), then one synchronisation
+    if (out->x_final_dev) {
+      if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
+      else HIP_TRY(launch_copy(n, have_x ? ws->xj : ws->r0, out->x_final_dev, s));
+    }
     if (pending >= 0) {
       ST_TRY(wait_event(c->ev_upd[pending & 1]));
       out->res_host[n_res++] = S.residual(pending);
@@ -1343,11 +1408,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
     HIP_TRY(hipStreamSynchronize(s));  // speculative Arnoldi steps finish before x / ws are used
     prof_drain(c);
-    if (out->x_final_dev) {
-      if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
-      else HIP_TRY(launch_copy(n, have_x ? ws->xj : ws->r0, out->x_final_dev, s));
-      HIP_TRY(hipStreamSynchronize(s));
-    }
     if (stamps) {
       stamps[4 * k] = t_start;
       stamps[4 * k + 1] = now_s();

@@ -218,3 +218,30 @@ def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
     if isinstance(v, DeviceVector):
         return v
     return DeviceVector.from_host(v, ctx=ctx, capacity=capacity)
+
+
+class DeviceConstraint:
+    """A class-form constraint ``1/2 X'MX + v.X + c`` (``solvers.py:22-36``) whose operators are
+    already resident in HBM: ``M`` a :class:`DeviceMatrix` or None, ``v`` a :class:`DeviceVector`
+    or None.  ``solvers.cgmres`` takes it wherever the reference takes a constraint class."""
+
+    def __init__(self, M, v, c):
+        self.M, self.v, self.c = M, v, c
+
+
+def device_constraints(conlist, ctx=None):
+    """Upload the operators of reference-form class constraints once (``M`` dropped when it is
+    all zeros, ``v`` when it is all zeros, as ``solvers.cgmres`` does per call)."""
+    ctx = ctx or get_context()
+    out = []
+    for con in conlist:
+        M = getattr(con, "M", None)
+        if M is not None and not isinstance(M, DeviceMatrix):
+            Ms = M if sps.issparse(M) else sps.csr_matrix(M)
+            M = None if Ms.nnz == 0 or not np.any(Ms.data) else device_matrix(Ms, ctx=ctx)
+        v = getattr(con, "v", None)
+        if v is not None and not isinstance(v, DeviceVector):
+            va = np.asarray(v, dtype=np.float64).reshape(-1)
+            v = DeviceVector.from_host(va, ctx=ctx) if np.any(va) else None
+        out.append(DeviceConstraint(M, v, float(np.asarray(getattr(con, "c", 0.0)))))
+    return out

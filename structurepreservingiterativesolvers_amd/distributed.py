@@ -35,6 +35,7 @@ import numpy as np
 import scipy.sparse as sps
 
 from . import _lib
+from .device import DeviceConstraint  # noqa: F401  (public here for the distributed API)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -246,14 +247,7 @@ class DistributedSystem:
         return self.part.from_locals(parts)
 
 
-class DeviceConstraint:
-    """A class-form constraint ``1/2 X'MX + v.X + c`` whose ``M`` is a (distributed)
-    DeviceMatrix or None and ``v`` a DeviceVector or None (solvers.py:22-36)."""
-
-    def __init__(self, M, v, c):
-        self.M, self.v, self.c = M, v, c
-
-
+# DeviceConstraint (imported above) takes rank-local operators: sysd.matrix / sysd.vector
 _DevCon = DeviceConstraint
 
 

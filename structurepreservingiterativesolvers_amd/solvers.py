@@ -399,6 +399,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     xs.trace = [(j, names[int(br[j])]) for j in range(n_iter)]  # branch per LS step (tests, diagnostics)
     xs.events = ev[: max(n_iter, out.steps)].copy()
     xs.y = [ys[j * k: j * k + j + 1].copy() for j in range(n_iter)]
+    xs.stamps = stamps  # host clock: per-iteration / constraint-step stamps, [4k] call start, [4k+1] end
     return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
                 stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)
 
