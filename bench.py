@@ -1,11 +1,17 @@
 """Benchmark: CGMRES iterations/sec + Arnoldi-SpMV achieved HBM GB/s (BASELINE.json).
 
-Workload (BASELINE.json configs[2]): swe-shaped RT2 x DG0
-CSR, N = 12 M^2 = 1,002,252 DoF per GPU (M = 289), 12.5 nnz/row, fp64;
-``swe.LinearSolver.cgmresWrapper`` semantics (mass + energy constraints),
-k = 30, tol = 1e-19 so every solve runs all 30 iterations and the last one is
-the constrained projection.  One "step" = one CGMRES(30) solve; inputs (A, b,
-x0, constraint operators) are resident in HBM before the timed region.
+Default workload (BASELINE.json configs[2]): swe-shaped RT2 x DG0 CSR,
+N = 12 M^2 = 1,002,252 DoF per GPU (M = 289), 12.5 nnz/row, fp64;
+``swe.LinearSolver.cgmresWrapper`` semantics (mass + energy constraints), k = 30, tol = 1e-19
+so every solve runs all 30 iterations and the last one is the constrained projection.  One
+"step" = one CGMRES(30) solve; inputs (A, b, x0, constraint operators) are resident in HBM
+before the timed region.
+
+``--config`` selects the other SURVEY §8 single-GPU configurations (not the driver's line):
+  c2  lkdv DG1 M=16,667, N=100,002, 3 constraints (mass, momentum, energy)
+  c4  lkdvRK GL(3) M=16,667, N=300,006, the 3 dict constraints lifted to (M, v, c) form
+  c5  swe M=913, N=10,002,828, 3 constraints (+ the synthetic third), restarted CGMRES(30),
+      one step = one restarted solve of --cycles cycles (default 10)
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): one global solve of
 N x 1,002,252 DoF row-partitioned over the N ranks (weak scaling), RCCL
@@ -53,7 +59,7 @@ def load_traffic():
     return None
 
 
-def cpu_baseline(dic, conlist, k, tol, budget_s):
+def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
     """The oracle (CPU restatement of the reference solvers.cgmres, NumPy/SciPy +
     SLSQP exactly as the reference) on the same workload, bounded sample."""
     import oracle
@@ -85,12 +91,52 @@ def cpu_baseline(dic, conlist, k, tol, budget_s):
     }
 
 
+def build_workload(args):
+    """A, b and the reference-form constraint list of the selected SURVEY §8 configuration."""
+    x0 = None
+    if args.config in ("c3", "c5"):
+        from structurepreservingiterativesolvers_amd.swe import LinearSolver as ls
+        from structurepreservingiterativesolvers_amd.swe import assembly
+
+        M = args.M or (289 if args.config == "c3" else 913)
+        dic, _ = assembly.linforms(M=M)
+        x0 = np.zeros(dic["A"].shape[0])
+        conlist = ls.constraints(dic, x0)
+        desc = f"swe-shaped RT2xDG0 CSR (config {args.config.upper()}, M={M}), mass+energy constraints"
+        if args.config == "c5":
+            D, c3 = assembly.extra_constraint(len(x0), dic["z0"], seed=2)
+            conlist.append(ls._Constraint(D, None, c3))
+            desc += " + synthetic third constraint (seed 2)"
+        return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "desc": desc,
+                "cycles": args.cycles if args.config == "c5" else 1}
+    if args.config == "c2":
+        from structurepreservingiterativesolvers_amd.lkdv import LinearSolver as ls
+        from structurepreservingiterativesolvers_amd.lkdv import assembly
+
+        M = args.M or 16667
+        dic, _ = assembly.linforms(M=M)
+        conlist = ls.constraints(dic, np.zeros(dic["A"].shape[0]))
+        return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "cycles": 1,
+                "desc": f"lkdv DG1 (config C2, M={M}), mass+momentum+energy constraints"}
+    from structurepreservingiterativesolvers_amd.lkdvRK import LinearSolver as ls
+    from structurepreservingiterativesolvers_amd.lkdvRK import assembly
+
+    M = args.M or 16667
+    dic, prob = assembly.linforms(M=M, tstages=3)
+    conlist = ls.constraints(dic, prob, lift=True)
+    return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "cycles": 1,
+            "desc": f"lkdvRK GL(3) block-stage (config C4, M={M}), 3 invariants lifted to (M, v, c) form"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--M", type=int, default=289, help="swe mesh per GPU (N = 12 M^2)")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
+                    help="SURVEY §8 configuration (c3 = the BASELINE.json line)")
+    ap.add_argument("--M", type=int, default=None, help="mesh size override (swe: N = 12 M^2 per GPU)")
+    ap.add_argument("--cycles", type=int, default=10, help="restart cycles for c5")
     ap.add_argument("--k", type=int, default=30)
     ap.add_argument("--tol", type=float, default=1e-19)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -110,22 +156,24 @@ def main():
     from structurepreservingiterativesolvers_amd import _lib, solvers
     from structurepreservingiterativesolvers_amd.device import (DeviceVector, device_constraints, device_matrix,
                                                                 get_context)
-    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
-    from structurepreservingiterativesolvers_amd.swe import assembly
 
-    dic, _ = assembly.linforms(M=args.M)
-    A = dic["A"]
+    wl = build_workload(args)
+    A = wl["A"]
     n = A.shape[0]
     ctx = get_context(0)
     device_matrix(A, ctx=ctx)
-    bd = DeviceVector.from_host(dic["b"], ctx=ctx)
+    bd = DeviceVector.from_host(wl["b"], ctx=ctx)
     x0 = np.zeros(n)
     x0d = DeviceVector.from_host(x0, ctx=ctx)
-    conlist = swe_ls.constraints(dic, x0)
+    conlist = wl["conlist"]
     conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
 
-    def solve():
-        return solvers.cgmres(A, bd, x0d, args.k, tol=args.tol, conlist=conlist_dev)
+    if wl["cycles"] > 1:
+        def solve():
+            return solvers.cgmres_restarted(A, bd, x0d, args.k, wl["cycles"], tol=args.tol, conlist=conlist_dev)
+    else:
+        def solve():
+            return solvers.cgmres(A, bd, x0d, args.k, tol=args.tol, conlist=conlist_dev)
 
     for _ in range(args.warmup):
         solve()
@@ -141,7 +189,7 @@ def main():
     for _ in range(args.steps):
         ts = time.perf_counter()
         _, d = solve()
-        st = d["x"].stamps if hasattr(d["x"], "stamps") else None
+        st = d["x"].stamps if "x" in d and hasattr(d["x"], "stamps") else None
         if st is not None:
             outside += (time.perf_counter() - ts) - (st[4 * args.k + 1] - st[4 * args.k])
         iters += d["steps"]
@@ -162,7 +210,8 @@ def main():
     mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
-    traffic = load_traffic()
+    # the committed PMC summary was measured on the C3 matrix: reported for that workload only
+    traffic = load_traffic() if args.config == "c3" and args.M in (None, 289) else None
     out = {
         "metric": METRIC,
         "value": iters / elapsed,
@@ -177,8 +226,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"swe-shaped RT2xDG0 CSR (config C3), N={n:,} DoF, nnz={A.nnz:,}, "
-                        f"CGMRES(k={args.k}, tol={args.tol:g}) with mass+energy constraints per step",
+            "workload": wl["desc"] + f", N={n:,} DoF, nnz={A.nnz:,}, CGMRES(k={args.k}, tol={args.tol:g})"
+                        + (f" restarted x{wl['cycles']}" if wl["cycles"] > 1 else ""),
+            "config": args.config,
             "global_dof": n,
             "k": args.k,
             "parallelism": "single GPU",
@@ -206,7 +256,7 @@ def main():
         },
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(dic, conlist, args.k, args.tol, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(wl, conlist, args.k, args.tol, args.cpu_budget)
     print(json.dumps(out))
 
 

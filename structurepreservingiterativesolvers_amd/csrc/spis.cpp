@@ -165,6 +165,7 @@ struct spis_workspace {
   double* ext = nullptr;  // scratch SpMV input with ghost space (constraint / preconditioner halos)
   double* ydev = nullptr;
   double* Ut = nullptr;  // transposed [Z, x0] for the fused constraint reduction (n x (p+1))
+  int Ut_cols = 0;       // its allocated row capacity (32 or 64)
   int32_t ext_len = 0;
   std::vector<ConCache> con;
   std::vector<double> y_all;  // k*k host copy of every iteration's y
@@ -396,6 +397,7 @@ static void free_workspace(spis_workspace* ws) {
   (void)hipFree(ws->x0);
   (void)hipFree(ws->ydev);
   if (ws->ext) (void)hipFree(ws->ext);
+  if (ws->Ut) (void)hipFree(ws->Ut);
   for (auto& cc : ws->con) {
     if (cc.MZ) (void)hipFree(cc.MZ);
     if (cc.Mx0) (void)hipFree(cc.Mx0);
@@ -826,7 +828,15 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                   int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   QuadCon* out) {
   const int np1 = p + 1;
-  if (!ws->Ut) HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * std::max<int64_t>(n, 1) * 64));
+  const int ut_cols = np1 <= 32 ? 32 : 64;  // Ut is N x np1 row-major: size for this p bucket
+  if (ws->Ut && ws->Ut_cols < ut_cols) {
+    HIP_TRY(hipFree(ws->Ut));
+    ws->Ut = nullptr;
+  }
+  if (!ws->Ut) {
+    HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * std::max<int64_t>(n, 1) * ut_cols));
+    ws->Ut_cols = ut_cols;
+  }
   const size_t need = static_cast<size_t>(constraint_gram_partials()) * (np1 * np1 + 4 * np1);
   if (c->cg_part_len < need) {
     if (c->cg_part) HIP_TRY(hipFree(c->cg_part));

@@ -465,3 +465,27 @@ def cgmres_p(A, b, x0, k, conlist=[], pre=None):
     _replay_warnings(r, _lib.CGMRES_P, None)
     d = {"name": "geosolve", "x": r["x"], "res": list(r["res"][1:])}
     return r["final"], d
+
+
+def cgmres_restarted(A, b, x0, k, cycles, tol=1e-8, contol=10, conlist=[], pre=None, keep_iterates=False):
+    """Restarted CGMRES(k): the caller-side restart loop of SURVEY §8 config C5 (the reference has
+    no restart inside ``solvers.py``; a driver restarts by calling ``cgmres`` again with
+    ``x0 = x[-1]``).  Class constraints ``1/2 X'MX + v.X + c`` are absolute in ``X``, so every
+    cycle's constrained step enforces them on the restarted iterate.  Stops after ``cycles``
+    cycles or when a cycle ends early (its stop test ``res < tol`` with an accepted constrained
+    step, ``solvers.py:296``, or a breakdown).  Returns ``(x, dict)`` with the concatenated
+    residual history, total ``steps``, the number of ``cycles`` run and each cycle's dict.  Only
+    the last cycle keeps its device basis (lazy ``x`` list) unless ``keep_iterates``: a cycle's
+    basis is (k+1) N doubles, which adds up over many cycles at large N."""
+    x = x0
+    res, steps, runs = [], 0, []
+    for _ in range(int(cycles)):
+        if runs and not keep_iterates:
+            runs[-1]["x"].release()
+        x, d = cgmres(A, b, x, k, tol=tol, contol=contol, conlist=conlist, pre=pre)
+        res.extend(d["res"])
+        steps += d["steps"]
+        runs.append(d)
+        if d["steps"] < int(k):
+            break
+    return x, {"name": "cgmres_restarted", "res": res, "steps": steps, "cycles": len(runs), "runs": runs}
