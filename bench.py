@@ -50,9 +50,15 @@ def mgs_bytes(n, p):
     return 32 * n * p + 16 * n
 
 
-def load_traffic():
-    """Per-launch HBM bytes of the Arnoldi SpMV from the committed PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "spmv_traffic.json")
+def dual_bytes(n_rows, nnz):
+    """Algorithmic bytes of the fused residual + Arnoldi SpMV: the matrix once, x_j and b read
+    (true residual, solvers.py:290), z_{j+2} read and w written (Arnoldi, :191)."""
+    return 12 * nnz + 4 * (n_rows + 1) + 32 * n_rows
+
+
+def load_traffic(name="spmv_traffic.json"):
+    """Per-launch HBM bytes of a kernel from a committed PMC summary under profiles/, if any."""
+    path = os.path.join(ROOT, "profiles", name)
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f)
@@ -143,6 +149,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-distributed", action="store_true",
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
+    ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
+    ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
     ap.add_argument("--prof-period", type=int, default=10,
                     help="time every n-th iteration's kernels with HIP events inside the timed region")
     args = ap.parse_args()
@@ -167,6 +175,8 @@ def main():
     x0d = DeviceVector.from_host(x0, ctx=ctx)
     conlist = wl["conlist"]
     conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1 if args.graphs else 0), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 0 if args.no_fuse else 1), "spis_set_option")
 
     if wl["cycles"] > 1:
         def solve():
@@ -195,23 +205,38 @@ def main():
         iters += d["steps"]
     ctx.synchronize()
     t1 = time.perf_counter()
-    ms = (C.c_double * 4)()
-    cnt = (C.c_int64 * 4)()
-    _lib.check(L.spis_profile_read(ctx.handle, ms, cnt), "spis_profile_read")
+    ms, cnt = _lib.profile_read(L, ctx.handle)
     _lib.check(L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
     elapsed = t1 - t0
 
     S = spmv_bytes(n, A.nnz)
     spmv_ms = ms[_lib.PROF_SPMV] / max(cnt[_lib.PROF_SPMV], 1)
     spmv_gbs = S / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
+    SD = dual_bytes(n, A.nnz)
+    dual_ms = ms[_lib.PROF_SPMV_DUAL] / max(cnt[_lib.PROF_SPMV_DUAL], 1)
+    dual_gbs = SD / (dual_ms * 1e-3) / 1e9 if dual_ms > 0 else 0.0
     sampled = [j + 1 for j in range(0, args.k, max(args.prof_period, 1))]
     p_mean = float(np.mean(sampled))  # basis size of the sampled (timed) MGS chains
     mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
     mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
-    # the committed PMC summary was measured on the C3 matrix: reported for that workload only
-    traffic = load_traffic() if args.config == "c3" and args.M in (None, 289) else None
+    # the committed PMC summaries were measured on the C3 matrix: reported for that workload only
+    c3 = args.config == "c3" and args.M in (None, 289)
+    fused = cnt[_lib.PROF_SPMV_DUAL] > 0
+    traffic = load_traffic("spmv_dual_traffic.json" if fused else "spmv_traffic.json") if c3 else None
+    if fused:  # the dominant SpMV launch: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
+        roof = {"kernel": "spmv_dual_kernel (true-residual SpMV of x_j, solvers.py:290, fused with the "
+                          "Arnoldi SpMV of z_{j+2}, :191; matrix read once)",
+                "bound": "hbm", "achieved": dual_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dual_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": SD,
+                "avg_launch_us": 1e3 * dual_ms, "launches": int(cnt[_lib.PROF_SPMV_DUAL])}
+    else:
+        roof = {"kernel": "spmv_rowblock_kernel<kEpiDot> (Arnoldi SpMV, solvers.py:191)",
+                "bound": "hbm", "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": spmv_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": S,
+                "avg_launch_us": 1e3 * spmv_ms, "launches": int(cnt[_lib.PROF_SPMV])}
+    roof["traffic"] = None if traffic is None else traffic.get("bytes_per_launch")
     out = {
         "metric": METRIC,
         "value": iters / elapsed,
@@ -233,20 +258,11 @@ def main():
             "k": args.k,
             "parallelism": "single GPU",
         },
-        "roofline": {
-            "kernel": "spmv_rowblock_kernel<kEpiDot> (Arnoldi SpMV, solvers.py:191)",
-            "bound": "hbm",
-            "achieved": spmv_gbs,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": spmv_gbs / HBM_PEAK_GBS,
-            "traffic": None if traffic is None else traffic.get("bytes_per_launch"),
-            "algorithmic_bytes_per_launch": S,
-            "avg_launch_us": 1e3 * spmv_ms,
-            "launches": int(cnt[_lib.PROF_SPMV]),
-        },
+        "roofline": roof,
         "kernels": {
             "spmv_arnoldi_us": 1e3 * spmv_ms,
+            "spmv_dual_us": 1e3 * dual_ms,
+            "spmv_dual_GBs": dual_gbs,
             "spmv_residual_us": 1e3 * res_ms,
             "mgs_chain_us_mean": 1e3 * mgs_ms,
             "mgs_chain_GBs": mgs_gbs,

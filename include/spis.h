@@ -102,14 +102,27 @@ int spis_context_stream(spis_context* ctx, void** stream_out);
  * disables; a negative value (tests) additionally routes the constraint
  * reduction through the generic Gram path instead of the fused kernel. */
 enum spis_prof_kind {
-  SPIS_PROF_SPMV = 0,      /* Arnoldi SpMV, solvers.py:191            */
-  SPIS_PROF_MGS = 1,       /* MGS chain + normalise, :193-198          */
-  SPIS_PROF_GEMV = 2,      /* Z y + x0, :287                           */
-  SPIS_PROF_SPMV_RES = 3,  /* true-residual SpMV + norm, :290          */
-  SPIS_PROF_KINDS = 4
+  SPIS_PROF_SPMV = 0,       /* Arnoldi SpMV, solvers.py:191 (standalone launches)          */
+  SPIS_PROF_MGS = 1,        /* MGS chain + normalise, :193-198                             */
+  SPIS_PROF_GEMV = 2,       /* Z y + x0, :287                                              */
+  SPIS_PROF_SPMV_RES = 3,   /* true-residual SpMV + norm, :290 (standalone launches)       */
+  SPIS_PROF_SPMV_DUAL = 4,  /* fused: residual SpMV of x_j + Arnoldi SpMV of z_{j+2}       */
+  SPIS_PROF_KINDS = 5
 };
 int spis_profile_enable(spis_context* ctx, int32_t on);
-int spis_profile_read(spis_context* ctx, double ms_out[4], int64_t count_out[4]);
+int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t count_out[SPIS_PROF_KINDS]);
+
+/* ---- options -------------------------------------------------------------------
+ * SPIS_OPT_FUSE_SPMV (default 1): the true-residual SpMV of update j and the Arnoldi SpMV of
+ *   step j+2 (adjacent in the pipelined stream) run as one launch reading the matrix once;
+ *   results are bit-identical either way.
+ * SPIS_OPT_GENERIC_GRAM (default 0): route the constraint reduction through the generic
+ *   SpMM + tiled Gram path instead of the fused kernel (tests).
+ * SPIS_OPT_GRAPHS (default 0): replay each Arnoldi step's launches (fused SpMV, MGS chain,
+ *   normalise) from a captured hipGraph (single GPU, no host preconditioner callback).  Cuts host
+ *   enqueue time ~9x, but each replay adds ~5 us of GPU time at its boundary: C3 is 2% slower. */
+enum spis_option { SPIS_OPT_FUSE_SPMV = 1, SPIS_OPT_GENERIC_GRAM = 2, SPIS_OPT_GRAPHS = 3 };
+int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 
 /* ---- multi-GPU (RCCL over xGMI) ----------------------------------------------
  * rank 0 creates the id (128 bytes), the host side broadcasts it (e.g. over

@@ -20,7 +20,9 @@ OK, ERR_ARG, ERR_HIP, ERR_RCCL, ERR_ALLOC, ERR_CALLBACK, ERR_STATE = range(7)
 CGMRES, GMRES, CGMRES_P = 0, 1, 2
 BRANCH_UNCON, BRANCH_CON, BRANCH_FALLBACK = 0, 1, 2
 EV_BREAKDOWN, EV_LS_MESSAGE, EV_NAN, EV_VIOLATION, EV_FALLBACK = 1, 2, 4, 8, 16
-PROF_SPMV, PROF_MGS, PROF_GEMV, PROF_SPMV_RES = range(4)
+PROF_SPMV, PROF_MGS, PROF_GEMV, PROF_SPMV_RES, PROF_SPMV_DUAL = range(5)
+PROF_KINDS = 5
+OPT_FUSE_SPMV, OPT_GENERIC_GRAM, OPT_GRAPHS = 1, 2, 3
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",
@@ -108,6 +110,7 @@ SIGNATURES = [
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),
+    ("spis_set_option", C.c_int, [_VP, _I32, _I64]),
     ("spis_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("spis_comm_init", C.c_int, [_VP, _I32, _I32, C.POINTER(C.c_uint8)]),
     ("spis_comm_allreduce_sum", C.c_int, [_VP, _VP, _I64]),
@@ -174,3 +177,11 @@ def lib():
     if n.value < 1:
         raise SpisUnavailable("no HIP device visible: the spis solver path runs only on an MI355X (gfx950)")
     return L
+
+
+def profile_read(L, handle):
+    """(total ms, launch count) per SPIS_PROF_* kind since spis_profile_enable."""
+    ms = (C.c_double * PROF_KINDS)()
+    cnt = (C.c_int64 * PROF_KINDS)()
+    check(L.spis_profile_read(handle, ms, cnt), "spis_profile_read")
+    return list(ms), list(cnt)

@@ -11,6 +11,7 @@ constexpr int kBlock = 256;      // threads per workgroup (4 waves of 64)
 constexpr int kRowCap = 256;     // rows per SpMV row block (one thread per row)
 constexpr int kNnzCap = 2048;    // nnz staged in LDS per row block (16 KiB fp64)
 constexpr int kItemCap = 2048;   // merge items (rows + nnz) per row block
+constexpr int kDualCap = 1024;   // nnz / items per row block of the fused dual SpMV (2 x 8 KiB LDS)
 constexpr int kSpmvGrid = 2048;  // max SpMV workgroups (= max epilogue partials)
 constexpr int kRedGrid = 1024;   // max BLAS-1 workgroups (= max reduction partials)
 constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's LDS copy of y
@@ -45,18 +46,37 @@ struct CsrView {
 int spmv_grid(const CsrView& A, bool fixed);
 int blas_grid(int64_t n, bool fixed);
 
+// Events carried by a kernel's own dispatch (hipExtLaunchKernel): `start` / `stop` are recorded
+// at the launch's start / completion without a separate marker packet on the stream (a marker
+// costs ~6 us of queue time between dependent kernels).
+struct LaunchEv {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+};
+
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
-                       double* partials, int grid, hipStream_t s);
+                       double* partials, int grid, hipStream_t s, const LaunchEv* ev = nullptr);
+// K1d: residual SpMV of x1 (||A x1 - b||^2 partials -> part1) and Arnoldi SpMV of x2 (w = A x2,
+// q0.w partials -> part2) reading the matrix once; both bit-identical to launch_spmv's.  A must
+// carry the kDualCap row-block table; grid <= kSpmvGrid (the partial arrays' length)
+hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
+                            const double* x2, double* w, const double* q0, double* part2, int grid,
+                            hipStream_t s, const LaunchEv* ev = nullptr);
 // y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,
-                           int grid, hipStream_t s);
+                           int grid, hipStream_t s, const LaunchEv* ev = nullptr,
+                           const double* xpart = nullptr, int n_x = 0, double* x_out = nullptr,
+                           unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr);
+// (xpart, n_x, x_out): workgroup 0 additionally reduces xpart in sum_partials order into *x_out;
+// with flag (host memory), it then publishes *seq there after a system-scope release
 // h = sqrt(sum(part_in)); q_next = y / h (if h != 0)
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
-                            int n_in, double* h_out, hipStream_t s, int grid);
+                            int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
-                       bool y_on_host, const double* x0, double* x, hipStream_t s);
+                       bool y_on_host, const double* x0, double* x, hipStream_t s,
+                       const LaunchEv* ev = nullptr);
 // W[c] = M Z[c] for c < nvec (vectors at stride ldx / ldy)
 hipError_t launch_spmm(const CsrView& A, const double* X, int64_t ldx, int nvec, double* Y,
                        int64_t ldy, hipStream_t s);
@@ -73,7 +93,9 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
 hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_out, int grid,
                       hipStream_t s);
 // out[0] = sum(part) (op 0) or sqrt(sum(part)) (op 1)
-hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s);
+hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s,
+                           const LaunchEv* ev = nullptr, unsigned long long* flag = nullptr,
+                           const unsigned long long* seq = nullptr);
 hipError_t launch_axpy(int64_t n, double h, const double* x, double* y, hipStream_t s);
 hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
 // send[i] = x[idx[i]]

@@ -9,6 +9,7 @@
 // Reference call sites (solvers.py): SpMV :191 / :167 / :290, MGS :193-195,
 // norm + normalise :196-198, GEMV :287, constraint Gram :33-36.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "kernels.h"
 
@@ -34,11 +35,34 @@ __device__ __forceinline__ double block_sum(double v, double* s_wave) {
   return t;
 }
 
+// One thread hands a value to the host: value store, system-scope release, then the flag (the
+// host spins on flag >= seq, then reads the value).  A single writer with a release between the
+// two stores is what makes the value visible first; the release's L2 write-back stalls only this
+// wave.  Without a flag, a plain store (the caller synchronises through an event).
+__device__ __forceinline__ void publish(double* out, double v, unsigned long long* flag,
+                                        const unsigned long long* seq) {
+  *out = v;
+  if (flag != nullptr) {
+    const unsigned long long sq = *seq;  // written by the host before the launch (graph replays)
+    __threadfence_system();
+    __hip_atomic_store(flag, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // every workgroup reduces the same partial array in the same order -> the same scalar
 __device__ __forceinline__ double sum_partials(const double* __restrict__ part, int n, double* s_wave) {
   double v = 0.0;
   for (int i = threadIdx.x; i < n; i += kBlock) v += part[i];
   return block_sum(v, s_wave);
+}
+
+// launch with events carried by the dispatch itself when requested (see LaunchEv)
+template <typename F, typename... Args>
+static void launch_k(F kernel, dim3 g, dim3 b, uint32_t shm, hipStream_t s, const LaunchEv* ev, Args... args) {
+  if (ev != nullptr && (ev->start != nullptr || ev->stop != nullptr))
+    hipExtLaunchKernelGGL(kernel, g, b, shm, s, ev->start, ev->stop, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, g, b, shm, s, args...);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -116,6 +140,100 @@ __global__ __launch_bounds__(kBlock) void spmv_rowblock_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1d: two SpMVs with the same matrix in one pass — the true residual of update U_j (x1 = x_j:
+// ||A x1 - b||^2 partials, solvers.py:290) and the Arnoldi SpMV of step j+2 (x2 = z_{j+2}:
+// w = A x2 and q0.w partials, solvers.py:191), adjacent in the pipelined stream order.  val/col
+// are read once; each product array and each row sum is exactly K1's (bit-identical rows).  It
+// runs on row blocks of <= CAP nnz (kDualCap: two CAP-long product arrays in LDS).
+// ---------------------------------------------------------------------------------------------
+template <int CAP>
+__global__ __launch_bounds__(kBlock) void spmv_dual_kernel(
+    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
+    const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ x1,
+    const double* __restrict__ b, double* __restrict__ part1, const double* __restrict__ x2,
+    double* __restrict__ w, const double* __restrict__ q0, double* __restrict__ part2) {
+  __shared__ double s_p1[CAP];
+  __shared__ double s_p2[CAP];
+  __shared__ double s_wave[4];
+  double pt1 = 0.0, pt2 = 0.0;
+  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int r0 = blk_row[blk];
+    const int r1 = blk_row[blk + 1];
+    const int nz0 = rp[r0];
+    const int nnz = rp[r1] - nz0;
+    if (nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction, twice
+      double a1 = 0.0, a2 = 0.0;
+      for (int i = nz0 + threadIdx.x; i < nz0 + nnz; i += kBlock) {
+        a1 += va[i] * x1[ci[i]];
+        a2 += va[i] * x2[ci[i]];
+      }
+      const double s1 = block_sum(a1, s_wave);
+      const double s2 = block_sum(a2, s_wave);
+      if (threadIdx.x == 0) {
+        const double t = s1 - b[r0];
+        pt1 += t * t;
+        w[r0] = s2;
+        pt2 += q0[r0] * s2;
+      }
+      continue;
+    }
+    constexpr int kPer = CAP / kBlock;
+    int cols[kPer];
+    double vals[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      cols[u] = i < nnz ? ci[nz0 + i] : 0;
+      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+    }
+    double g1[kPer], g2[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      g1[u] = x1[cols[u]];
+      g2[u] = x2[cols[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < nnz) {
+        s_p1[i] = vals[u] * g1[u];
+        s_p2[i] = vals[u] * g2[u];
+      }
+    }
+    __syncthreads();
+    const int r = r0 + threadIdx.x;
+    if (r < r1) {
+      const int s = rp[r] - nz0;
+      const int e = rp[r + 1] - nz0;
+      double s1 = 0.0, s2 = 0.0;
+      for (int t = s; t < e; ++t) {
+        s1 += s_p1[t];
+        s2 += s_p2[t];
+      }
+      const double t = s1 - b[r];
+      pt1 += t * t;
+      w[r] = s2;
+      pt2 += q0[r] * s2;
+    }
+    __syncthreads();
+  }
+  const double tot1 = block_sum(pt1, s_wave);
+  const double tot2 = block_sum(pt2, s_wave);
+  if (threadIdx.x == 0) {
+    part1[blockIdx.x] = tot1;
+    part2[blockIdx.x] = tot2;
+  }
+}
+
+hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
+                            const double* x2, double* w, const double* q0, double* part2, int grid,
+                            hipStream_t s, const LaunchEv* ev) {
+  launch_k(spmv_dual_kernel<kDualCap>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
+           A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
+  return hipGetLastError();
+}
+
 int spmv_grid(const CsrView& A, bool fixed) {
   if (fixed) return kSpmvGrid;
   int g = A.n_blk < kSpmvGrid ? A.n_blk : kSpmvGrid;
@@ -130,24 +248,24 @@ int blas_grid(int64_t n, bool fixed) {
 }
 
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
-                       double* partials, int grid, hipStream_t s) {
+                       double* partials, int grid, hipStream_t s, const LaunchEv* ev) {
   dim3 g(grid), b(kBlock);
   switch (epi) {
     case kEpiPlain:
-      hipLaunchKernelGGL(spmv_rowblock_kernel<kEpiPlain>, g, b, 0, s, A.indptr, A.indices, A.vals,
-                         A.blk_row, A.n_blk, x, y, aux, partials);
+      launch_k(spmv_rowblock_kernel<kEpiPlain>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
+               x, y, aux, partials);
       break;
     case kEpiDot:
-      hipLaunchKernelGGL(spmv_rowblock_kernel<kEpiDot>, g, b, 0, s, A.indptr, A.indices, A.vals,
-                         A.blk_row, A.n_blk, x, y, aux, partials);
+      launch_k(spmv_rowblock_kernel<kEpiDot>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
+               x, y, aux, partials);
       break;
     case kEpiResNorm:
-      hipLaunchKernelGGL(spmv_rowblock_kernel<kEpiResNorm>, g, b, 0, s, A.indptr, A.indices,
-                         A.vals, A.blk_row, A.n_blk, x, y, aux, partials);
+      launch_k(spmv_rowblock_kernel<kEpiResNorm>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row,
+               A.n_blk, x, y, aux, partials);
       break;
     default:
-      hipLaunchKernelGGL(spmv_rowblock_kernel<kEpiR0>, g, b, 0, s, A.indptr, A.indices, A.vals,
-                         A.blk_row, A.n_blk, x, y, aux, partials);
+      launch_k(spmv_rowblock_kernel<kEpiR0>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
+               x, y, aux, partials);
       break;
   }
   return hipGetLastError();
@@ -167,7 +285,11 @@ __global__ __launch_bounds__(kBlock) void mgs_step_kernel(int64_t n, double* __r
                                                           const double* __restrict__ qn,
                                                           const double* __restrict__ part_in,
                                                           int n_in, double* __restrict__ part_out,
-                                                          double* __restrict__ h_out) {
+                                                          double* __restrict__ h_out,
+                                                          const double* __restrict__ xpart, int n_x,
+                                                          double* __restrict__ x_out,
+                                                          unsigned long long* __restrict__ flag,
+                                                          const unsigned long long* __restrict__ seq) {
 #pragma clang fp contract(off)
   __shared__ double s_wave[4];
   double part = 0.0;
@@ -236,20 +358,25 @@ __global__ __launch_bounds__(kBlock) void mgs_step_kernel(int64_t n, double* __r
   }
   const double tot = block_sum(part, s_wave);
   if (threadIdx.x == 0) part_out[blockIdx.x] = tot;
+  if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (e.g. a residual's partials)
+    const double t = sum_partials(xpart, n_x, s_wave);
+    if (threadIdx.x == 0) publish(x_out, t, flag, seq);
+  }
 }
 
 static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,
-                           int grid, hipStream_t s) {
+                           int grid, hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x,
+                           double* x_out, unsigned long long* flag, const unsigned long long* seq) {
   const bool vec = aligned16(y) && aligned16(qi) && (qnext == nullptr || aligned16(qnext));
   if (vec)
-    hipLaunchKernelGGL(mgs_step_kernel<true>, dim3(grid), dim3(kBlock), 0, s, n, y, qi, qnext,
-                       part_in, n_in, part_out, h_out);
+    launch_k(mgs_step_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qi, qnext, part_in, n_in, part_out,
+             h_out, xpart, n_x, x_out, flag, seq);
   else
-    hipLaunchKernelGGL(mgs_step_kernel<false>, dim3(grid), dim3(kBlock), 0, s, n, y, qi, qnext,
-                       part_in, n_in, part_out, h_out);
+    launch_k(mgs_step_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qi, qnext, part_in, n_in, part_out,
+             h_out, xpart, n_x, x_out, flag, seq);
   return hipGetLastError();
 }
 
@@ -292,9 +419,8 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
 }
 
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
-                            int n_in, double* h_out, hipStream_t s, int grid) {
-  hipLaunchKernelGGL(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, n, y, qnext, part_in, n_in,
-                     h_out);
+                            int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev) {
+  launch_k(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qnext, part_in, n_in, h_out);
   return hipGetLastError();
 }
 
@@ -348,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
 }
 
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y_host_or_dev,
-                       bool y_on_host, const double* x0, double* x, hipStream_t s) {
+                       bool y_on_host, const double* x0, double* x, hipStream_t s, const LaunchEv* ev) {
   if (p > kMaxK || p < 1) return hipErrorInvalidValue;
   const bool vec = aligned16(Z) && (pitch % 2 == 0) && aligned16(x0) && aligned16(x);
   int64_t g = (n / (vec ? 2 : 1) + kBlock - 1) / kBlock;
@@ -361,13 +487,13 @@ hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const d
     for (int i = 0; i < p; ++i) ya.v[i] = y_host_or_dev[i];
   const double* yd = arg ? nullptr : y_host_or_dev;
   if (vec && arg)
-    hipLaunchKernelGGL((gemv_kernel<true, true>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
   else if (vec)
-    hipLaunchKernelGGL((gemv_kernel<true, false>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<true, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
   else if (arg)
-    hipLaunchKernelGGL((gemv_kernel<false, true>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<false, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
   else
-    hipLaunchKernelGGL((gemv_kernel<false, false>), dim3(g), dim3(kBlock), 0, s, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<false, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
   return hipGetLastError();
 }
 
@@ -455,14 +581,17 @@ hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_
 }
 
 __global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restrict__ part, int n_in,
-                                                          double* __restrict__ out, int op) {
+                                                          double* __restrict__ out, int op,
+                                                          unsigned long long* __restrict__ flag,
+                                                          const unsigned long long* __restrict__ seq) {
   __shared__ double s_wave[4];
   const double t = sum_partials(part, n_in, s_wave);
-  if (threadIdx.x == 0) out[0] = op == 1 ? sqrt(t) : t;
+  if (threadIdx.x == 0) publish(out, op == 1 ? sqrt(t) : t, flag, seq);
 }
 
-hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kBlock), 0, s, part, n_in, out, op);
+hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s, const LaunchEv* ev,
+                           unsigned long long* flag, const unsigned long long* seq) {
+  launch_k(finalize_kernel, dim3(1), dim3(kBlock), 0, s, ev, part, n_in, out, op, flag, seq);
   return hipGetLastError();
 }
 

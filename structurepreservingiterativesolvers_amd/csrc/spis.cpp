@@ -97,6 +97,7 @@ struct spis_context {
   double* pinned_dev = nullptr;  // the same memory as seen from the device
   size_t pinned_len = 0;     // doubles
   hipEvent_t ev_arn = nullptr, ev_upd[2] = {nullptr, nullptr};  // solver pipeline events
+  unsigned long long seq = 0;  // last completion sequence number handed to a publishing kernel
   double* gram_part = nullptr;
   size_t gram_part_len = 0;
   double* gram_G = nullptr;
@@ -113,6 +114,9 @@ struct spis_context {
   int prof_period = 1;            // time every prof_period-th Arnoldi iteration
   int prof_iter = 0;              // iteration counter for the sampling
   bool force_generic_gram = false;  // tests: take the MZ + tiled-Gram path
+  bool fuse_spmv = true;            // residual SpMV of U_j + Arnoldi SpMV of A_{j+2} in one launch
+  bool use_graphs = false;          // replay captured Arnoldi steps (opt-in: each replay's boundary
+                                    // costs ~5 us of GPU time, more than the host launches it saves)
   std::vector<hipEvent_t> ev_free;
   struct Pending { int kind; hipEvent_t a, b; };
   std::vector<Pending> ev_pending;
@@ -134,6 +138,8 @@ struct spis_matrix {
   double* vals = nullptr;
   int32_t* blk_row = nullptr;
   int32_t n_blk = 0, n_long = 0;
+  int32_t* blk_row_d = nullptr;  // row blocks of <= kDualCap nnz / items for the fused dual SpMV
+  int32_t n_blk_d = 0;
   bool all_zero = false;
   // halo plan
   int32_t n_ghost = 0;
@@ -142,6 +148,7 @@ struct spis_matrix {
   int32_t* send_idx = nullptr;
   double* send_buf = nullptr;
   CsrView view() const { return CsrView{n_rows, indptr, indices, vals, blk_row, n_blk}; }
+  CsrView dual_view() const { return CsrView{n_rows, indptr, indices, vals, blk_row_d, n_blk_d}; }
 };
 
 struct ConCache {
@@ -173,7 +180,25 @@ struct spis_workspace {
   int steps = 0;
   int n_iter_y = 0;           // iterations with a stored y
   bool broke_at_start = false;
+  double* bcopy = nullptr;    // b copied at solve start: graph nodes never capture caller pointers
+  // captured [dual SpMV + MGS chain + normalise] of Arnoldi step ja (single GPU, no callback),
+  // replayed with one hipGraphLaunch; valid while graph_key matches
+  std::vector<hipGraphExec_t> arn_graph;
+  struct GraphKey {
+    const void* A = nullptr;
+    const double* pinned_dev = nullptr;
+    int gs = 0, gb = 0;
+    bool operator==(const GraphKey& o) const {
+      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb;
+    }
+  } graph_key;
 };
+
+static void drop_graphs(spis_workspace* ws) {
+  for (auto& g : ws->arn_graph)
+    if (g) (void)hipGraphExecDestroy(g);
+  ws->arn_graph.clear();
+}
 
 // ------------------------------------------------------------------------------------------------
 // helpers
@@ -192,22 +217,24 @@ static hipEvent_t prof_event(spis_context* c) {
   return e;
 }
 
-struct ProfScope {  // records [a, b] around the launches issued in its lifetime
+// Sampled live timing: a start/stop event pair carried by the timed launches themselves
+// (hipExtLaunchKernel), so sampling adds no marker packets to the stream.
+struct ProfEv {
   spis_context* c;
   int kind;
-  hipEvent_t a = nullptr;
-  ProfScope(spis_context* c_, int kind_) : c(c_), kind(kind_) {
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfEv(spis_context* c_, int kind_) : c(c_), kind(kind_) {
     if (c->prof && (c->prof_iter % c->prof_period) == 0) {
       a = prof_event(c);
-      (void)hipEventRecord(a, c->stream);
+      b = prof_event(c);
     }
   }
-  ~ProfScope() {
-    if (c->prof && a) {
-      hipEvent_t b = prof_event(c);
-      (void)hipEventRecord(b, c->stream);
-      c->ev_pending.push_back({kind, a, b});
-    }
+  bool on() const { return a != nullptr; }
+  LaunchEv first() const { LaunchEv e; e.start = a; return e; }
+  LaunchEv last() const { LaunchEv e; e.stop = b; return e; }
+  LaunchEv both() const { LaunchEv e; e.start = a; e.stop = b; return e; }
+  ~ProfEv() {
+    if (a) c->ev_pending.push_back({kind, a, b});
   }
 };
 
@@ -262,6 +289,7 @@ static int ensure_pinned(spis_context* c, size_t len) {
   // into host memory, uncached on the GPU side, so a device-scope event release suffices
   HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), len * sizeof(double),
                         hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(c->pinned, 0, len * sizeof(double));  // completion flags start below any seq
   void* dp = nullptr;
   HIP_TRY(hipHostGetDevicePointer(&dp, c->pinned, 0));
   c->pinned_dev = static_cast<double*>(dp);
@@ -371,9 +399,12 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
     // pipeline events only order host reads of the coherent pinned slots: device-scope release
     // (a system-scope one writes back and invalidates L2 at every iteration, ~8 us each);
-    // SPIS_SYSTEM_EVENTS=1 restores the system-scope release
-    const char* se = std::getenv("SPIS_SYSTEM_EVENTS");
-    const unsigned evf = hipEventDisableTiming | ((se && se[0] == '1') ? 0u : hipEventReleaseToDevice);
+    // (SPIS_EVENT_MODE below selects the scope for measurements)
+    // SPIS_EVENT_MODE: 0 system-scope release, 1 device scope (default), 2 no release fence
+    const char* se = std::getenv("SPIS_EVENT_MODE");
+    const int mode = se ? std::atoi(se) : 1;
+    const unsigned evf = hipEventDisableTiming | (mode == 1 ? hipEventReleaseToDevice : 0u) |
+                         (mode == 2 ? hipEventDisableSystemFence : 0u);
     HIP_TRY(hipEventCreateWithFlags(&c->ev_arn, evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
@@ -398,6 +429,8 @@ static void free_workspace(spis_workspace* ws) {
   (void)hipFree(ws->ydev);
   if (ws->ext) (void)hipFree(ws->ext);
   if (ws->Ut) (void)hipFree(ws->Ut);
+  if (ws->bcopy) (void)hipFree(ws->bcopy);
+  drop_graphs(ws);
   for (auto& cc : ws->con) {
     if (cc.MZ) (void)hipFree(cc.MZ);
     if (cc.Mx0) (void)hipFree(cc.Mx0);
@@ -448,6 +481,19 @@ extern "C" int spis_context_stream(spis_context* c, void** s) {
   if (!c || !s) return fail(SPIS_ERR_ARG, "null argument");
   *s = c->stream;
   return SPIS_OK;
+}
+
+extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
+  ABI_GUARD({
+    if (!c) return fail(SPIS_ERR_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    switch (option) {
+      case SPIS_OPT_FUSE_SPMV: c->fuse_spmv = value != 0; return SPIS_OK;
+      case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
+      case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
+      default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
+    }
+  })
 }
 
 extern "C" int spis_profile_enable(spis_context* c, int32_t on) {
@@ -534,21 +580,22 @@ extern "C" int spis_comm_barrier(spis_context* c) {
 // kNnzCap nnz or kItemCap merge items (rows + nnz).  A row with more than kNnzCap entries forms
 // a block of its own (workgroup-wide reduction in the kernel).  For bounded FE rows this is the
 // merge-path partition snapped to row boundaries: every block carries ~kItemCap items.
-static void build_row_blocks(int64_t n, const int32_t* rp, std::vector<int32_t>& blk, int32_t& n_long) {
+static void build_row_blocks(int64_t n, const int32_t* rp, std::vector<int32_t>& blk, int32_t& n_long,
+                             int64_t nnz_cap = kNnzCap, int64_t item_cap = kItemCap) {
   blk.clear();
   blk.push_back(0);
   n_long = 0;
   int64_t rows = 0, nnz = 0;
   for (int64_t r = 0; r < n; ++r) {
     const int64_t len = static_cast<int64_t>(rp[r + 1]) - rp[r];
-    if (len > kNnzCap) {
+    if (len > nnz_cap) {
       if (rows > 0) blk.push_back(static_cast<int32_t>(r));
       blk.push_back(static_cast<int32_t>(r + 1));
       ++n_long;
       rows = nnz = 0;
       continue;
     }
-    if (rows > 0 && (rows + 1 > kRowCap || nnz + len > kNnzCap || rows + 1 + nnz + len > kItemCap)) {
+    if (rows > 0 && (rows + 1 > kRowCap || nnz + len > nnz_cap || rows + 1 + nnz + len > item_cap)) {
       blk.push_back(static_cast<int32_t>(r));
       rows = nnz = 0;
     }
@@ -599,6 +646,13 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       HIP_TRY(hipMemcpy(M->vals, data, sizeof(double) * nnz, hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMemcpy(M->blk_row, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+    {  // the fused residual + Arnoldi SpMV stages two product arrays: half-size blocks keep its LDS
+      int32_t n_long_d = 0;  // at 16 KiB per workgroup (kbench: 52 vs 62 us at C3)
+      build_row_blocks(n_rows, indptr, blk, n_long_d, kDualCap, kDualCap);
+      M->n_blk_d = static_cast<int32_t>(blk.size()) - 1;
+      HIP_TRY(hipMalloc(&M->blk_row_d, sizeof(int32_t) * blk.size()));
+      HIP_TRY(hipMemcpy(M->blk_row_d, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+    }
     if (halo && halo->n_neighbors > 0) {
       M->n_ghost = n_ghost;
       const int nn = halo->n_neighbors;
@@ -638,6 +692,7 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->indices);
     (void)hipFree(M->vals);
     (void)hipFree(M->blk_row);
+    (void)hipFree(M->blk_row_d);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
     delete M;
@@ -1129,11 +1184,22 @@ struct Solver {
   size_t hoff(int j) const { return static_cast<size_t>(j) * (k + 2); }
   size_t roff(int j) const { return static_cast<size_t>(k) * (k + 2) + static_cast<size_t>(j & 1) * kSpmvGrid; }
   size_t yoff() const { return static_cast<size_t>(k) * (k + 2) + 2 * kSpmvGrid; }
+  size_t flag_off() const { return yoff() + kMaxK + 8; }  // completion flag word (beta at +kMaxK)
+  size_t seq_off(int j) const { return yoff() + kMaxK + 9 + (j & 1); }  // seq to publish for U_j
   size_t pinned_need() const { return yoff() + kMaxK + 16; }
+  unsigned long long upd_seq[2] = {0, 0};  // completion sequence number of U_j (slot j & 1)
+  unsigned long long* flag_dev() const { return reinterpret_cast<unsigned long long*>(c->pinned_dev + flag_off()); }
+  const unsigned long long* seq_dev(int j) const {
+    return reinterpret_cast<const unsigned long long*>(c->pinned_dev + seq_off(j));
+  }
+  void next_seq(int j) {  // the kernel that publishes U_j reads its seq from pinned memory
+    upd_seq[j & 1] = ++c->seq;
+    *reinterpret_cast<volatile unsigned long long*>(c->pinned + seq_off(j)) = upd_seq[j & 1];
+  }
 
-  int enqueue_arnoldi(int j) {  // solvers.py:190-198
+  // A_j = arnoldi_pre (preconditioner + halo) -> Arnoldi SpMV -> arnoldi_post (MGS + normalise)
+  int arnoldi_pre(int j) {  // solvers.py:190
     hipStream_t s = c->stream;
-    c->prof_iter = j;
     double* zj = Zv(j);
     if (o->pre_matrix) {
       ST_TRY(spmv_local(c, ws, o->pre_matrix, Qv(j), zj));
@@ -1146,60 +1212,176 @@ struct Solver {
         return fail(SPIS_ERR_CALLBACK, "preconditioner callback failed at iteration %d", j);
       HIP_TRY(hipMemcpyAsync(zj, hostz.data(), sizeof(double) * n, hipMemcpyHostToDevice, s));
     }
-    ST_TRY(exchange(c, A, zj));
-    {
-      ProfScope ps(c, SPIS_PROF_SPMV);
-      HIP_TRY(launch_spmv(A->view(), kEpiDot, zj, ws->w, Qv(0), c->partA, gs, s));
-    }
+    return exchange(c, A, zj);
+  }
+
+  // (xpart, x_out, done): the first MGS step also reduces the previous update's residual partials
+  // into host memory and carries that update's completion event (single GPU, fused path)
+  int arnoldi_post(int j, const double* xpart = nullptr, double* x_out = nullptr,
+                   unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr) {
+    hipStream_t s = c->stream;
+    c->prof_iter = j;
     ST_TRY(allreduce(c, c->partA, gs));
     double* hcol = c->pinned_dev + hoff(j);  // the kernels write H[:, j] straight to host memory
-    {
-      ProfScope pm(c, SPIS_PROF_MGS);
-      double* src = c->partA;
-      double* dst = c->partB;
-      int n_in = gs;
-      for (int i = 0; i <= j; ++i) {
-        const double* qn = i < j ? Qv(i + 1) : nullptr;
+    ProfEv pm(c, SPIS_PROF_MGS);  // start on the first MGS step, stop on the normalise
+    const LaunchEv e_first = pm.first();
+    const LaunchEv e_last = pm.last();
+    double* src = c->partA;
+    double* dst = c->partB;
+    int n_in = gs;
+    for (int i = 0; i <= j; ++i) {
+      const double* qn = i < j ? Qv(i + 1) : nullptr;
+      if (i == 0)
+        HIP_TRY(launch_mgs_step(n, ws->w, Qv(i), qn, src, n_in, dst, hcol + i, gb, s, &e_first, xpart, gs, x_out,
+                                flag, seq));
+      else
         HIP_TRY(launch_mgs_step(n, ws->w, Qv(i), qn, src, n_in, dst, hcol + i, gb, s));
-        ST_TRY(allreduce(c, dst, gb));
-        std::swap(src, dst);
-        n_in = gb;
-      }
-      HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, hcol + j + 1, s, gb));
+      ST_TRY(allreduce(c, dst, gb));
+      std::swap(src, dst);
+      n_in = gb;
     }
+    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, hcol + j + 1, s, gb, &e_last));
     return SPIS_OK;
   }
 
-  int enqueue_update(int j, int p, const double* y) {  // solvers.py:287,290
+  int enqueue_arnoldi(int j) {  // solvers.py:190-198
+    c->prof_iter = j;
+    ST_TRY(arnoldi_pre(j));
+    {
+      ProfEv ps(c, SPIS_PROF_SPMV);
+      const LaunchEv le = ps.both();
+      HIP_TRY(launch_spmv(A->dual_view(), kEpiDot, Zv(j), ws->w, Qv(0), c->partA, gs, c->stream, &le));
+    }
+    return arnoldi_post(j);
+  }
+
+  // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
+  int update_gemv(int j, int p, const double* y) {  // solvers.py:287
     hipStream_t s = c->stream;
     c->prof_iter = j;
     {
-      ProfScope pg(c, SPIS_PROF_GEMV);
+      ProfEv pg(c, SPIS_PROF_GEMV);
+      const LaunchEv le = pg.both();
       if (p <= kYArg) {
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, ws->xj, s));
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, ws->xj, s, &le));
       } else {
         double* yh = c->pinned + yoff();
         for (int a = 0; a < p; ++a) yh[a] = y[a];
         HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, ws->xj, s));
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, ws->xj, s, &le));
       }
     }
-    ST_TRY(exchange(c, A, ws->xj));
-    double* rpart = c->comm ? c->partR : c->pinned_dev + roff(j);
-    {
-      ProfScope ps(c, SPIS_PROF_SPMV_RES);
-      HIP_TRY(launch_spmv(A->view(), kEpiResNorm, ws->xj, nullptr, b, rpart, gs, s));
-    }
-    if (c->comm) {
-      ST_TRY(allreduce(c, c->partR, gs));
-      HIP_TRY(hipMemcpyAsync(c->pinned + roff(j), c->partR, sizeof(double) * gs, hipMemcpyDeviceToHost, s));
-    }
+    return exchange(c, A, ws->xj);
+  }
+
+  // U_j's true-residual partials go to device memory (partR).  Single GPU: one workgroup reduces
+  // them into the host slot roff(j) and publishes upd_seq[j & 1] to the host flag after a
+  // system-scope release (the first MGS step of A_{j+2} when fused, else a finalize kernel): no
+  // event, marker or completion signal on the stream (each costs 4-7 us, tools/kbench sig).
+  // Multi-GPU: all-reduce, copy the partials, event marker.
+  int update_comm_finish(int j) {
+    hipStream_t s = c->stream;
+    ST_TRY(allreduce(c, c->partR, gs));
+    HIP_TRY(hipMemcpyAsync(c->pinned + roff(j), c->partR, sizeof(double) * gs, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(c->ev_upd[j & 1], s));
     return SPIS_OK;
   }
 
-  double residual(int j) const {  // fixed-order host sum of the partials of U_j
+  int enqueue_update(int j, int p, const double* y) {  // solvers.py:287,290
+    ST_TRY(update_gemv(j, p, y));
+    {
+      ProfEv ps(c, SPIS_PROF_SPMV_RES);
+      const LaunchEv le = ps.both();
+      HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, ws->xj, nullptr, b, c->partR, gs, c->stream, &le));
+    }
+    if (c->comm) return update_comm_finish(j);
+    next_seq(j);
+    HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
+    return SPIS_OK;
+  }
+
+  // the dual SpMV of (U_j, A_ja) and A_ja's MGS chain + normalise, as launched on the stream
+  int fused_tail(int j, int ja) {
+    c->prof_iter = j;
+    {
+      ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
+      const LaunchEv le = pd.both();
+      HIP_TRY(launch_spmv_dual(A->dual_view(), ws->xj, ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
+                               c->stream, &le));
+    }
+    if (c->comm) {
+      ST_TRY(update_comm_finish(j));
+      return arnoldi_post(ja);
+    }
+    return arnoldi_post(ja, c->partR, c->pinned_dev + roff(j), flag_dev(), seq_dev(j));
+  }
+
+  bool graphable() const { return c->use_graphs && !c->comm && !o->pre_fn && !o->pre_matrix; }
+
+  // captured once per workspace and step index; every pointer in it is a workspace / context /
+  // matrix pointer (graph_key), the per-call values (seq) are read from pinned memory
+  int arn_graph(int ja, hipGraphExec_t* out) {
+    const spis_workspace::GraphKey key{A, c->pinned_dev, gs, gb};
+    if (!(ws->graph_key == key)) {
+      drop_graphs(ws);
+      ws->graph_key = key;
+    }
+    if (ws->arn_graph.size() < static_cast<size_t>(k + 2)) ws->arn_graph.resize(k + 2, nullptr);
+    if (!ws->arn_graph[ja]) {
+      const bool prof = c->prof;
+      c->prof = false;  // no events inside a captured graph
+      hipGraph_t g = nullptr;
+      HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      const int st = fused_tail(ja - 2, ja);
+      const hipError_t ec = hipStreamEndCapture(c->stream, &g);
+      c->prof = prof;
+      ST_TRY(st);
+      HIP_TRY(ec);
+      hipGraphExec_t ge = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIP_TRY(ei);
+      ws->arn_graph[ja] = ge;
+    }
+    *out = ws->arn_graph[ja];
+    return SPIS_OK;
+  }
+
+  // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
+  int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
+    ST_TRY(update_gemv(j, p, y));
+    ST_TRY(arnoldi_pre(ja));
+    if (!c->comm) next_seq(j);
+    const bool sampled = c->prof && ((j % c->prof_period) == 0 || (ja % c->prof_period) == 0);
+    if (graphable() && !sampled) {
+      hipGraphExec_t ge = nullptr;
+      ST_TRY(arn_graph(ja, &ge));
+      HIP_TRY(hipGraphLaunch(ge, c->stream));
+      return SPIS_OK;
+    }
+    return fused_tail(j, ja);
+  }
+
+  // host wait for U_j (which also covers every earlier launch on the stream)
+  int wait_update(int j) const {
+    if (c->comm) return wait_event(c->ev_upd[j & 1]);
+    const unsigned long long want = upd_seq[j & 1];
+    const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(c->pinned + flag_off());
+    for (unsigned spin = 0;; ++spin) {
+      if (__atomic_load_n(fl, __ATOMIC_ACQUIRE) >= want) return SPIS_OK;
+      if ((spin & 1023) == 1023) {  // a failed launch must not leave the host spinning forever
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e != hipSuccess && e != hipErrorNotReady) return fail(SPIS_ERR_HIP, "stream: %s", hipGetErrorString(e));
+        if (e == hipSuccess && __atomic_load_n(fl, __ATOMIC_ACQUIRE) < want)
+          return fail(SPIS_ERR_STATE, "update %d drained without publishing its residual", j);
+      }
+      __builtin_ia32_pause();
+    }
+  }
+
+  double residual(int j) const {  // ||A x_j - b||: device-reduced (1 GPU) or fixed-order host sum
     const double* q = c->pinned + roff(j);
+    if (!c->comm) return std::sqrt(q[0]);
     double t = 0.0;
     for (int i = 0; i < gs; ++i) t += q[i];
     return std::sqrt(t);
@@ -1237,7 +1419,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     const bool use_cb = o->conls_fn != nullptr;
     if (!use_cb && o->n_constraints > 0) ST_TRY(ensure_con_cache(ws, o->n_constraints, o->constraints));
 
-    Solver S{c, A, o, ws, b, n, k, spmv_grid(A->view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
+    // every solver SpMV runs on the kDualCap row blocks, so the fused and the single launches
+    // group their partial sums identically (bit-identical results either way)
+    Solver S{c, A, o, ws, b, n, k, spmv_grid(A->dual_view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
     ST_TRY(ensure_pinned(c, S.pinned_need()));
     hipStream_t s = c->stream;
     double* stamps = out->stamps_host;  // [0,k) iter start, [k,2k) iter end, [2k,3k) con start, [3k,4k) con end
@@ -1249,10 +1433,12 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
 
     // r0 = b - A x0 ; beta = ||r0|| ; q0 = r0 / beta      (solvers.py:167-177)
+    if (!ws->bcopy) HIP_TRY(hipMalloc(&ws->bcopy, sizeof(double) * ws->pitch));
+    HIP_TRY(launch_copy(n, b, ws->bcopy, s));
     HIP_TRY(launch_copy(n, x0, ws->x0, s));
     HIP_TRY(launch_copy(n, x0, ws->xj, s));
     ST_TRY(exchange(c, A, ws->xj));
-    HIP_TRY(launch_spmv(A->view(), kEpiR0, ws->xj, ws->r0, b, c->partA, S.gs, s));
+    HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, ws->xj, ws->r0, b, c->partA, S.gs, s));
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
@@ -1283,7 +1469,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
     }
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
-      ST_TRY(wait_event(j == 0 ? c->ev_arn : c->ev_upd[(j - 1) & 1]));
+      ST_TRY(j == 0 ? wait_event(c->ev_arn) : S.wait_update(j - 1));
       prof_drain(c);
       if (pending >= 0) {  // finish iteration j-1: true residual + stop test (solvers.py:290-297)
         out->res_host[n_res++] = S.residual(pending);
@@ -1397,13 +1583,18 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         out->y_host[static_cast<size_t>(j) * k + a] = y[a];
       }
       ws->n_iter_y = j + 1;
-      ST_TRY(S.enqueue_update(j, p, y.data()));
+      if (j + 2 < k && c->fuse_spmv) {
+        if (stamps) stamps[j + 2] = now_s();
+        ST_TRY(S.enqueue_update_arnoldi(j, p, y.data(), j + 2));
+      } else {
+        ST_TRY(S.enqueue_update(j, p, y.data()));
+        if (j + 2 < k) {
+          if (stamps) stamps[j + 2] = now_s();
+          ST_TRY(S.enqueue_arnoldi(j + 2));
+        }
+      }
       have_x = true;
       pending = j;
-      if (j + 2 < k) {
-        if (stamps) stamps[j + 2] = now_s();
-        ST_TRY(S.enqueue_arnoldi(j + 2));
-      }
     }
     // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
     // Arnoldi step, which never touches xj / r0), then one synchronisation
@@ -1412,7 +1603,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       else HIP_TRY(launch_copy(n, have_x ? ws->xj : ws->r0, out->x_final_dev, s));
     }
     if (pending >= 0) {
-      ST_TRY(wait_event(c->ev_upd[pending & 1]));
+      ST_TRY(S.wait_update(pending));
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
     }

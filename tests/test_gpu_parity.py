@@ -224,6 +224,42 @@ def test_fused_and_generic_constraint_reduction_agree(spis):
     np.testing.assert_allclose(xf, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
 
 
+def test_fused_dual_spmv_bit_identical(spis):
+    """SPIS_OPT_FUSE_SPMV / SPIS_OPT_GRAPHS: the true-residual SpMV of U_j fused with the Arnoldi
+    SpMV of A_{j+2} (matrix read once), and the Arnoldi steps replayed from captured graphs, give
+    bit-identical iterates, residuals, LS solutions and basis."""
+    from structurepreservingiterativesolvers_amd import _lib, solvers
+    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    ctx = get_context()
+    outs = []
+    for case in ("swe", "lkdv"):
+        if case == "swe":
+            dic, _ = sa.linforms(M=20)
+            cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+            A, b = dic["A"], dic["b"]
+        else:
+            c = Case("lkdv_m50_cgmres_tol1e-19")
+            A, b, cons = c.A, c.b, c.conlist()
+        runs = []
+        for fuse, graphs in ((0, 0), (1, 0), (1, 1), (1, 1)):  # the last run replays cached graphs
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, graphs), "spis_set_option")
+            try:
+                x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
+            finally:
+                _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 1), "spis_set_option")
+                _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1), "spis_set_option")
+            runs.append((x, np.asarray(d["res"]), np.concatenate(d["x"].y), d["x"].basis(25), np.asarray(d["x"])))
+        for r in runs[1:]:
+            for a, bb in zip(runs[0], r):
+                assert np.array_equal(a, bb), case
+        outs.append(case)
+    assert outs == ["swe", "lkdv"]
+
+
 def test_lkdvrk_dict_form_through_callback(spis):
     """lift=False keeps the reference's dict-form constraints (host SLSQP through
     the constrained-LS callback of spis_solve)."""

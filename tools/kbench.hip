@@ -3,6 +3,7 @@
 // events, back-to-back launches like the solver issues them.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -225,6 +226,167 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double S = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
+  if (argc > 2 && std::string(argv[2]) == "sig") {
+    // cost of host-visible completion signals between dependent kernels: 100 x (copy 8 MB)
+    const int64_t m = (n / 2) & ~int64_t(1);
+    auto k = [&](const LaunchEv* ev) {
+      launch_k(copy2_kernel, dim3(2048), dim3(kBlock), 0, s, ev, m / 2, reinterpret_cast<const double2*>(dx),
+               reinterpret_cast<double2*>(dy));
+    };
+    hipEvent_t evd, evs, evn, evt;
+    CK(hipEventCreateWithFlags(&evd, hipEventDisableTiming | hipEventReleaseToDevice));
+    CK(hipEventCreateWithFlags(&evs, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&evn, hipEventDisableTiming | hipEventDisableSystemFence));
+    CK(hipEventCreate(&evt));
+    uint64_t* flag;
+    CK(hipHostMalloc(reinterpret_cast<void**>(&flag), 64, hipHostMallocMapped | hipHostMallocCoherent));
+    void* flag_dev;
+    CK(hipHostGetDevicePointer(&flag_dev, flag, 0));
+    auto run = [&](const char* name, int mode) {
+      for (int w = 0; w < 2; ++w) {
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < 100; ++i) {
+          LaunchEv le;
+          if (mode == 4) le.stop = evd;
+          if (mode == 5) le.stop = evs;
+          if (mode == 6) le.stop = evn;
+          if (mode == 7) le.stop = evt;
+          k(mode >= 4 && mode <= 7 ? &le : nullptr);
+          if (mode == 1) CK(hipEventRecord(evd, s));
+          if (mode == 2) CK(hipEventRecord(evs, s));
+          if (mode == 3) CK(hipEventRecord(evn, s));
+          if (mode == 8) CK(hipStreamWriteValue64(s, flag_dev, i + 1, 0));
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (w == 1) printf("%-52s %8.2f us per kernel\n", name, 1e3 * ms / 100);
+      }
+    };
+    {  // host-side enqueue cost of back-to-back MGS-step launches (GPU kept busy by a long copy)
+      double* big;
+      const int64_t mb = int64_t(1) << 27;
+      CK(hipMalloc(&big, 16 * mb));
+      for (int rep = 0; rep < 2; ++rep) {
+        CK(hipStreamSynchronize(s));
+        hipLaunchKernelGGL(copy2_kernel, dim3(4096), dim3(kBlock), 0, s, mb / 2, reinterpret_cast<const double2*>(big),
+                           reinterpret_cast<double2*>(big + mb));  // ~0.5 ms of GPU work queued first
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < 60; ++i)
+          (void)launch_mgs_step(n, dy, dQ, dQ + pitch, dpart, 1024, dpart2, dh, 490, s);
+        const auto t1 = std::chrono::steady_clock::now();
+        CK(hipStreamSynchronize(s));
+        if (rep == 1)
+          printf("host enqueue, launch_mgs_step: %.2f us per launch\n",
+                 std::chrono::duration<double, std::micro>(t1 - t0).count() / 60);
+      }
+      for (int rep = 0; rep < 2; ++rep) {
+        CK(hipStreamSynchronize(s));
+        hipLaunchKernelGGL(copy2_kernel, dim3(4096), dim3(kBlock), 0, s, mb / 2, reinterpret_cast<const double2*>(big),
+                           reinterpret_cast<double2*>(big + mb));
+        LaunchEv le;
+        le.stop = evt;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < 60; ++i)
+          (void)launch_mgs_step(n, dy, dQ, dQ + pitch, dpart, 1024, dpart2, dh, 490, s, &le);
+        const auto t1 = std::chrono::steady_clock::now();
+        CK(hipStreamSynchronize(s));
+        if (rep == 1)
+          printf("host enqueue, ext launch + stop event: %.2f us per launch\n",
+                 std::chrono::duration<double, std::micro>(t1 - t0).count() / 60);
+      }
+      CK(hipFree(big));
+    }
+    {  // 30-step MGS chain: eager launches vs one captured graph (host enqueue + GPU time)
+      auto chain = [&]() {
+        for (int i = 0; i < 30; ++i)
+          (void)launch_mgs_step(n, dy, dQ + i * pitch, dQ + (i + 1) * pitch, (i & 1) ? dpart2 : dpart, 490,
+                                (i & 1) ? dpart : dpart2, dh + i, 490, s);
+      };
+      hipGraph_t gr;
+      hipGraphExec_t ge;
+      CK(hipStreamSynchronize(s));
+      CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      chain();
+      CK(hipStreamEndCapture(s, &gr));
+      CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+      for (int mode = 0; mode < 2; ++mode) {
+        double host = 0.0;
+        float gpu = 0.f;
+        for (int rep = 0; rep < 6; ++rep) {
+          CK(hipStreamSynchronize(s));
+          CK(hipEventRecord(e0, s));
+          const auto t0 = std::chrono::steady_clock::now();
+          if (mode == 0) chain();
+          else CK(hipGraphLaunch(ge, s));
+          const auto t1 = std::chrono::steady_clock::now();
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (rep >= 2) {
+            host += std::chrono::duration<double, std::micro>(t1 - t0).count();
+            gpu += ms;
+          }
+        }
+        printf("MGS chain x30 %-6s: host enqueue %7.1f us, GPU %7.1f us\n", mode == 0 ? "eager" : "graph", host / 4,
+               1e3 * gpu / 4);
+      }
+      CK(hipGraphExecDestroy(ge));
+      CK(hipGraphDestroy(gr));
+    }
+    {  // graph boundary cost: 20 replays of a 5-step MGS graph vs 100 eager steps (GPU time)
+      auto chain5 = [&]() {
+        for (int i = 0; i < 5; ++i)
+          (void)launch_mgs_step(n, dy, dQ + i * pitch, dQ + (i + 1) * pitch, (i & 1) ? dpart2 : dpart, 490,
+                                (i & 1) ? dpart : dpart2, dh + i, 490, s);
+      };
+      hipGraph_t gr;
+      hipGraphExec_t ge;
+      CK(hipStreamSynchronize(s));
+      CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      chain5();
+      CK(hipStreamEndCapture(s, &gr));
+      CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+      for (int mode = 0; mode < 3; ++mode) {
+        float best = 1e30f;
+        for (int rep = 0; rep < 4; ++rep) {
+          CK(hipStreamSynchronize(s));
+          CK(hipEventRecord(e0, s));
+          for (int g = 0; g < 20; ++g) {
+            if (mode == 0) chain5();
+            if (mode == 1) CK(hipGraphLaunch(ge, s));
+            if (mode == 2) {  // graph + one eager kernel between replays
+              CK(hipGraphLaunch(ge, s));
+              (void)launch_mgs_step(n, dy, dQ, dQ + pitch, dpart, 490, dpart2, dh, 490, s);
+            }
+          }
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          best = ms < best ? ms : best;
+        }
+        const int steps = mode == 2 ? 120 : 100;
+        printf("MGS steps %-22s: %6.2f us per step\n", mode == 0 ? "eager" : mode == 1 ? "20 x graph(5)" : "graph(5) + eager",
+               1e3 * best / steps);
+      }
+      CK(hipGraphExecDestroy(ge));
+      CK(hipGraphDestroy(gr));
+    }
+    run("copy 8 MB, no signal", 0);
+    run("copy + marker event (device-scope release)", 1);
+    run("copy + marker event (system-scope release)", 2);
+    run("copy + marker event (no fence)", 3);
+    run("copy with ext stop event (device-scope flags)", 4);
+    run("copy with ext stop event (system-scope flags)", 5);
+    run("copy with ext stop event (no fence flags)", 6);
+    run("copy with ext stop event (timing event)", 7);
+    run("copy + hipStreamWriteValue64 to host", 8);
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "pmc") {
     // PMC mode: 3 calibration streams of 1 GiB each (known bytes), then 5 Arnoldi SpMVs
     const int64_t m8 = int64_t(1) << 27;
@@ -308,6 +470,42 @@ int main(int argc, char** argv) {
       }
     }
     CK(hipFree(dblk));
+  }
+  // ---- fused residual + Arnoldi SpMV vs the two single launches
+  {
+    double *dx2, *dw, *dpr;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&dpr, 8 * 8192));
+    CK(hipMemcpy(dx2, hx.data(), 8 * pitch, hipMemcpyHostToDevice));
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    for (int cap : {1024, 2048}) {
+      std::vector<int32_t> blk;
+      blocks(n, rp.data(), cap, 256, cap, blk);
+      CK(hipMalloc(&dblk, 4 * blk.size()));
+      CK(hipMemcpy(dblk, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+      const int nb = static_cast<int>(blk.size()) - 1;
+      CsrView A{n, drp, dci, dva, dblk, nb};
+      for (int g : {1024, 2048, 4096}) {
+        const int gg = g < nb ? g : nb;
+        char nm[128];
+        snprintf(nm, sizeof nm, "spmv res+arn (2 launches) cap=%d grid=%d", cap, gg);
+        timeit(nm, 50, SD, [&] {
+          (void)launch_spmv(A, kEpiResNorm, dx, nullptr, dy, dpr, gg, s);
+          (void)launch_spmv(A, kEpiDot, dx2, dw, dQ, dpart, gg, s);
+        });
+        snprintf(nm, sizeof nm, "spmv dual cap=%d grid=%d", cap, gg);
+        timeit(nm, 50, SD, [&] {
+          if (cap == 1024)
+            hipLaunchKernelGGL(spmv_dual_kernel<1024>, dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy,
+                               dpr, dx2, dw, dQ, dpart);
+          else
+            hipLaunchKernelGGL(spmv_dual_kernel<2048>, dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy,
+                               dpr, dx2, dw, dQ, dpart);
+        });
+      }
+      CK(hipFree(dblk));
+    }
   }
   // ---- MGS chain of 30 steps (y, q_i, q_{i+1})
   const double mgsB = 32.0 * n;
