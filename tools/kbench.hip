@@ -119,6 +119,65 @@ __global__ __launch_bounds__(kBlock) void spmv_v1(const int32_t* __restrict__ rp
   }
 }
 
+// ---- dual SpMV with x1/x2 interleaved (one 16-B gather per nonzero) ------------------------------
+template <int CAP>
+__global__ __launch_bounds__(kBlock) void spmv_dual_il(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                       const double* __restrict__ va, const int32_t* __restrict__ blk_row,
+                                                       int n_blk, const double2* __restrict__ xz,
+                                                       const double* __restrict__ b, double* __restrict__ part1,
+                                                       double* __restrict__ w, const double* __restrict__ q0,
+                                                       double* __restrict__ part2) {
+  __shared__ double2 s_p[CAP];
+  __shared__ double s_wave[4];
+  double pt1 = 0.0, pt2 = 0.0;
+  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int r0 = blk_row[blk];
+    const int r1 = blk_row[blk + 1];
+    const int nz0 = rp[r0];
+    const int nnz = rp[r1] - nz0;
+    constexpr int kPer = CAP / kBlock;
+    int cols[kPer];
+    double vals[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      cols[u] = i < nnz ? ci[nz0 + i] : 0;
+      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+    }
+    double2 g[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) g[u] = xz[cols[u]];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < nnz) s_p[i] = make_double2(vals[u] * g[u].x, vals[u] * g[u].y);
+    }
+    __syncthreads();
+    const int r = r0 + threadIdx.x;
+    if (r < r1) {
+      const int s0 = rp[r] - nz0;
+      const int e = rp[r + 1] - nz0;
+      double s1 = 0.0, s2 = 0.0;
+      for (int t = s0; t < e; ++t) {
+        const double2 pp = s_p[t];
+        s1 += pp.x;
+        s2 += pp.y;
+      }
+      const double t = s1 - b[r];
+      pt1 += t * t;
+      w[r] = s2;
+      pt2 += q0[r] * s2;
+    }
+    __syncthreads();
+  }
+  const double tot1 = block_sum(pt1, s_wave);
+  const double tot2 = block_sum(pt2, s_wave);
+  if (threadIdx.x == 0) {
+    part1[blockIdx.x] = tot1;
+    part2[blockIdx.x] = tot2;
+  }
+}
+
 // ---- MGS variant: PER pairs per thread, all loads first ---------------------------------------
 template <int PER>
 __global__ __launch_bounds__(kBlock) void mgs_v1(int64_t n, double* __restrict__ y, const double* __restrict__ qi,
@@ -376,6 +435,29 @@ int main(int argc, char** argv) {
       CK(hipGraphExecDestroy(ge));
       CK(hipGraphDestroy(gr));
     }
+    {  // MGS chain writing h to device memory vs to mapped pinned host memory (as the solver does)
+      double* hp;
+      CK(hipHostMalloc(reinterpret_cast<void**>(&hp), 8 * 64, hipHostMallocMapped | hipHostMallocCoherent));
+      double* hpd;
+      CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hpd), hp, 0));
+      for (int mode = 0; mode < 2; ++mode) {
+        double* hh = mode == 0 ? dh : hpd;
+        float best = 1e30f;
+        for (int rep = 0; rep < 5; ++rep) {
+          CK(hipStreamSynchronize(s));
+          CK(hipEventRecord(e0, s));
+          for (int i = 0; i < 30; ++i)
+            (void)launch_mgs_step(n, dy, dQ + i * pitch, dQ + (i + 1) * pitch, (i & 1) ? dpart2 : dpart, 490,
+                                  (i & 1) ? dpart : dpart2, hh + i, 490, s);
+          CK(hipEventRecord(e1, s));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          best = ms < best ? ms : best;
+        }
+        printf("MGS chain x30, h to %-12s: %6.2f us per step\n", mode == 0 ? "device" : "pinned host", 1e3 * best / 30);
+      }
+    }
     run("copy 8 MB, no signal", 0);
     run("copy + marker event (device-scope release)", 1);
     run("copy + marker event (system-scope release)", 2);
@@ -405,6 +487,21 @@ int main(int argc, char** argv) {
     const int g = A.n_blk < 2048 ? A.n_blk : 2048;
     for (int i = 0; i < 5; ++i) CK(launch_spmv(A, kEpiDot, dx, dy, dQ, dpart, g, s));
     const int nb = A.n_blk;
+    {  // the solver's fused residual + Arnoldi SpMV on its kDualCap row blocks
+      std::vector<int32_t> blkd;
+      blocks(n, rp.data(), kDualCap, 256, kDualCap, blkd);
+      int32_t* dblkd;
+      CK(hipMalloc(&dblkd, 4 * blkd.size()));
+      CK(hipMemcpy(dblkd, blkd.data(), 4 * blkd.size(), hipMemcpyHostToDevice));
+      CsrView Ad{n, drp, dci, dva, dblkd, static_cast<int>(blkd.size()) - 1};
+      double *dx2, *dw, *dpr;
+      CK(hipMalloc(&dx2, 8 * pitch));
+      CK(hipMalloc(&dw, 8 * pitch));
+      CK(hipMalloc(&dpr, 8 * 8192));
+      CK(hipMemcpy(dx2, hx.data(), 8 * pitch, hipMemcpyHostToDevice));
+      for (int i = 0; i < 5; ++i) CK(launch_spmv_dual(Ad, dx, dy, dpr, dx2, dw, dQ, dpart, g, s));
+      CK(hipStreamSynchronize(s));
+    }
     for (int i = 0; i < 5; ++i)
       hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1, false>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
     for (int i = 0; i < 5; ++i)
@@ -473,7 +570,9 @@ int main(int argc, char** argv) {
   }
   // ---- fused residual + Arnoldi SpMV vs the two single launches
   {
-    double *dx2, *dw, *dpr;
+    double *dx2, *dw, *dpr, *dxz;
+    CK(hipMalloc(&dxz, 16 * pitch));
+    CK(hipMemset(dxz, 0, 16 * pitch));
     CK(hipMalloc(&dx2, 8 * pitch));
     CK(hipMalloc(&dw, 8 * pitch));
     CK(hipMalloc(&dpr, 8 * 8192));
@@ -493,6 +592,15 @@ int main(int argc, char** argv) {
         timeit(nm, 50, SD, [&] {
           (void)launch_spmv(A, kEpiResNorm, dx, nullptr, dy, dpr, gg, s);
           (void)launch_spmv(A, kEpiDot, dx2, dw, dQ, dpart, gg, s);
+        });
+        snprintf(nm, sizeof nm, "spmv dual interleaved cap=%d grid=%d", cap, gg);
+        timeit(nm, 50, SD, [&] {
+          if (cap == 1024)
+            hipLaunchKernelGGL(spmv_dual_il<1024>, dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb,
+                               reinterpret_cast<const double2*>(dxz), dy, dpr, dw, dQ, dpart);
+          else
+            hipLaunchKernelGGL(spmv_dual_il<2048>, dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb,
+                               reinterpret_cast<const double2*>(dxz), dy, dpr, dw, dQ, dpart);
         });
         snprintf(nm, sizeof nm, "spmv dual cap=%d grid=%d", cap, gg);
         timeit(nm, 50, SD, [&] {
