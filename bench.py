@@ -151,6 +151,8 @@ def main():
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
+    ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
+                    help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
                     help="time every n-th iteration's kernels with HIP events inside the timed region")
     args = ap.parse_args()
@@ -177,6 +179,8 @@ def main():
     conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1 if args.graphs else 0), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 0 if args.no_fuse else 1), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
+               "spis_set_option")
 
     if wl["cycles"] > 1:
         def solve():
@@ -254,6 +258,7 @@ def main():
             "workload": wl["desc"] + f", N={n:,} DoF, nnz={A.nnz:,}, CGMRES(k={args.k}, tol={args.tol:g})"
                         + (f" restarted x{wl['cycles']}" if wl["cycles"] > 1 else ""),
             "config": args.config,
+            "orthogonalisation": args.orthog,
             "global_dof": n,
             "k": args.k,
             "parallelism": "single GPU",

@@ -120,8 +120,12 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   SpMM + tiled Gram path instead of the fused kernel (tests).
  * SPIS_OPT_GRAPHS (default 0): replay each Arnoldi step's launches (fused SpMV, MGS chain,
  *   normalise) from a captured hipGraph (single GPU, no host preconditioner callback).  Cuts host
- *   enqueue time ~9x, but each replay adds ~5 us of GPU time at its boundary: C3 is 2% slower. */
-enum spis_option { SPIS_OPT_FUSE_SPMV = 1, SPIS_OPT_GENERIC_GRAM = 2, SPIS_OPT_GRAPHS = 3 };
+ *   enqueue time ~9x, but each replay adds ~5 us of GPU time at its boundary: C3 is 2% slower.
+ * SPIS_OPT_ORTHOG (default 0): 0 = modified Gram-Schmidt (the reference's, solvers.py:193-195);
+ *   1 = CGS2, classical Gram-Schmidt with one re-orthogonalisation pass (3 reductions per
+ *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
+ *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only. */
+enum spis_option { SPIS_OPT_FUSE_SPMV = 1, SPIS_OPT_GENERIC_GRAM = 2, SPIS_OPT_GRAPHS = 3, SPIS_OPT_ORTHOG = 4 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 
 /* ---- multi-GPU (RCCL over xGMI) ----------------------------------------------

@@ -18,6 +18,7 @@ constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's L
 constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
 constexpr int kGramMaxVec = 64;  // max vectors on either side of one Gram launch (<= 256 4x4 tiles)
 constexpr int kYArg = 128;
+constexpr int kCgsMax = 32;      // basis vectors per step of the opt-in CGS2 orthogonalisation
 constexpr int kMgsPer = 4;       // 16-B pairs per lane per round in MGS / normalise (loads issued first)
 constexpr int kConGramGrid = 1024;  // max workgroups (partial slots) of the fused constraint Gram      // GEMV coefficients passed by value up to this p
 
@@ -73,6 +74,16 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // h = sqrt(sum(part_in)); q_next = y / h (if h != 0)
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
+
+// K2c (opt-in CGS2): part = nv x grid partials of q_i . w; update w -= Q coef with, if dot, the
+// nv x grid partials of q_i . w' (else ||w'||^2 partials, grid of them); finalize: workgroup i
+// reduces vector i's partials into c[i] and, with h_out, writes add[i] + c[i] there.
+hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
+                          hipStream_t s, const LaunchEv* ev = nullptr);
+hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
+                             bool dot, double* part, int grid, hipStream_t s);
+hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
+                               hipStream_t s);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,

@@ -425,6 +425,129 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 }
 
 // ---------------------------------------------------------------------------------------------
+// K2c: CGS2 ("classical Gram-Schmidt, twice") — the opt-in low-synchronisation orthogonalisation
+// (SURVEY §8e).  Per Arnoldi step with nv = j+1 <= kCgsMax basis vectors:
+//   cgs_dot:       c1_i partials = q_i . w                 (one pass, all nv dots)
+//   cgs_finalize:  c1 (device)
+//   cgs_update<1>: w' = w - sum_i c1_i q_i ; c2_i partials = q_i . w'
+//   cgs_finalize:  c2 (device); h_i = c1_i + c2_i -> host H column
+//   cgs_update<0>: w'' = w' - sum_i c2_i q_i ; ||w''||^2 partials   -> normalize_kernel
+// 3 reductions per step instead of MGS's j+2 (one all-reduce each on several GPUs); not MGS's
+// arithmetic (the reference's, solvers.py:193-195), so it is never the default.
+// ---------------------------------------------------------------------------------------------
+// per-block partials of nv sums: waves reduce by butterfly, the 4 wave sums combine in order
+__device__ __forceinline__ void store_partials(const double* acc, int nv, double* s_red, double* part) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kCgsMax; ++i) {
+    if (i < nv) {
+      const double t = wave_sum(acc[i]);
+      if (lane == 0) s_red[wid * kCgsMax + i] = t;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int i = threadIdx.x;
+    part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] =
+        ((s_red[i] + s_red[kCgsMax + i]) + s_red[2 * kCgsMax + i]) + s_red[3 * kCgsMax + i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double* __restrict__ w,
+                                                         const double* __restrict__ Q, int64_t pitch, int nv,
+                                                         double* __restrict__ part) {
+  __shared__ double s_red[4 * kCgsMax];
+  double acc[kCgsMax];
+#pragma unroll
+  for (int i = 0; i < kCgsMax; ++i) acc[i] = 0.0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    const double we = w[e];
+    const double* qp = Q + e;  // walk the basis column: one VGPR address, no per-vector SGPR bases
+#pragma unroll
+    for (int i = 0; i < kCgsMax; ++i) {
+      if (i < nv) acc[i] += *qp * we;
+      qp += pitch;
+    }
+  }
+  store_partials(acc, nv, s_red, part);
+}
+
+template <int DOT>
+__global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* __restrict__ w,
+                                                            const double* __restrict__ Q, int64_t pitch, int nv,
+                                                            const double* __restrict__ coef,
+                                                            double* __restrict__ part) {
+  __shared__ double s_red[4 * kCgsMax];
+  __shared__ double s_c[kCgsMax];
+  if (threadIdx.x < nv) s_c[threadIdx.x] = coef[threadIdx.x];
+  __syncthreads();
+  double acc[DOT ? kCgsMax : 1];
+#pragma unroll
+  for (int i = 0; i < (DOT ? kCgsMax : 1); ++i) acc[i] = 0.0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    double t = w[e];
+    const double* qp = Q + e;
+    for (int i = 0; i < nv; ++i, qp += pitch) t -= s_c[i] * *qp;  // w' = w - Q c (basis order)
+    w[e] = t;
+    if (DOT) {  // q_i . w' : the column was just read, so these loads hit L1/L2
+      qp = Q + e;
+#pragma unroll
+      for (int i = 0; i < kCgsMax; ++i) {
+        if (i < nv) acc[i] += *qp * t;
+        qp += pitch;
+      }
+    } else {
+      acc[0] += t * t;
+    }
+  }
+  if (DOT) {
+    store_partials(acc, nv, s_red, part);
+  } else {
+    __shared__ double s_wave[4];
+    const double tot = block_sum(acc[0], s_wave);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+  }
+}
+
+// workgroup i reduces vector i's partials; add (nullable) + c -> h_out (host H column, nullable)
+__global__ __launch_bounds__(kBlock) void cgs_finalize_kernel(const double* __restrict__ part, int n_in,
+                                                              double* __restrict__ c, const double* __restrict__ add,
+                                                              double* __restrict__ h_out) {
+  __shared__ double s_wave[4];
+  const int i = blockIdx.x;
+  const double t = sum_partials(part + static_cast<int64_t>(i) * n_in, n_in, s_wave);
+  if (threadIdx.x == 0) {
+    c[i] = t;
+    if (h_out != nullptr) h_out[i] = add[i] + t;
+  }
+}
+
+hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
+                          hipStream_t s, const LaunchEv* ev) {
+  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
+  launch_k(cgs_dot_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
+                             bool dot, double* part, int grid, hipStream_t s) {
+  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
+  if (dot)
+    hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+  else
+    hipLaunchKernelGGL(cgs_update_kernel<0>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(cgs_finalize_kernel, dim3(nv), dim3(kBlock), 0, s, part, n_in, c, add, h_out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // K4: x = Z[:, :p] y + x0 (solvers.py:287).  For p <= kYArg the coefficients travel in the
 // kernel-argument segment (scalar loads, no H2D copy in front of the launch); otherwise they
 // are copied to LDS from a device buffer.  Each lane streams one (VEC: two) element(s) of every

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -115,6 +116,9 @@ struct spis_context {
   int prof_iter = 0;              // iteration counter for the sampling
   bool force_generic_gram = false;  // tests: take the MZ + tiled-Gram path
   bool fuse_spmv = true;            // residual SpMV of U_j + Arnoldi SpMV of A_{j+2} in one launch
+  bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
+  double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
+  double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   bool use_graphs = false;          // replay captured Arnoldi steps (opt-in: each replay's boundary
                                     // costs ~5 us of GPU time, more than the host launches it saves)
   std::vector<hipEvent_t> ev_free;
@@ -132,6 +136,7 @@ struct spis_context {
 
 struct spis_matrix {
   spis_context* ctx = nullptr;
+  uint64_t uid = 0;  // unique per upload (cache keys must not use the reusable object address)
   int64_t n_rows = 0, n_cols = 0, nnz = 0;
   int32_t* indptr = nullptr;
   int32_t* indices = nullptr;
@@ -185,11 +190,12 @@ struct spis_workspace {
   // replayed with one hipGraphLaunch; valid while graph_key matches
   std::vector<hipGraphExec_t> arn_graph;
   struct GraphKey {
-    const void* A = nullptr;
+    uint64_t A = 0;  // matrix upload id (an address can be reused by a later upload)
     const double* pinned_dev = nullptr;
     int gs = 0, gb = 0;
+    bool cgs2 = false;
     bool operator==(const GraphKey& o) const {
-      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb;
+      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb && cgs2 == o.cgs2;
     }
   } graph_key;
 };
@@ -396,6 +402,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->partR, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
+    HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
+    HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
     ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
     // pipeline events only order host reads of the coherent pinned slots: device-scope release
     // (a system-scope one writes back and invalidates L2 at every iteration, ~8 us each);
@@ -450,6 +458,8 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->partB);
     (void)hipFree(c->partR);
     (void)hipFree(c->dscal);
+    (void)hipFree(c->cgs_part);
+    (void)hipFree(c->cgs_c);
     if (c->gram_part) (void)hipFree(c->gram_part);
     if (c->gram_G) (void)hipFree(c->gram_G);
     if (c->gram_ptrs) (void)hipFree(c->gram_ptrs);
@@ -491,6 +501,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_FUSE_SPMV: c->fuse_spmv = value != 0; return SPIS_OK;
       case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
+      case SPIS_OPT_ORTHOG:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
+        c->cgs2 = value == 1;
+        return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }
   })
@@ -628,6 +642,8 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
     }
     HIP_TRY(hipSetDevice(c->device));
     std::unique_ptr<spis_matrix> M(new spis_matrix());
+    static std::atomic<uint64_t> next_uid{1};
+    M->uid = next_uid++;
     M->ctx = c;
     M->n_rows = n_rows;
     M->n_cols = n_cols;
@@ -1219,6 +1235,7 @@ struct Solver {
   // into host memory and carries that update's completion event (single GPU, fused path)
   int arnoldi_post(int j, const double* xpart = nullptr, double* x_out = nullptr,
                    unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr) {
+    if (c->cgs2 && j + 1 <= kCgsMax) return arnoldi_post_cgs2(j, xpart, x_out, flag, seq);
     hipStream_t s = c->stream;
     c->prof_iter = j;
     ST_TRY(allreduce(c, c->partA, gs));
@@ -1241,6 +1258,30 @@ struct Solver {
       n_in = gb;
     }
     HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, hcol + j + 1, s, gb, &e_last));
+    return SPIS_OK;
+  }
+
+  // opt-in CGS2 (SPIS_OPT_ORTHOG = 1): 3 reductions per step instead of j + 2 (kernels.hip K2c)
+  int arnoldi_post_cgs2(int j, const double* xpart, double* x_out, unsigned long long* flag,
+                        const unsigned long long* seq) {
+    hipStream_t s = c->stream;
+    c->prof_iter = j;
+    if (xpart) HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));  // U_{j-2}'s residual
+    const int nv = j + 1;
+    double* hcol = c->pinned_dev + hoff(j);
+    double* c1 = c->cgs_c;
+    double* c2 = c->cgs_c + kCgsMax;
+    ProfEv pm(c, SPIS_PROF_MGS);
+    const LaunchEv e_first = pm.first(), e_last = pm.last();
+    HIP_TRY(launch_cgs_dot(n, ws->w, Qv(0), ws->pitch, nv, c->cgs_part, gb, s, &e_first));
+    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gb));
+    HIP_TRY(launch_cgs_finalize(c->cgs_part, gb, nv, c1, nullptr, nullptr, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c1, true, c->cgs_part, gb, s));
+    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gb));
+    HIP_TRY(launch_cgs_finalize(c->cgs_part, gb, nv, c2, c1, hcol, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c2, false, c->partB, gb, s));
+    ST_TRY(allreduce(c, c->partB, gb));
+    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), c->partB, gb, hcol + j + 1, s, gb, &e_last));
     return SPIS_OK;
   }
 
@@ -1321,7 +1362,7 @@ struct Solver {
   // captured once per workspace and step index; every pointer in it is a workspace / context /
   // matrix pointer (graph_key), the per-call values (seq) are read from pinned memory
   int arn_graph(int ja, hipGraphExec_t* out) {
-    const spis_workspace::GraphKey key{A, c->pinned_dev, gs, gb};
+    const spis_workspace::GraphKey key{A->uid, c->pinned_dev, gs, gb, c->cgs2};
     if (!(ws->graph_key == key)) {
       drop_graphs(ws);
       ws->graph_key = key;

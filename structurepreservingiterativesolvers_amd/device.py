@@ -46,6 +46,28 @@ class Context:
             self.handle = None
 
 
+_OPTIONS = {
+    "fuse_spmv": (_lib.OPT_FUSE_SPMV, None),
+    "generic_gram": (_lib.OPT_GENERIC_GRAM, None),
+    "graphs": (_lib.OPT_GRAPHS, None),
+    "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
+}
+
+
+def set_option(name, value, ctx=None):
+    """Per-context solver options (``spis_set_option``, include/spis.h):
+
+    * ``fuse_spmv`` (True): true-residual and Arnoldi SpMVs in one launch (bit-identical);
+    * ``graphs`` (False): replay captured Arnoldi steps;
+    * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
+      low-synchronisation option (3 reductions per step; not MGS's rounding);
+    * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests)."""
+    ctx = ctx or get_context()
+    opt, names = _OPTIONS[name]
+    v = names[value] if names is not None else int(bool(value))
+    _lib.check(ctx.L.spis_set_option(ctx.handle, opt, v), "spis_set_option")
+
+
 def _release(ctx, fn_name, handle):
     """Finalizer: release a device object unless its context was already destroyed."""
     if ctx.handle:

@@ -278,6 +278,8 @@ def bench_main(args, metric):
     n_glob = A.shape[0]
     sysd = DistributedSystem(comm, A, swe_fields(M))
     ctx = comm.ctx
+    if getattr(args, "orthog", "mgs") == "cgs2":
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1), "spis_set_option")
     bd = sysd.vector(dic["b"])
     x0d = DeviceVector.from_host(np.zeros(sysd.n_local), ctx=ctx)
     conlist = [
@@ -343,6 +345,7 @@ def bench_main(args, metric):
                                ", mass+energy constraints")
                             + "; value = global iterations x (global DoF / 1,002,252) / s",
                 "config": "c5" if c5 else "c3",
+                "orthogonalisation": getattr(args, "orthog", "mgs"),
                 "global_dof": n_glob,
                 "k": args.k,
                 "parallelism": f"row partition x{P}, RCCL allreduce + halo send/recv",

@@ -249,15 +249,70 @@ def test_fused_dual_spmv_bit_identical(spis):
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, graphs), "spis_set_option")
             try:
                 x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
-            finally:
+            finally:  # back to the defaults
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 1), "spis_set_option")
-                _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1), "spis_set_option")
+                _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 0), "spis_set_option")
             runs.append((x, np.asarray(d["res"]), np.concatenate(d["x"].y), d["x"].basis(25), np.asarray(d["x"])))
         for r in runs[1:]:
             for a, bb in zip(runs[0], r):
                 assert np.array_equal(a, bb), case
         outs.append(case)
     assert outs == ["swe", "lkdv"]
+
+
+def test_graph_cache_not_stale_after_matrix_reupload(spis):
+    """SPIS_OPT_GRAPHS: captured Arnoldi steps are keyed on the matrix upload id, so a new matrix
+    (possibly at a freed matrix's address) never replays a graph holding the old one's pointers."""
+    import gc
+
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    def solve(dic, graphs):
+        set_option("graphs", graphs)
+        try:
+            x, d = solvers.cgmres(dic["A"], dic["b"], np.zeros_like(dic["b"]), 20, tol=1e-19,
+                                  conlist=swe_ls.constraints(dic, np.zeros_like(dic["b"])))
+            return x, np.asarray(d["res"])
+        finally:
+            set_option("graphs", False)
+
+    for seed in (0, 1, 2):  # same shape, different values; each freed before the next upload
+        dic, _ = sa.linforms(M=16, seed=seed)
+        xg, rg = solve(dic, True)
+        xe, re_ = solve(dic, False)
+        assert np.array_equal(xg, xe) and np.array_equal(rg, re_), seed
+        del dic
+        gc.collect()
+
+
+def test_cgs2_option_vs_oracle_and_orthogonality(spis):
+    """SPIS_OPT_ORTHOG = CGS2 (opt-in low-sync orthogonalisation): same iterates as the reference's
+    MGS to roundoff on swe (CGS2 is MGS-equivalent in exact arithmetic), a basis orthonormal to
+    1e-12, and the constrained step still holds the invariants."""
+    import oracle
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    x0 = np.zeros_like(dic["b"])
+    cons = swe_ls.constraints(dic, x0)
+    set_option("orthog", "cgs2")
+    try:
+        x, d = solvers.cgmres(dic["A"], dic["b"], x0, 25, tol=1e-19, conlist=cons)
+        Q = d["x"].basis(25)
+    finally:
+        set_option("orthog", "mgs")
+    xr, dr, trace, bad = _oracle_run(dic["A"], dic["b"], x0, 25, tol=1e-19, conlist=cons)
+    if _oracle_prefix_match(d["x"].trace, trace, np.asarray(d["x"]), np.asarray(dr["x"]), bad=bad):
+        np.testing.assert_allclose(x, xr, atol=1e-8 * np.linalg.norm(xr))
+    assert np.abs(Q @ Q.T - np.eye(25)).max() < 1e-12
+    assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-11 * max(1.0, abs(dic["m0"]))
+    assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-11 * max(1.0, abs(dic["e0"]))
 
 
 def test_lkdvrk_dict_form_through_callback(spis):
@@ -277,7 +332,6 @@ def test_lkdvrk_dict_form_through_callback(spis):
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("M,k,tol", [(40, 30, 1e-19), (40, 30, 1e-9)])
 def test_swe_vs_oracle_medium(spis, M, k, tol):
-    import oracle
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
 
@@ -285,21 +339,14 @@ def test_swe_vs_oracle_medium(spis, M, k, tol):
     x0 = np.zeros_like(dic["b"])
     x, d = swe_ls.cgmresWrapper(dic, x0=x0, k=k, tol=tol)
     cons = swe_ls.constraints(dic, x0)
-    trace = []
-    xr, dr = oracle.cgmres(dic["A"], dic["b"], x0, k, tol=tol, conlist=cons, trace=trace)
+    xr, dr, trace, bad = _oracle_run(dic["A"], dic["b"], x0, k, tol=tol, conlist=cons)
     # Where the reference's SLSQP cannot land the O(1e4)-magnitude energy constraint within
-    # ctol = 1e-12 absolute (solvers.py:267) it falls back; whether it does depends on the
-    # host BLAS (observed: not in the build container, yes on the GPU box's CPU).  Compare
-    # up to the first such reference-side fallback; our constrained steps must then hold.
-    if "fallback" in [t for _, t in trace]:
-        first = next(j for j, t in trace if t == "fallback")
-        assert d["x"].trace[:first] == trace[:first]
-        xs, xrs = np.asarray(d["x"]), np.asarray(dr["x"])
-        for i in range(1, first + 1):
-            assert np.linalg.norm(xs[i] - xrs[i]) <= 1e-8 * np.linalg.norm(xrs[i])
-    else:
+    # ctol = 1e-12 absolute (solvers.py:267) it falls back, and where it stops at its iteration
+    # limit its iterate is unconverged; both depend on the host BLAS (observed on the GPU box's
+    # CPU, not in the build container).  Compare up to the first such reference-side event; our
+    # constrained steps must then still hold the invariants.
+    if _oracle_prefix_match(d["x"].trace, trace, np.asarray(d["x"]), np.asarray(dr["x"]), bad=bad):
         assert d["steps"] == dr["steps"]
-        assert d["x"].trace == trace
         np.testing.assert_allclose(x, xr, atol=1e-8 * np.linalg.norm(xr))
     inv_m = dic["omega"] @ x - dic["m0"]
     inv_e = 0.5 * x @ dic["L"] @ x - dic["e0"]
@@ -338,12 +385,35 @@ def _envelope(A, b, x0, k, tol, cons, seeds=(11, 12)):
     return env
 
 
-def _oracle_prefix_match(trace_dev, trace_ref, xs, xrs, env=None):
-    """Compare a device run with the oracle up to the oracle's first SLSQP fallback (whether the
-    reference's SLSQP lands a large-magnitude constraint within ctol = 1e-12 depends on the host
-    BLAS, see test_swe_vs_oracle_medium); per-iterate tolerance max(1e-8, 10 x envelope) as in
+def _oracle_run(*args, **kw):
+    """oracle.cgmres with its SLSQP failure warnings recorded: returns (x, dict, trace, failed
+    iterations).  Where the reference's SLSQP stops unconverged ("Iteration limit reached", ...)
+    its constrained iterate is not the exact LS solution the device computes."""
+    import re
+
+    import oracle
+
+    trace = []
+    with warnings.catch_warnings(record=True) as wl:
+        warnings.simplefilter("always")
+        x, d = oracle.cgmres(*args, trace=trace, **kw)
+    bad = []
+    for w in wl:
+        m = re.search(r"Iteration (\d+) failed with message", str(w.message))
+        if m:
+            bad.append(int(m.group(1)))
+    return x, d, trace, bad
+
+
+def _oracle_prefix_match(trace_dev, trace_ref, xs, xrs, env=None, bad=()):
+    """Compare a device run with the oracle up to the oracle's first SLSQP fallback or failure
+    message (whether the reference's SLSQP lands a large-magnitude constraint within
+    ctol = 1e-12, or within its iteration limit, depends on the host BLAS, see
+    test_swe_vs_oracle_medium); per-iterate tolerance max(1e-8, 10 x envelope) as in
     test_golden; returns True when the whole runs were compared."""
     first = next((j for j, t in trace_ref if t == "fallback"), None)
+    if bad:
+        first = min(bad) if first is None else min(first, min(bad))
     upto = len(trace_ref) if first is None else first
     assert trace_dev[:upto] == trace_ref[:upto]
     for i in range(1, upto + 1):
@@ -372,10 +442,9 @@ def test_restarted_cgmres_vs_oracle_loop(spis):
     assert d["cycles"] == cycles and d["steps"] == k * cycles
     xr = x0
     for c in range(cycles):
-        trace = []
-        xr_next, dr = oracle.cgmres(dic["A"], dic["b"], xr, k, tol=1e-19, conlist=cons, trace=trace)
+        xr_next, dr, trace, bad = _oracle_run(dic["A"], dic["b"], xr, k, tol=1e-19, conlist=cons)
         run = d["runs"][c]
-        whole = _oracle_prefix_match(run["x"].trace, trace, np.asarray(run["x"]), np.asarray(dr["x"]))
+        whole = _oracle_prefix_match(run["x"].trace, trace, np.asarray(run["x"]), np.asarray(dr["x"]), bad=bad)
         if not whole:
             break  # later cycles start from different iterates
         np.testing.assert_allclose(run["res"], dr["res"], rtol=1e-8, atol=1e-12 * dr["res"][0])
@@ -395,13 +464,12 @@ def test_lkdvrk_gl3_vs_oracle_medium(spis):
     dic, prob = ra.linforms(M=400, tstages=3)
     x0 = np.zeros_like(dic["b"])
     x, d = rk_ls.cgmresWrapper(dic, x0, 30, prob=prob, tol=1e-19)
-    trace = []
     cons = rk_ls.constraints(dic, prob)
-    xr, dr = oracle.cgmres(dic["A"], dic["b"], x0, 30, tol=1e-19, conlist=cons, trace=trace)
+    xr, dr, trace, bad = _oracle_run(dic["A"], dic["b"], x0, 30, tol=1e-19, conlist=cons)
     # lkdvRK is roundoff-sensitive (the golden fixtures' envelope reaches 3.5e-3): the bound is
     # the reference's own envelope at this size, as in test_golden
     env = _envelope(dic["A"], dic["b"], x0, 30, 1e-19, cons)
-    if _oracle_prefix_match(d["x"].trace, trace, np.asarray(d["x"]), np.asarray(dr["x"]), env):
+    if _oracle_prefix_match(d["x"].trace, trace, np.asarray(d["x"]), np.asarray(dr["x"]), env, bad=bad):
         tol_f = max(1e-8, 10 * env[-1])
         np.testing.assert_allclose(x, xr, atol=tol_f * np.linalg.norm(xr))
 
