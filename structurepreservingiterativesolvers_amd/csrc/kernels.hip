@@ -435,42 +435,60 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 // 3 reductions per step instead of MGS's j+2 (one all-reduce each on several GPUs); not MGS's
 // arithmetic (the reference's, solvers.py:193-195), so it is never the default.
 // ---------------------------------------------------------------------------------------------
-// per-block partials of nv sums: waves reduce by butterfly, the 4 wave sums combine in order
-__device__ __forceinline__ void store_partials(const double* acc, int nv, double* s_red, double* part) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < kCgsMax; ++i) {
-    if (i < nv) {
-      const double t = wave_sum(acc[i]);
-      if (lane == 0) s_red[wid * kCgsMax + i] = t;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < nv) {
-    const int i = threadIdx.x;
-    part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] =
-        ((s_red[i] + s_red[kCgsMax + i]) + s_red[2 * kCgsMax + i]) + s_red[3 * kCgsMax + i];
-  }
-}
+// Basis vectors are split over the workgroup's 4 waves (vector i -> wave i % 4, 8 per wave), all
+// 4 waves walk the same 256-element chunks (lane: 2 x double2, i.e. 2 KB contiguous per vector and
+// chunk): 8 accumulators and 8 address streams per lane.  The scalar tail (odd n, unaligned
+// chunks) is handled element-wise by wave 0's lanes in the last chunk.
+constexpr int kCgsPerWave = kCgsMax / (kBlock / 64);
+constexpr int kCgsChunk = 256;
+
+__device__ __forceinline__ bool aligned16d(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 __global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double* __restrict__ w,
                                                          const double* __restrict__ Q, int64_t pitch, int nv,
                                                          double* __restrict__ part) {
-  __shared__ double s_red[4 * kCgsMax];
-  double acc[kCgsMax];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double acc[kCgsPerWave];
 #pragma unroll
-  for (int i = 0; i < kCgsMax; ++i) acc[i] = 0.0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
-    const double we = w[e];
-    const double* qp = Q + e;  // walk the basis column: one VGPR address, no per-vector SGPR bases
+  for (int m = 0; m < kCgsPerWave; ++m) acc[m] = 0.0;
+  const double* Qw = Q + wid * pitch;
+  const int64_t step = 4 * pitch;
+  const bool vec = aligned16d(w) && aligned16d(Q) && (pitch % 2 == 0);
+  const int64_t n_vec = vec ? (n / kCgsChunk) * kCgsChunk : 0;
+  for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kCgsChunk; e0 < n_vec;
+       e0 += static_cast<int64_t>(gridDim.x) * kCgsChunk) {
+    const int64_t e = e0 + 2 * lane;  // elements e, e+1 and e+128, e+129
+    const double2 wa = *reinterpret_cast<const double2*>(w + e);
+    const double2 wb = *reinterpret_cast<const double2*>(w + e + 128);
 #pragma unroll
-    for (int i = 0; i < kCgsMax; ++i) {
-      if (i < nv) acc[i] += *qp * we;
-      qp += pitch;
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      if (wid + 4 * m < nv) {
+        const double* qv = Qw + m * step;
+        const double2 qa = *reinterpret_cast<const double2*>(qv + e);
+        const double2 qb = *reinterpret_cast<const double2*>(qv + e + 128);
+        acc[m] += qa.x * wa.x;
+        acc[m] += qa.y * wa.y;
+        acc[m] += qb.x * wb.x;
+        acc[m] += qb.y * wb.y;
+      }
     }
   }
-  store_partials(acc, nv, s_red, part);
+  for (int64_t e = n_vec + static_cast<int64_t>(blockIdx.x) * 64 + lane; e < n;
+       e += static_cast<int64_t>(gridDim.x) * 64) {
+    const double we = w[e];
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m)
+      if (wid + 4 * m < nv) acc[m] += Qw[m * step + e] * we;
+  }
+#pragma unroll
+  for (int m = 0; m < kCgsPerWave; ++m) {
+    const int i = wid + 4 * m;
+    if (i < nv) {
+      const double t = wave_sum(acc[m]);
+      if (lane == 0) part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] = t;
+    }
+  }
 }
 
 template <int DOT>
@@ -478,34 +496,112 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
                                                             const double* __restrict__ Q, int64_t pitch, int nv,
                                                             const double* __restrict__ coef,
                                                             double* __restrict__ part) {
-  __shared__ double s_red[4 * kCgsMax];
   __shared__ double s_c[kCgsMax];
+  __shared__ double s_sum[4][4][64];  // [wave][element slot][lane]
+  __shared__ double s_wave[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x < nv) s_c[threadIdx.x] = coef[threadIdx.x];
   __syncthreads();
-  double acc[DOT ? kCgsMax : 1];
+  double acc[kCgsPerWave];
 #pragma unroll
-  for (int i = 0; i < (DOT ? kCgsMax : 1); ++i) acc[i] = 0.0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
-    double t = w[e];
-    const double* qp = Q + e;
-    for (int i = 0; i < nv; ++i, qp += pitch) t -= s_c[i] * *qp;  // w' = w - Q c (basis order)
-    w[e] = t;
-    if (DOT) {  // q_i . w' : the column was just read, so these loads hit L1/L2
-      qp = Q + e;
+  for (int m = 0; m < kCgsPerWave; ++m) acc[m] = 0.0;
+  const double* Qw = Q + wid * pitch;
+  const int64_t step = 4 * pitch;
+  const bool vec = aligned16d(w) && aligned16d(Q) && (pitch % 2 == 0);
+  const int64_t n_vec = vec ? (n / kCgsChunk) * kCgsChunk : 0;
+  // w' = w - Q c: each wave sums its vectors' share (basis order within the wave), the 4 shares
+  // combine in a fixed order through LDS (every wave gets the same w'); wave 0 stores it
+  for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kCgsChunk; e0 < n_vec;
+       e0 += static_cast<int64_t>(gridDim.x) * kCgsChunk) {
+    const int64_t e = e0 + 2 * lane;
+    double2 qa[kCgsPerWave], qb[kCgsPerWave];
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
-      for (int i = 0; i < kCgsMax; ++i) {
-        if (i < nv) acc[i] += *qp * t;
-        qp += pitch;
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      if (wid + 4 * m < nv) {
+        const double* qv = Qw + m * step;
+        qa[m] = *reinterpret_cast<const double2*>(qv + e);
+        qb[m] = *reinterpret_cast<const double2*>(qv + e + 128);
+        const double cm = s_c[wid + 4 * m];
+        p0 += cm * qa[m].x;
+        p1 += cm * qa[m].y;
+        p2 += cm * qb[m].x;
+        p3 += cm * qb[m].y;
+      } else {
+        qa[m] = make_double2(0.0, 0.0);
+        qb[m] = make_double2(0.0, 0.0);
       }
-    } else {
+    }
+    const double2 wa = *reinterpret_cast<const double2*>(w + e);
+    const double2 wb = *reinterpret_cast<const double2*>(w + e + 128);
+    s_sum[wid][0][lane] = p0;
+    s_sum[wid][1][lane] = p1;
+    s_sum[wid][2][lane] = p2;
+    s_sum[wid][3][lane] = p3;
+    __syncthreads();
+    double t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      t[k] = (((s_sum[0][k][lane] + s_sum[1][k][lane]) + s_sum[2][k][lane]) + s_sum[3][k][lane]);
+    t[0] = wa.x - t[0];
+    t[1] = wa.y - t[1];
+    t[2] = wb.x - t[2];
+    t[3] = wb.y - t[3];
+    if (wid == 0) {
+      *reinterpret_cast<double2*>(w + e) = make_double2(t[0], t[1]);
+      *reinterpret_cast<double2*>(w + e + 128) = make_double2(t[2], t[3]);
+    }
+    if (DOT) {
+#pragma unroll
+      for (int m = 0; m < kCgsPerWave; ++m) {
+        acc[m] += qa[m].x * t[0];
+        acc[m] += qa[m].y * t[1];
+        acc[m] += qb[m].x * t[2];
+        acc[m] += qb[m].y * t[3];
+      }
+    } else if (wid == 0) {
+      acc[0] += t[0] * t[0];
+      acc[0] += t[1] * t[1];
+      acc[0] += t[2] * t[2];
+      acc[0] += t[3] * t[3];
+    }
+    __syncthreads();
+  }
+  // scalar tail (odd / unaligned n): the same 4-wave structure, one element per lane
+  for (int64_t e0 = n_vec + static_cast<int64_t>(blockIdx.x) * 64; e0 < n; e0 += static_cast<int64_t>(gridDim.x) * 64) {
+    const int64_t e = e0 + lane;
+    const bool ok = e < n;
+    double q[kCgsPerWave];
+    double ps = 0.0;
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      q[m] = (ok && wid + 4 * m < nv) ? Qw[m * step + e] : 0.0;
+      if (wid + 4 * m < nv) ps += s_c[wid + 4 * m] * q[m];
+    }
+    const double we = ok ? w[e] : 0.0;
+    s_sum[wid][0][lane] = ps;
+    __syncthreads();
+    const double t = we - (((s_sum[0][0][lane] + s_sum[1][0][lane]) + s_sum[2][0][lane]) + s_sum[3][0][lane]);
+    if (wid == 0 && ok) w[e] = t;
+    if (DOT) {
+#pragma unroll
+      for (int m = 0; m < kCgsPerWave; ++m) acc[m] += q[m] * t;
+    } else if (wid == 0) {
       acc[0] += t * t;
     }
+    __syncthreads();
   }
   if (DOT) {
-    store_partials(acc, nv, s_red, part);
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nv) {
+        const double t = wave_sum(acc[m]);
+        if (lane == 0) part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] = t;
+      }
+    }
   } else {
-    __shared__ double s_wave[4];
     const double tot = block_sum(acc[0], s_wave);
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
   }

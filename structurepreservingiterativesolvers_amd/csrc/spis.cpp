@@ -1271,17 +1271,20 @@ struct Solver {
     double* hcol = c->pinned_dev + hoff(j);
     double* c1 = c->cgs_c;
     double* c2 = c->cgs_c + kCgsMax;
+    // 64-element chunks per workgroup iteration: up to kRedGrid workgroups (the partial slots);
+    // fixed on several GPUs so every rank's partial arrays have the same length
+    const int gc = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 63) / 64)));
     ProfEv pm(c, SPIS_PROF_MGS);
     const LaunchEv e_first = pm.first(), e_last = pm.last();
-    HIP_TRY(launch_cgs_dot(n, ws->w, Qv(0), ws->pitch, nv, c->cgs_part, gb, s, &e_first));
-    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gb));
-    HIP_TRY(launch_cgs_finalize(c->cgs_part, gb, nv, c1, nullptr, nullptr, s));
-    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c1, true, c->cgs_part, gb, s));
-    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gb));
-    HIP_TRY(launch_cgs_finalize(c->cgs_part, gb, nv, c2, c1, hcol, s));
-    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c2, false, c->partB, gb, s));
-    ST_TRY(allreduce(c, c->partB, gb));
-    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), c->partB, gb, hcol + j + 1, s, gb, &e_last));
+    HIP_TRY(launch_cgs_dot(n, ws->w, Qv(0), ws->pitch, nv, c->cgs_part, gc, s, &e_first));
+    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gc));
+    HIP_TRY(launch_cgs_finalize(c->cgs_part, gc, nv, c1, nullptr, nullptr, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c1, true, c->cgs_part, gc, s));
+    ST_TRY(allreduce(c, c->cgs_part, static_cast<int64_t>(nv) * gc));
+    HIP_TRY(launch_cgs_finalize(c->cgs_part, gc, nv, c2, c1, hcol, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, c2, false, c->partB, gc, s));
+    ST_TRY(allreduce(c, c->partB, gc));
+    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), c->partB, gc, hcol + j + 1, s, gb, &e_last));
     return SPIS_OK;
   }
 
