@@ -124,8 +124,16 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  * SPIS_OPT_ORTHOG (default 0): 0 = modified Gram-Schmidt (the reference's, solvers.py:193-195);
  *   1 = CGS2, classical Gram-Schmidt with one re-orthogonalisation pass (3 reductions per
  *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
- *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only. */
-enum spis_option { SPIS_OPT_FUSE_SPMV = 1, SPIS_OPT_GENERIC_GRAM = 2, SPIS_OPT_GRAPHS = 3, SPIS_OPT_ORTHOG = 4 };
+ *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only.
+ * SPIS_OPT_ELL_GRAM (default 1): the fused constraint reduction (p + 1 <= 32) reads a sliced-ELL
+ *   copy of each constraint matrix, built once on first use (static row boundaries). */
+enum spis_option {
+  SPIS_OPT_FUSE_SPMV = 1,
+  SPIS_OPT_GENERIC_GRAM = 2,
+  SPIS_OPT_GRAPHS = 3,
+  SPIS_OPT_ORTHOG = 4,
+  SPIS_OPT_ELL_GRAM = 5
+};
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 
 /* ---- multi-GPU (RCCL over xGMI) ----------------------------------------------

@@ -98,8 +98,18 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 // G = [U^T M U | U^T v_0 .. U^T v_{nvv-1}] from Ut (M may be null: linear terms only);
 // partials: constraint_gram_partials() x (np1*np1 + nvv*np1) doubles
 int constraint_gram_partials();
+// Sliced ELL of a constraint matrix for K7: 16-row slices, slice c holds W_c = (off[c+1] -
+// off[c]) / 16 columns of entries, entry (row 16c + r, t) at off[c] + 16 t + r (zero padding).
+struct EllView {
+  const int32_t* col;
+  const double* val;
+  const int64_t* off;
+};
+constexpr int kEllRows = 16;
+
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
-                                  const double* const* v, double* partials, double* G, hipStream_t s);
+                                  const double* const* v, double* partials, double* G, hipStream_t s,
+                                  const EllView* ell = nullptr);
 // partial dot / sum of squares
 hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_out, int grid,
                       hipStream_t s);

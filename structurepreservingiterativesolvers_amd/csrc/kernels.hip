@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kern
   const int grp = blockIdx.x % ngrp;
   const int64_t wpg = static_cast<int64_t>(gridDim.x / ngrp) * NW;  // waves per group
   const int64_t gw = static_cast<int64_t>(blockIdx.x / ngrp) * NW + wid;
-  const int64_t rpg = (n + ngrp - 1) / ngrp;
+  const int64_t rpg = ((n + ngrp - 1) / ngrp + kConRows - 1) / kConRows * kConRows;  // whole slices
   const int64_t g0 = grp * rpg;
   const int64_t g1 = g0 + rpg < n ? g0 + rpg : n;
   const int64_t nch = g1 > g0 ? (g1 - g0 + kConRows - 1) / kConRows : 0;
@@ -1219,6 +1219,137 @@ __global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kern
   }
 }
 
+// K7 on a sliced-ELL copy of M (p + 1 <= 32): row boundaries are static, so each lane half keeps 8
+// rows' w in registers (row 2r + h), gather addresses come straight from per-lane ELL loads, and
+// the slice's t loop has no control flow: independent gathers in flight.  Same chunk / XCD-group
+// schedule, W tile and rank-16 update as constraint_gram_kernel.
+__global__ __launch_bounds__(kBlock, 3) void constraint_gram_ell_kernel(
+    int64_t n, int np1, const int32_t* __restrict__ ecol, const double* __restrict__ eval,
+    const int64_t* __restrict__ eoff, const double* __restrict__ Ut, int nvv, const double* __restrict__ v0,
+    const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ v3,
+    double* __restrict__ partials) {
+  constexpr int NP = 32, SEG = 16, NW = kBlock / 64;
+  constexpr int kWin = 16 * kConRows;  // ELL entries staged per wave and window (16 slice columns)
+  __shared__ __attribute__((aligned(16))) double s_w[NW][kConRows][NP];
+  __shared__ double s_acc[64 * (SEG + 4)];
+  __shared__ int s_ecol[NW][kWin];
+  __shared__ double s_eval[NW][kWin];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int la = lane % NP;
+  const int h = lane / NP;
+  const bool on = la < np1;
+  const int lac = on ? la : 0;
+  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int grp = blockIdx.x % ngrp;
+  const int64_t wpg = static_cast<int64_t>(gridDim.x / ngrp) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x / ngrp) * NW + wid;
+  const int64_t rpg = ((n + ngrp - 1) / ngrp + kConRows - 1) / kConRows * kConRows;
+  const int64_t g0 = grp * rpg;
+  const int64_t g1 = g0 + rpg < n ? g0 + rpg : n;
+  const int64_t nch = g1 > g0 ? (g1 - g0 + kConRows - 1) / kConRows : 0;
+  const bool has_m = ecol != nullptr;
+  double acc[SEG];
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  double (*W)[NP] = s_w[wid];
+  for (int64_t ch = gw; ch < nch; ch += wpg) {
+    const int64_t r0 = g0 + ch * kConRows;
+    const int nr = static_cast<int>(g1 - r0 < kConRows ? g1 - r0 : kConRows);
+    const int64_t cg = r0 / kConRows;  // global slice index (g0 is a multiple of 16)
+    double u[kConRows];
+#pragma unroll
+    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * np1 + lac];
+    double vc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (lane < nr) {
+      if (nvv > 0) vc[0] = v0[r0 + lane];
+      if (nvv > 1) vc[1] = v1[r0 + lane];
+      if (nvv > 2) vc[2] = v2[r0 + lane];
+      if (nvv > 3) vc[3] = v3[r0 + lane];
+    }
+    if (has_m) {
+      const int64_t e0 = eoff[cg];
+      const int width = static_cast<int>((eoff[cg + 1] - e0) / kConRows);
+      double wr[kConRows / 2];
+#pragma unroll
+      for (int r = 0; r < kConRows / 2; ++r) wr[r] = 0.0;
+      int* sc = s_ecol[wid];
+      double* sv = s_eval[wid];
+      for (int t0 = 0; t0 < width; t0 += 16) {  // windows of 16 slice columns
+        const int nt = width - t0 < 16 ? width - t0 : 16;
+        const int ne = nt * kConRows;
+        // stage the window's (col, val): contiguous in HBM, coalesced, one round trip
+#pragma unroll
+        for (int q = 0; q < kWin / 64; ++q) {
+          const int e = q * 64 + lane;
+          const int64_t src = e0 + static_cast<int64_t>(t0) * kConRows + (e < ne ? e : 0);
+          sc[e] = ecol[src];
+          sv[e] = eval[src];
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 2
+        for (int t = 0; t < nt; ++t) {
+          double g[kConRows / 2];
+#pragma unroll
+          for (int r = 0; r < kConRows / 2; ++r)
+            g[r] = Ut[static_cast<int64_t>(sc[t * kConRows + 2 * r + h]) * np1 + lac];
+#pragma unroll
+          for (int r = 0; r < kConRows / 2; ++r) wr[r] += sv[t * kConRows + 2 * r + h] * g[r];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int r = 0; r < kConRows / 2; ++r) W[2 * r + h][la] = on ? wr[r] : 0.0;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < kConRows; ++i) {  // rank-16 update, this lane's segment of G's row
+        const double ui = (on && i < nr) ? u[i] : 0.0;
+        const double2* wrow = reinterpret_cast<const double2*>(&W[i][SEG * h]);
+#pragma unroll
+        for (int j = 0; j < SEG; j += 2) {
+          const double2 x2 = wrow[j >> 1];
+          acc[j] += ui * x2.x;
+          acc[j + 1] += ui * x2.y;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (h == 0) {
+#pragma unroll
+      for (int i = 0; i < kConRows; ++i) {
+        const double ui = (on && i < nr) ? u[i] : 0.0;
+        if (nvv > 0) gv[0] += ui * readlane_f64(vc[0], i);
+        if (nvv > 1) gv[1] += ui * readlane_f64(vc[1], i);
+        if (nvv > 2) gv[2] += ui * readlane_f64(vc[2], i);
+        if (nvv > 3) gv[3] += ui * readlane_f64(vc[3], i);
+      }
+    }
+  }
+  for (int w = 0; w < NW; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) s_acc[lane * (SEG + 4) + j] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + j]) + acc[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        s_acc[lane * (SEG + 4) + SEG + c] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + SEG + c]) + gv[c];
+    }
+    __syncthreads();
+  }
+  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
+  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
+  for (int idx = threadIdx.x; idx < stride; idx += kBlock) {
+    if (idx < np1 * np1) {
+      const int a = idx / np1, b = idx - (idx / np1) * np1;
+      out[idx] = has_m ? s_acc[(a + NP * (b / SEG)) * (SEG + 4) + (b % SEG)] : 0.0;
+    } else {
+      const int k2 = idx - np1 * np1;
+      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
+      out[idx] = s_acc[a * (SEG + 4) + SEG + c];
+    }
+  }
+}
+
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   double* Ut, hipStream_t s) {
   const int np1 = p + 1;
@@ -1232,7 +1363,8 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 int constraint_gram_partials() { return kConGramGrid; }
 
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
-                                  const double* const* v, double* partials, double* G, hipStream_t s) {
+                                  const double* const* v, double* partials, double* G, hipStream_t s,
+                                  const EllView* ell) {
   if (np1 > 64 || nvv > 4 || (M == nullptr && nvv == 0)) return hipErrorInvalidValue;
   const int32_t* rp = M ? M->indptr : nullptr;
   const int32_t* ci = M ? M->indices : nullptr;
@@ -1242,7 +1374,10 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
   // one resident wave-set (256 CUs x blocks per CU at the kernel's occupancy): every group's
   // waves sweep their row range together; a multiple of 8 and <= constraint_gram_partials()
   const int grid = np1 <= 32 ? 256 * 3 : 256 * 2;
-  if (np1 <= 32)
+  if (np1 <= 32 && ell != nullptr)
+    hipLaunchKernelGGL(constraint_gram_ell_kernel, dim3(grid), dim3(kBlock), 0, s, n, np1, ell->col, ell->val,
+                       ell->off, Ut, nvv, vv[0], vv[1], vv[2], vv[3], partials);
+  else if (np1 <= 32)
     hipLaunchKernelGGL(constraint_gram_kernel<32>, dim3(grid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
                        nvv, vv[0], vv[1], vv[2], vv[3], partials);
   else

@@ -119,6 +119,7 @@ struct spis_context {
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
+  bool ell_gram = true;             // K7 on the sliced-ELL copy (SPIS_OPT_ELL_GRAM)
   bool use_graphs = false;          // replay captured Arnoldi steps (opt-in: each replay's boundary
                                     // costs ~5 us of GPU time, more than the host launches it saves)
   std::vector<hipEvent_t> ev_free;
@@ -145,6 +146,10 @@ struct spis_matrix {
   int32_t n_blk = 0, n_long = 0;
   int32_t* blk_row_d = nullptr;  // row blocks of <= kDualCap nnz / items for the fused dual SpMV
   int32_t n_blk_d = 0;
+  // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
+  int32_t* ell_col = nullptr;
+  double* ell_val = nullptr;
+  int64_t* ell_off = nullptr;
   bool all_zero = false;
   // halo plan
   int32_t n_ghost = 0;
@@ -501,6 +506,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_FUSE_SPMV: c->fuse_spmv = value != 0; return SPIS_OK;
       case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
+      case SPIS_OPT_ELL_GRAM: c->ell_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
@@ -709,6 +715,9 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->vals);
     (void)hipFree(M->blk_row);
     (void)hipFree(M->blk_row_d);
+    if (M->ell_col) (void)hipFree(M->ell_col);
+    if (M->ell_val) (void)hipFree(M->ell_val);
+    if (M->ell_off) (void)hipFree(M->ell_off);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
     delete M;
@@ -895,6 +904,59 @@ extern "C" int spis_gram(spis_context* c, int64_t n, int32_t nu, const double* c
 // ------------------------------------------------------------------------------------------------
 // fused path (single GPU, p + 1 <= 64, <= 4 linear terms): transpose [Z, x0] once, then one
 // wave-per-row pass per constraint matrix (K7) — no M Z columns are materialised
+// One-time sliced-ELL copy of a constraint matrix (kEllRows-row slices, each padded to its longest
+// row with zero entries whose column is the row itself): the CSR comes back to the host once.
+static int ensure_ell(spis_context* c, spis_matrix* M, EllView* out) {
+  if (!M->ell_col) {
+    const int64_t n = M->n_rows, nnz = M->nnz;
+    std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
+    std::vector<double> va(std::max<int64_t>(nnz, 1));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+    if (nnz > 0) {
+      HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+    }
+    const int64_t nch = (n + kEllRows - 1) / kEllRows;
+    std::vector<int64_t> off(nch + 1, 0);
+    for (int64_t ch = 0; ch < nch; ++ch) {
+      int64_t width = 0;
+      for (int64_t r = ch * kEllRows; r < std::min<int64_t>(n, (ch + 1) * kEllRows); ++r)
+        width = std::max<int64_t>(width, rp[r + 1] - rp[r]);
+      off[ch + 1] = off[ch] + kEllRows * width;
+    }
+    const int64_t tot = std::max<int64_t>(off[nch], 1);
+    std::vector<int32_t> ecol(tot, 0);
+    std::vector<double> eval(tot, 0.0);
+    for (int64_t ch = 0; ch < nch; ++ch) {
+      const int64_t width = (off[ch + 1] - off[ch]) / kEllRows;
+      for (int rr = 0; rr < kEllRows; ++rr) {
+        const int64_t r = ch * kEllRows + rr;
+        const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
+        for (int64_t t = 0; t < width; ++t) {
+          const int64_t e = off[ch] + t * kEllRows + rr;
+          if (t < len) {
+            ecol[e] = ci[rp[r] + t];
+            eval[e] = va[rp[r] + t];
+          } else {
+            ecol[e] = static_cast<int32_t>(r < n ? r : 0);
+          }
+        }
+      }
+    }
+    HIP_TRY(hipMalloc(&M->ell_col, sizeof(int32_t) * tot));
+    HIP_TRY(hipMalloc(&M->ell_val, sizeof(double) * tot));
+    HIP_TRY(hipMalloc(&M->ell_off, sizeof(int64_t) * (nch + 1)));
+    HIP_TRY(hipMemcpy(M->ell_col, ecol.data(), sizeof(int32_t) * tot, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->ell_val, eval.data(), sizeof(double) * tot, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(M->ell_off, off.data(), sizeof(int64_t) * (nch + 1), hipMemcpyHostToDevice));
+  }
+  out->col = M->ell_col;
+  out->val = M->ell_val;
+  out->off = M->ell_off;
+  return SPIS_OK;
+}
+
 static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
                                   int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   QuadCon* out) {
@@ -934,7 +996,11 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
     if (mzero) continue;
     const CsrView mv = cons[ci].M->view();
     const int nvv = v_done ? 0 : static_cast<int>(vlist.size());
-    HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
+    EllView ev{};
+    const bool use_ell = np1 <= 32 && c->ell_gram;
+    if (use_ell) ST_TRY(ensure_ell(c, cons[ci].M, &ev));
+    HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream,
+                                   use_ell ? &ev : nullptr));
     const int cnt = np1 * np1 + nvv * np1;
     HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

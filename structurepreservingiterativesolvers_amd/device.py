@@ -51,6 +51,7 @@ _OPTIONS = {
     "generic_gram": (_lib.OPT_GENERIC_GRAM, None),
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
+    "ell_gram": (_lib.OPT_ELL_GRAM, None),
 }
 
 
@@ -61,7 +62,8 @@ def set_option(name, value, ctx=None):
     * ``graphs`` (False): replay captured Arnoldi steps;
     * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
       low-synchronisation option (3 reductions per step; not MGS's rounding);
-    * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests)."""
+    * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
+    * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix."""
     ctx = ctx or get_context()
     opt, names = _OPTIONS[name]
     v = names[value] if names is not None else int(bool(value))

@@ -204,10 +204,10 @@ def test_golden(spis, name, caplog):
 
 
 def test_fused_and_generic_constraint_reduction_agree(spis):
-    """The fused transpose + wave-per-row kernel (K7) and the generic M Z + tiled Gram path
-    (K5 + K6) give the same constrained solve."""
+    """The fused constraint reduction (K7, on the sliced-ELL copy and on the CSR) and the generic
+    M Z + tiled Gram path (K5 + K6) give the same constrained solve."""
     from structurepreservingiterativesolvers_amd import _lib
-    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.device import get_context, set_option
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
 
@@ -220,8 +220,14 @@ def test_fused_and_generic_constraint_reduction_agree(spis):
         xg, dg = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
     finally:
         _lib.check(ctx.L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
-    assert df["x"].trace == dg["x"].trace
+    set_option("ell_gram", False)  # K7 on the CSR (row-boundary walk) instead of the sliced ELL
+    try:
+        xc, dc = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
+    finally:
+        set_option("ell_gram", True)
+    assert df["x"].trace == dg["x"].trace == dc["x"].trace
     np.testing.assert_allclose(xf, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
+    np.testing.assert_allclose(xc, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
 
 
 def test_fused_dual_spmv_bit_identical(spis):
