@@ -185,6 +185,22 @@ class IterateList(collections.abc.Sequence):
 
             self._fin = __import__("weakref").finalize(self, _release, ctx, "spis_workspace_release", C.c_void_p(ws))
 
+    _BRANCH = {_lib.BRANCH_UNCON: "uncon", _lib.BRANCH_CON: "con", _lib.BRANCH_FALLBACK: "fallback"}
+
+    def _set_meta(self, branch, events, ys, k, n_iter):
+        self._branch, self.events, self._ys, self._k, self._n_iter = branch, events, ys, k, n_iter
+
+    @property
+    def trace(self):
+        """Branch per LS step: [(j, "uncon" | "con" | "fallback")] (tests, diagnostics)."""
+        return [(j, self._BRANCH[int(self._branch[j])]) for j in range(self._n_iter)]
+
+    @property
+    def y(self):
+        """The LS solution of every step (y_j has j + 1 entries)."""
+        k = self._k
+        return [self._ys[j * k: j * k + j + 1].copy() for j in range(self._n_iter)]
+
     def __len__(self):
         return self._count
 
@@ -395,10 +411,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     n_iter = out.n_res - 1
     final = xf if device_io else xf.numpy()
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
-    names = {_lib.BRANCH_UNCON: "uncon", _lib.BRANCH_CON: "con", _lib.BRANCH_FALLBACK: "fallback"}
-    xs.trace = [(j, names[int(br[j])]) for j in range(n_iter)]  # branch per LS step (tests, diagnostics)
-    xs.events = ev[: max(n_iter, out.steps)].copy()
-    xs.y = [ys[j * k: j * k + j + 1].copy() for j in range(n_iter)]
+    xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)
     xs.stamps = stamps  # host clock: per-iteration / constraint-step stamps, [4k] call start, [4k+1] end
     return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
                 stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)
@@ -406,6 +419,8 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
 
 def _replay_warnings(r, method, timing):
     """Re-emit, in iteration order, the warnings the reference raises."""
+    if not r["events"].any():
+        return
     n_it = max(r["n_iter"], r["steps"])
     for j in range(min(n_it, len(r["events"]))):
         e = int(r["events"][j])
