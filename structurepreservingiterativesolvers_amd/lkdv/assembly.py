@@ -152,8 +152,30 @@ def linforms(N=100, M=50, degree=1, T=1, space="DG", zinit=None):
         "mo0": float(0.5 * u0 @ Mass @ u0),
         "e0": float(0.5 * w0 @ Mass @ w0 - 0.5 * u0 @ Mass @ u0),
         "T": T,
+        "_step": {"Mass": Mass, "G": G, "dt": dt, "nf": nf},  # for step_forms
     }
     return out, prob
+
+
+def step_forms(dic, zinit):
+    """``linforms(..., zinit=z)`` for the next time step (``lkdv/Evolve.py:41``) without
+    rebuilding the operators: ``A``, ``M``, ``L``, ``omega`` are the same objects (so they stay
+    resident in HBM), ``b``, ``z0`` and the invariant targets are recomputed from ``z``."""
+    st = dic["_step"]
+    Mass, G, dt, nf = st["Mass"], st["G"], st["dt"], st["nf"]
+    z = np.asarray(zinit, dtype=np.float64)
+    u0, w0 = z[:nf].copy(), z[2 * nf:].copy()
+    n = 3 * nf
+    b = np.zeros(n)
+    b[:nf] = Mass @ u0 / dt
+    b[nf:2 * nf] = 0.5 * (Mass @ u0) + 0.5 * (G @ w0)
+    z_vec = np.zeros(n)
+    z_vec[:nf] = u0
+    z_vec[2 * nf:] = w0
+    out = dict(dic)
+    out.update(b=b, z0=z_vec, m0=float(dic["omega"][:nf] @ u0), mo0=float(0.5 * u0 @ Mass @ u0),
+               e0=float(0.5 * w0 @ Mass @ w0 - 0.5 * u0 @ Mass @ u0))
+    return out
 
 
 def compute_invariants(prob, dic, uvec):

@@ -34,18 +34,22 @@ def _lift(dic, prob):
     bw = np.asarray(prob.butcher_tableau.b, dtype=np.float64)
     z0 = np.asarray(dic["z0"], dtype=np.float64)
     M, L, omega = dic["M"], dic["L"], np.asarray(dic["omega"], dtype=np.float64)
-    K = L - M
+    K = derived([L, M], ["L-M"], lambda: L - M)
     PtP = np.outer(dt * bw, dt * bw)
 
     def Pt(w):
         return np.kron(dt * bw, w)
 
     n = len(bw) * len(z0)
-    mass = _Constraint(sps.csr_matrix((n, n)), Pt(omega), float(omega @ z0 - dic["m0"]))
-    mom = _Constraint(sps.csr_matrix(sps.kron(PtP, M)), Pt(0.5 * (M @ z0 + M.T @ z0)),
-                      float(0.5 * z0 @ (M @ z0) - dic["mo0"]))
-    en = _Constraint(sps.csr_matrix(sps.kron(PtP, K)), Pt(0.5 * (K @ z0 + K.T @ z0)),
-                     float(0.5 * z0 @ (K @ z0) - dic["e0"]))
+    # the lifted matrices depend on the operators and the tableau only: built once per problem
+    # (time steps share them, so they stay resident in HBM with their sliced-ELL copies)
+    key = ["lift", float(dt)] + [float(v) for v in bw]
+    zero = derived([M], key + ["zero"], lambda: sps.csr_matrix((n, n)))
+    MM = derived([M], key + ["M"], lambda: sps.csr_matrix(sps.kron(PtP, M)))
+    KK = derived([L, M], key + ["K"], lambda: sps.csr_matrix(sps.kron(PtP, K)))
+    mass = _Constraint(zero, Pt(omega), float(omega @ z0 - dic["m0"]))
+    mom = _Constraint(MM, Pt(0.5 * (M @ z0 + M.T @ z0)), float(0.5 * z0 @ (M @ z0) - dic["mo0"]))
+    en = _Constraint(KK, Pt(0.5 * (K @ z0 + K.T @ z0)), float(0.5 * z0 @ (K @ z0) - dic["e0"]))
     return [mass, mom, en]
 
 

@@ -130,8 +130,22 @@ def linforms(N=100, M=50, degree=1, tstages=2, T=10, t=0.0, zinit=None):
         "e0": float(0.5 * (w0 @ Mass @ w0 - u0 @ Mass @ u0)),
         "T": T,
         "z0": z0,
+        "_step": {"K": K, "Mass": Mass, "s": s, "nf": nf},  # for step_forms
     }
     return out, prob
+
+
+def step_forms(dic, zinit):
+    """``linforms(..., zinit=z)`` for the next time step (``lkdvRK/Evolve.py:55-58``) without
+    rebuilding the stage operator (``A``, ``M``, ``L``, ``omega`` stay the same objects)."""
+    st = dic["_step"]
+    K, Mass, s, nf = st["K"], st["Mass"], st["s"], st["nf"]
+    z0 = np.asarray(zinit, dtype=np.float64).copy()
+    u0, w0 = z0[:nf], z0[2 * nf:]
+    out = dict(dic)
+    out.update(b=-np.tile(K @ z0, s), z0=z0, m0=float(dic["omega"][:nf] @ u0), mo0=float(0.5 * u0 @ Mass @ u0),
+               e0=float(0.5 * (w0 @ Mass @ w0 - u0 @ Mass @ u0)))
+    return out
 
 
 def z1calc(prob, zbig, z0):

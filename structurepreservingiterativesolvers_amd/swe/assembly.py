@@ -149,8 +149,18 @@ def linforms(N=100, M=50, degree=1, T=10, zinit=None, seed=0):
         "e0": float(0.5 * z0 @ L @ z0),
         "z0": z0,
         "T": T,
+        "_step": {"B": Bop},  # for step_forms
     }
     return out, prob
+
+
+def step_forms(dic, zinit):
+    """``linforms(..., zinit=z)`` for the next time step (``swe/Evolve.py:40``) without
+    rebuilding the operators (``A``, ``L``, ``omega`` are the same objects, resident in HBM)."""
+    z0 = np.asarray(zinit, dtype=np.float64).copy()
+    out = dict(dic)
+    out.update(b=dic["_step"]["B"] @ z0, z0=z0, m0=float(dic["omega"] @ z0), e0=float(0.5 * z0 @ dic["L"] @ z0))
+    return out
 
 
 def extra_constraint(n, z_ref, seed=2):
