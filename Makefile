@@ -8,7 +8,7 @@ SRC      := $(PKG)/csrc
 LIB      := $(PKG)/libspis.so
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I include -I $(SRC)
 HIPFLAGS := --offload-arch=$(ARCH) -munsafe-fp-atomics
-OBJS     := build/kernels.o build/spis.o build/lsq.o
+OBJS     := build/kernels.o build/sptrsv.o build/spis.o build/lsq.o build/ilu_plan.o
 
 all: $(LIB) $(PKG)/liblsq_host.so
 
@@ -16,9 +16,17 @@ build/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -c $< -o $@
 
-build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/lsq.h include/spis.h
+build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/sptrsv.h $(SRC)/ilu_plan.h $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -x hip --offload-arch=$(ARCH) -c $< -o $@
+
+build/sptrsv.o: $(SRC)/sptrsv.hip $(SRC)/sptrsv.h $(SRC)/ilu_plan.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -c $< -o $@
+
+build/ilu_plan.o: $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h
+	@mkdir -p build
+	g++ $(CXXFLAGS) -c $< -o $@
 
 build/lsq.o: $(SRC)/lsq.cpp $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
@@ -28,8 +36,8 @@ $(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
 # host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
-$(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp
-	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp
+$(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp
+	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp
 
 clean:
 	rm -rf build $(LIB) $(PKG)/liblsq_host.so

@@ -82,6 +82,7 @@ enum spis_ls_message {
 typedef struct spis_context spis_context;
 typedef struct spis_matrix spis_matrix;
 typedef struct spis_workspace spis_workspace;
+typedef struct spis_ilu spis_ilu;
 
 /* ---- library / context ---------------------------------------------------- */
 int spis_abi_version(void);
@@ -167,6 +168,24 @@ int spis_matrix_destroy(spis_matrix* A);
  * info[5]=n_ghost info[6]=all values zero (1/0) */
 int spis_matrix_info(spis_matrix* A, int64_t info[8]);
 
+/* ---- device ILU preconditioner (pre.solve of a SuperLU spilu object) -------- */
+/* Replaces the host call pre.solve(vec) of solvers.py:152-154 (used at :190) for
+ * pre = scipy.sparse.linalg.spilu(A, ...) (swe/TimedSolve.py:23, lkdvRK/Evolve.py:51,
+ * lkdvRK/SingleSolve.py:19).  Takes SuperLU's factors Pr A Pc = L U as scipy exposes them
+ * (pre.L, pre.U as CSR with sorted columns, pre.perm_r, pre.perm_c) and applies
+ *   z = Pc U^{-1} L^{-1} Pr q   (y[perm_r[i]] = q[i]; L y' = y; U v = y'; z[i] = v[perm_c[i]])
+ * on the device.  L must be unit lower triangular (a stored diagonal must be 1), U upper
+ * triangular with a non-zero diagonal.  Single GPU.  The factorisation itself stays with SuperLU
+ * on the host (once per operator, as in the reference). */
+int spis_ilu_create(spis_context* ctx, int64_t n, const int32_t* l_rowptr, const int32_t* l_col,
+                    const double* l_val, const int32_t* u_rowptr, const int32_t* u_col, const double* u_val,
+                    const int32_t* perm_r, const int32_t* perm_c, spis_ilu** out);
+/* z = P^{-1} q (device pointers, must not alias); synchronises the context stream */
+int spis_ilu_apply(spis_ilu* ilu, const double* q_dev, double* z_dev);
+/* info: levels(L), levels(U), blocks(L), blocks(U), steps(L), steps(U), nnz(L strict), nnz(U strict) */
+int spis_ilu_info(spis_ilu* ilu, int64_t info[8]);
+int spis_ilu_destroy(spis_ilu* ilu);
+
 /* ---- vectors / BLAS-1 primitives (device pointers, n = local length) -------- */
 /* spis_malloc: zero-filled block, ordered on the context stream (no host wait); blocks come from
  * a per-context stream-ordered cache.  spis_free returns a block to that cache (it must come
@@ -230,6 +249,7 @@ typedef struct spis_solve_opts {
   void* pre_user;
   spis_conls_fn conls_fn;    /* dict-form constraints                              */
   void* conls_user;
+  spis_ilu* pre_ilu;         /* device ILU apply of pre.solve (spilu), single GPU  */
 } spis_solve_opts;
 
 typedef struct spis_solve_out {

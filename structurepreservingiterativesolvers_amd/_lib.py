@@ -80,6 +80,7 @@ class SolveOpts(C.Structure):
         ("pre_user", C.c_void_p),
         ("conls_fn", CONLS_FN),
         ("conls_user", C.c_void_p),
+        ("pre_ilu", C.c_void_p),
     ]
 
 
@@ -118,6 +119,10 @@ SIGNATURES = [
     ("spis_csr_upload", C.c_int, [_VP, _I64, _I64, _I64, _PI32, _PI32, _PD, C.POINTER(HaloDesc), C.POINTER(_VP)]),
     ("spis_matrix_destroy", C.c_int, [_VP]),
     ("spis_matrix_info", C.c_int, [_VP, _PI64]),
+    ("spis_ilu_create", C.c_int, [_VP, _I64, _PI32, _PI32, _PD, _PI32, _PI32, _PD, _PI32, _PI32, C.POINTER(_VP)]),
+    ("spis_ilu_apply", C.c_int, [_VP, _VP, _VP]),
+    ("spis_ilu_info", C.c_int, [_VP, _PI64]),
+    ("spis_ilu_destroy", C.c_int, [_VP]),
     ("spis_malloc", C.c_int, [_VP, _I64, C.POINTER(_VP)]),
     ("spis_free", C.c_int, [_VP, _VP]),
     ("spis_memcpy_h2d", C.c_int, [_VP, _VP, _VP, _I64]),

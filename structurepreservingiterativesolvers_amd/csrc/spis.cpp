@@ -25,8 +25,10 @@
 #include <unordered_map>
 #include <vector>
 
+#include "ilu_plan.h"
 #include "kernels.h"
 #include "lsq.h"
+#include "sptrsv.h"
 #include "spis.h"
 
 using namespace spis;
@@ -725,6 +727,137 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
   })
 }
 
+// ------------------------------------------------------------------------------------------------
+// device ILU preconditioner (K8, sptrsv.h): the plan is built on the host once per factorisation
+// (levels, solve order, blocks), uploaded, and every apply is two memsets + one launch
+// ------------------------------------------------------------------------------------------------
+struct DevTri {
+  std::vector<void*> bufs;
+  TriDev view{};
+};
+
+struct spis_ilu {
+  spis_context* ctx = nullptr;
+  int64_t n = 0;
+  DevTri L, U;
+  double* gran = nullptr;        // [2n] granules: y then v
+  unsigned* ticket = nullptr;
+  unsigned* err_host = nullptr;  // pinned, device-mapped: a bounded spin gave up
+  unsigned* err_dev = nullptr;
+  int64_t stats[8] = {0};
+};
+
+template <typename T>
+static int upload_vec(DevTri& d, const std::vector<T>& v, const T** out) {
+  *out = nullptr;
+  if (v.empty()) return SPIS_OK;
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, sizeof(T) * v.size()));
+  d.bufs.push_back(p);
+  HIP_TRY(hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+  *out = static_cast<const T*>(p);
+  return SPIS_OK;
+}
+
+static int upload_tri(DevTri& d, const TriPlan& P) {
+  ST_TRY(upload_vec(d, P.rowptr, &d.view.rowptr));
+  ST_TRY(upload_vec(d, P.col, &d.view.col));
+  ST_TRY(upload_vec(d, P.val, &d.view.val));
+  ST_TRY(upload_vec(d, P.diag, &d.view.diag));
+  ST_TRY(upload_vec(d, P.in_idx, &d.view.in_idx));
+  ST_TRY(upload_vec(d, P.out_idx, &d.view.out_idx));
+  ST_TRY(upload_vec(d, P.blk_row, &d.view.blk_row));
+  ST_TRY(upload_vec(d, P.blk_step, &d.view.blk_step));
+  ST_TRY(upload_vec(d, P.step_row, &d.view.step_row));
+  ST_TRY(upload_vec(d, P.step_long, &d.view.step_long));
+  ST_TRY(upload_vec(d, P.blk_ent, &d.view.blk_ent));
+  ST_TRY(upload_vec(d, P.blk_long, &d.view.blk_long));
+  d.view.nb = P.n_blocks();
+  return SPIS_OK;
+}
+
+static void free_ilu(spis_ilu* P) {
+  for (void* b : P->L.bufs) (void)hipFree(b);
+  for (void* b : P->U.bufs) (void)hipFree(b);
+  if (P->gran) (void)hipFree(P->gran);
+  if (P->ticket) (void)hipFree(P->ticket);
+  if (P->err_host) (void)hipHostFree(P->err_host);
+  delete P;
+}
+
+static int ilu_enqueue(spis_ilu* P, const double* q, double* z, hipStream_t s) {
+  HIP_TRY(launch_ilu_apply(P->n, P->L.view, P->U.view, q, P->gran, z, P->ticket, P->err_dev, s));
+  return SPIS_OK;
+}
+
+static int ilu_check(spis_ilu* P) {  // after a synchronisation of the stream the applies ran on
+  if (*reinterpret_cast<volatile unsigned*>(P->err_host) != 0) {
+    *P->err_host = 0;
+    return fail(SPIS_ERR_STATE, "device ILU apply: a triangular-solve wait timed out (values set to NaN)");
+  }
+  return SPIS_OK;
+}
+
+extern "C" int spis_ilu_create(spis_context* c, int64_t n, const int32_t* l_rowptr, const int32_t* l_col,
+                               const double* l_val, const int32_t* u_rowptr, const int32_t* u_col,
+                               const double* u_val, const int32_t* perm_r, const int32_t* perm_c,
+                               spis_ilu** out) {
+  ABI_GUARD({
+    if (!c || !out || !l_rowptr || !u_rowptr || !perm_r || !perm_c) return fail(SPIS_ERR_ARG, "null argument");
+    if (n < 0 || n >= (int64_t(1) << 30)) return fail(SPIS_ERR_ARG, "n out of range");
+    if ((l_rowptr[n] > 0 && (!l_col || !l_val)) || (u_rowptr[n] > 0 && (!u_col || !u_val)))
+      return fail(SPIS_ERR_ARG, "null factor arrays");
+    TriPlan L, U;
+    std::string err;
+    if (!build_ilu_plans(n, l_rowptr, l_col, l_val, u_rowptr, u_col, u_val, perm_r, perm_c, &L, &U, &err))
+      return fail(SPIS_ERR_ARG, "ILU factors: %s", err.c_str());
+    HIP_TRY(hipSetDevice(c->device));
+    std::unique_ptr<spis_ilu, void (*)(spis_ilu*)> P(new spis_ilu(), free_ilu);
+    P->ctx = c;
+    P->n = n;
+    ST_TRY(upload_tri(P->L, L));
+    ST_TRY(upload_tri(P->U, U));
+    HIP_TRY(hipMalloc(&P->gran, sizeof(double) * std::max<int64_t>(2 * n, 2)));
+    HIP_TRY(hipMalloc(&P->ticket, 16));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&P->err_host), 16, hipHostMallocMapped));
+    *P->err_host = 0;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&P->err_dev), P->err_host, 0));
+    const int64_t st[8] = {L.levels, U.levels, L.n_blocks(), U.n_blocks(),
+                           static_cast<int64_t>(L.step_row.size()) - 1, static_cast<int64_t>(U.step_row.size()) - 1,
+                           static_cast<int64_t>(L.col.size()), static_cast<int64_t>(U.col.size())};
+    std::copy(st, st + 8, P->stats);
+    *out = P.release();
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_ilu_apply(spis_ilu* P, const double* q_dev, double* z_dev) {
+  ABI_GUARD({
+    if (!P || (P->n > 0 && (!q_dev || !z_dev))) return fail(SPIS_ERR_ARG, "null argument");
+    if (q_dev == z_dev && P->n > 0) return fail(SPIS_ERR_ARG, "q and z must not alias");
+    HIP_TRY(hipSetDevice(P->ctx->device));
+    ST_TRY(ilu_enqueue(P, q_dev, z_dev, P->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(P->ctx->stream));
+    return ilu_check(P);
+  })
+}
+
+extern "C" int spis_ilu_info(spis_ilu* P, int64_t info[8]) {
+  if (!P || !info) return fail(SPIS_ERR_ARG, "null argument");
+  std::copy(P->stats, P->stats + 8, info);
+  return SPIS_OK;
+}
+
+extern "C" int spis_ilu_destroy(spis_ilu* P) {
+  ABI_GUARD({
+    if (!P) return SPIS_OK;
+    (void)hipSetDevice(P->ctx->device);
+    (void)hipStreamSynchronize(P->ctx->stream);
+    free_ilu(P);
+    return SPIS_OK;
+  })
+}
+
 extern "C" int spis_matrix_info(spis_matrix* M, int64_t info[8]) {
   if (!M || !info) return fail(SPIS_ERR_ARG, "null argument");
   info[0] = M->n_rows;
@@ -1285,6 +1418,8 @@ struct Solver {
     double* zj = Zv(j);
     if (o->pre_matrix) {
       ST_TRY(spmv_local(c, ws, o->pre_matrix, Qv(j), zj));
+    } else if (o->pre_ilu) {
+      ST_TRY(ilu_enqueue(o->pre_ilu, Qv(j), zj, s));
     } else if (o->pre_fn) {
       hostq.resize(n);
       hostz.resize(n);
@@ -1426,7 +1561,7 @@ struct Solver {
     return arnoldi_post(ja, c->partR, c->pinned_dev + roff(j), flag_dev(), seq_dev(j));
   }
 
-  bool graphable() const { return c->use_graphs && !c->comm && !o->pre_fn && !o->pre_matrix; }
+  bool graphable() const { return c->use_graphs && !c->comm && !o->pre_fn && !o->pre_matrix && !o->pre_ilu; }
 
   // captured once per workspace and step index; every pointer in it is a workspace / context /
   // matrix pointer (graph_key), the per-call values (seq) are read from pinned memory
@@ -1513,11 +1648,15 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       return fail(SPIS_ERR_ARG, "output arrays missing");
     const int64_t n = A->n_rows;
     if (o->pre_matrix && o->pre_matrix->n_rows != n) return fail(SPIS_ERR_ARG, "preconditioner size mismatch");
+    if (o->pre_ilu && o->pre_ilu->n != n) return fail(SPIS_ERR_ARG, "ILU preconditioner size mismatch");
+    if (o->pre_ilu && c->comm) return fail(SPIS_ERR_ARG, "the device ILU preconditioner is single-GPU");
+    if (o->pre_ilu && o->pre_ilu->ctx != c) return fail(SPIS_ERR_ARG, "ILU preconditioner of another context");
+    if (!!o->pre_matrix + !!o->pre_ilu + !!o->pre_fn > 1) return fail(SPIS_ERR_ARG, "more than one preconditioner");
     for (int i = 0; i < (o->conls_fn ? 0 : o->n_constraints); ++i)
       if (o->constraints[i].M && o->constraints[i].M->n_rows != n)
         return fail(SPIS_ERR_ARG, "constraint %d matrix size mismatch", i);
     HIP_TRY(hipSetDevice(c->device));
-    const bool sep_z = o->pre_matrix != nullptr || o->pre_fn != nullptr;
+    const bool sep_z = o->pre_matrix != nullptr || o->pre_fn != nullptr || o->pre_ilu != nullptr;
     spis_workspace* ws = nullptr;
     ST_TRY(get_workspace(c, n, n + A->n_ghost, k, sep_z, &ws));
     std::unique_ptr<spis_workspace, int (*)(spis_workspace*)> guard(ws, spis_workspace_release);
@@ -1719,6 +1858,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
     HIP_TRY(hipStreamSynchronize(s));  // speculative Arnoldi steps finish before x / ws are used
     prof_drain(c);
+    if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
     if (stamps) {
       stamps[4 * k] = t_start;
       stamps[4 * k + 1] = now_s();

@@ -34,6 +34,7 @@ class Context:
         self.device = int(device)
         self.nranks = 1
         self.rank = 0
+        self.device_ilu = "auto"  # SuperLU preconditioners on the device (K8) where the plan predicts a win
 
     def synchronize(self):
         _lib.check(self.L.spis_context_synchronize(self.handle), "spis_context_synchronize")
@@ -63,8 +64,18 @@ def set_option(name, value, ctx=None):
     * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
       low-synchronisation option (3 reductions per step; not MGS's rounding);
     * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
-    * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix."""
+    * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix;
+    * ``device_ilu`` ("auto"): how a SuperLU ``pre`` (``spilu``/``splu``) is applied — True on
+      the device (K8), False by its host ``pre.solve`` through the callback (as the reference
+      does), "auto" on the device when the plan's cost model predicts it is faster
+      (``DeviceILU.predicted_ms``: shallow level structures; deep dependency chains stay on the
+      host, where a sequential sweep is faster than any level-by-level GPU schedule)."""
     ctx = ctx or get_context()
+    if name == "device_ilu":
+        if value not in (True, False, "auto"):
+            raise ValueError("device_ilu must be True, False or 'auto'")
+        ctx.device_ilu = value
+        return
     opt, names = _OPTIONS[name]
     v = names[value] if names is not None else int(bool(value))
     _lib.check(ctx.L.spis_set_option(ctx.handle, opt, v), "spis_set_option")
@@ -227,6 +238,103 @@ def device_matrix(A, ctx=None) -> DeviceMatrix:
     except TypeError:  # not weak-referenceable: keep until invalidate()
         pass
     return dm
+
+
+class DeviceILU:
+    """Device apply of a SuperLU (incomplete) LU factorisation ``Pr A Pc = L U``: the
+    ``pre.solve(vec)`` of ``solvers.py:152-154`` for ``pre = spilu(A, ...)``
+    (``swe/TimedSolve.py:23``, ``lkdvRK/Evolve.py:51``) as two sync-free level-blocked triangular
+    solves in one launch (K8, ``spis_ilu_*``).  The factorisation stays SuperLU's, on the host."""
+
+    def __init__(self, ctx: Context, lu):
+        self.ctx = ctx
+        n = int(lu.shape[0])
+        self.n = n
+        Lf = _as_csr(lu.L.tocsr())
+        Uf = _as_csr(lu.U.tocsr())
+        Lf.sort_indices()
+        Uf.sort_indices()
+        pr = np.ascontiguousarray(lu.perm_r, dtype=np.int32)
+        pc = np.ascontiguousarray(lu.perm_c, dtype=np.int32)
+        h = C.c_void_p()
+        _lib.check(
+            ctx.L.spis_ilu_create(
+                ctx.handle, n, Lf.indptr.ctypes.data_as(_I32_P), Lf.indices.ctypes.data_as(_I32_P),
+                Lf.data.ctypes.data_as(_DOUBLE_P), Uf.indptr.ctypes.data_as(_I32_P),
+                Uf.indices.ctypes.data_as(_I32_P), Uf.data.ctypes.data_as(_DOUBLE_P),
+                pr.ctypes.data_as(_I32_P), pc.ctypes.data_as(_I32_P), C.byref(h)),
+            "spis_ilu_create")
+        self.handle = h
+        self._fin = weakref.finalize(self, _release, ctx, "spis_ilu_destroy", h)
+        info = (C.c_int64 * 8)()
+        _lib.check(ctx.L.spis_ilu_info(h, info), "spis_ilu_info")
+        self.info = {k: int(v) for k, v in zip(
+            ("levels_L", "levels_U", "blocks_L", "blocks_U", "steps_L", "steps_U", "nnz_L", "nnz_U"), info)}
+
+    # cost model fitted on MI355X (tools/ilu_sweep.py, DESIGN.md §K8): the device apply pays ~1.3 us
+    # per dependency level plus ~0.32 ns per factor entry; SuperLU's host solve ~2 ns per entry,
+    # plus, inside a solve, the callback's two PCIe copies of n doubles and a stream sync
+    DEV_US_PER_LEVEL, DEV_NS_PER_NNZ, DEV_US_FIXED = 1.3, 0.32, 20.0
+    HOST_NS_PER_NNZ, HOST_US_FIXED, PCIE_GBS = 2.0, 40.0, 25.0
+
+    def predicted_ms(self):
+        """(device, host) predicted milliseconds per apply."""
+        i = self.info
+        nnz = i["nnz_L"] + i["nnz_U"] + 2 * self.n
+        dev = (self.DEV_US_PER_LEVEL * (i["levels_L"] + i["levels_U"]) + self.DEV_NS_PER_NNZ * 1e-3 * nnz
+               + self.DEV_US_FIXED) * 1e-3
+        host = (self.HOST_NS_PER_NNZ * 1e-3 * nnz + self.HOST_US_FIXED
+                + 16.0 * self.n / (self.PCIE_GBS * 1e3)) * 1e-3
+        return dev, host
+
+    def apply(self, q: DeviceVector, z: DeviceVector):
+        _lib.check(self.ctx.L.spis_ilu_apply(self.handle, C.c_void_p(q.ptr), C.c_void_p(z.ptr)), "spis_ilu_apply")
+        return z
+
+    def solve(self, b):
+        """Host arrays in and out, like ``SuperLU.solve`` (a test/diagnostic convenience)."""
+        q = DeviceVector.from_host(np.asarray(b, dtype=np.float64).reshape(-1), ctx=self.ctx)
+        z = DeviceVector(self.ctx, self.n)
+        return self.apply(q, z).numpy()
+
+
+def is_superlu(pre):
+    return all(hasattr(pre, a) for a in ("L", "U", "perm_r", "perm_c", "solve", "shape"))
+
+
+_ILU_CACHE: dict = {}
+_ILU_CACHE_MAX = 4
+
+
+def choose_ilu(pre, ctx) -> "DeviceILU | None":
+    """The device apply to use for SuperLU object ``pre`` under the context's ``device_ilu``
+    option, or None for the host callback."""
+    mode = ctx.device_ilu
+    if mode is False:
+        return None
+    d = device_ilu(pre, ctx)
+    if mode is True:
+        return d
+    dev, host = d.predicted_ms()
+    return d if dev < host else None
+
+
+def device_ilu(pre, ctx=None) -> DeviceILU:
+    """Device copy of SuperLU object ``pre`` (cached; SuperLU objects take no weak references, so
+    the cache holds ``pre`` itself — its id cannot be reused while cached — and keeps the last
+    few)."""
+    if isinstance(pre, DeviceILU):
+        return pre
+    ctx = ctx or get_context()
+    key = (id(pre), ctx.device)
+    hit = _ILU_CACHE.get(key)
+    if hit is not None and hit[0] is pre:
+        return hit[1]
+    d = DeviceILU(ctx, pre)
+    while len(_ILU_CACHE) >= _ILU_CACHE_MAX:
+        _ILU_CACHE.pop(next(iter(_ILU_CACHE)))
+    _ILU_CACHE[key] = (pre, d)
+    return d
 
 
 def invalidate(A=None):

@@ -40,7 +40,7 @@ import scipy.optimize as spo
 import scipy.sparse as sps
 
 from . import _lib
-from .device import DeviceMatrix, DeviceVector, device_matrix, device_vector, get_context
+from .device import DeviceMatrix, DeviceVector, choose_ilu, device_matrix, device_vector, get_context, is_superlu
 
 log = logging.getLogger("structurepreservingiterativesolvers_amd")
 
@@ -240,13 +240,22 @@ class IterateList(collections.abc.Sequence):
 # preconditioners (solvers.py:149-161)
 # ------------------------------------------------------------------------------------------------
 def _precond_setup(pre, n, ctx, keep):
-    """Returns (pre_matrix handle or None, PRECOND_FN or null)."""
+    """Returns (pre_matrix handle or None, PRECOND_FN or null, pre_ilu handle or None).
+
+    A SuperLU object (``spilu``/``splu``) is applied on the device (K8) as the context's
+    ``device_ilu`` option decides (single GPU); other objects with ``.solve``, non-sparse ``@``
+    operators and host-chosen SuperLU objects go through the host callback (``solvers.py:152-161``)."""
     if pre is None:
-        return None, _lib.PRECOND_FN()
+        return None, _lib.PRECOND_FN(), None
     if sps.issparse(pre) and not hasattr(pre, "solve"):
         dm = device_matrix(pre, ctx=ctx)
         keep.append(dm)
-        return dm.handle.value, _lib.PRECOND_FN()
+        return dm.handle.value, _lib.PRECOND_FN(), None
+    if is_superlu(pre) and ctx.nranks == 1 and tuple(pre.shape) == (n, n):
+        di = choose_ilu(pre, ctx)
+        if di is not None:
+            keep.append(di)
+            return None, _lib.PRECOND_FN(), di.handle.value
     if hasattr(pre, "solve"):
         apply = pre.solve
     else:
@@ -272,7 +281,7 @@ def _precond_setup(pre, n, ctx, keep):
     fn = _lib.PRECOND_FN(cb)
     keep.append(fn)
     keep.append(err)
-    return None, fn
+    return None, fn, None
 
 
 # ------------------------------------------------------------------------------------------------
@@ -366,7 +375,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     if k < 1:
         raise ValueError("k must be >= 1")
     keep = []
-    pre_mat, pre_fn = _precond_setup(pre, n, ctx, keep)
+    pre_mat, pre_fn, pre_ilu = _precond_setup(pre, n, ctx, keep)
     conlist = list(conlist)
     descs = None
     conls = _lib.CONLS_FN()
@@ -385,7 +394,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
             conls = _make_conls(conlist, x0_host, n, timing, method, ctx, keep)
     opts = _lib.SolveOpts(
         method=method, k=k, tol=float(tol), contol=float(contol), timing=1 if timing else 0,
-        n_constraints=len(conlist), constraints=descs, pre_matrix=pre_mat, pre_fn=pre_fn, pre_user=None,
+        n_constraints=len(conlist), constraints=descs, pre_matrix=pre_mat, pre_fn=pre_fn, pre_user=None, pre_ilu=pre_ilu,
         conls_fn=conls, conls_user=None,
     )
     res = np.zeros(k + 1)
