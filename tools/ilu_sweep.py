@@ -3,8 +3,11 @@
 SPIS_ILU_SLEEP (read once per process) select launch parameters for sweeps; prints one JSON
 line per case."""
 import json
+import os
 import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import numpy as np
 import scipy.sparse.linalg as spsla
