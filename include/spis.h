@@ -127,13 +127,18 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
  *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only.
  * SPIS_OPT_ELL_GRAM (default 1): the fused constraint reduction (p + 1 <= 32) reads a sliced-ELL
- *   copy of each constraint matrix, built once on first use (static row boundaries). */
+ *   copy of each constraint matrix, built once on first use (static row boundaries).
+ * SPIS_OPT_MGS_CHAIN (default 1): each Arnoldi step's MGS chain + normalise runs as one persistent
+ *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^23); 0 = one
+ *   launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
+ *   so results differ from the per-step launches at roundoff level. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
   SPIS_OPT_GRAPHS = 3,
   SPIS_OPT_ORTHOG = 4,
-  SPIS_OPT_ELL_GRAM = 5
+  SPIS_OPT_ELL_GRAM = 5,
+  SPIS_OPT_MGS_CHAIN = 6
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

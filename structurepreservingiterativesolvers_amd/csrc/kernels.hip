@@ -381,6 +381,191 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 }
 
 // ---------------------------------------------------------------------------------------------
+// K2p: persistent MGS chain (kernels.h).  Workgroup g owns pairs [g*256*PER, (g+1)*256*PER); thread
+// t holds pairs t + 256 k.  Per step i (h_i known everywhere):
+//   y -= h_i q_i ; part = q_{i+1}.y (or y.y at the last step) — MGS's arithmetic, contraction off
+//   block_sum -> the workgroup's partial -> two granules {tag, lo32} {tag, hi32}, slot parity i&1
+//   wave 0 sweeps all partials' granules until every tag matches, sums them in a fixed order
+//   (identical in every workgroup) -> h_{i+1}; q_{i+2} loads are in flight meanwhile
+// Tags are base + i + 1 with base read from a device counter the previous chain advanced, so no
+// per-call reset is needed and a replayed graph stays valid.  A slot parity is rewritten two steps
+// later, after every workgroup has read it (it cannot publish step i+2 before step i+1's exchange
+// completed).  Spins are bounded (0.5 s of s_memrealtime): a missing workgroup sets *err, the
+// launch drains, and the host reports the failure.
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long chain_gu64;
+constexpr unsigned long long kChainWaitTicks = 50000000ull;  // 0.5 s at 100 MHz
+
+__device__ __forceinline__ void chain_store(unsigned long long* p, unsigned tag, unsigned half) {
+  __hip_atomic_store((chain_gu64*)p, (static_cast<unsigned long long>(tag) << 32) | half, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long chain_load(const unsigned long long* p) {
+  return __hip_atomic_load((chain_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int PER>
+__global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
+    int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
+    const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
+    unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
+    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq) {
+#pragma clang fp contract(off)
+  __shared__ double s_wave[4];
+  __shared__ double s_h;
+  __shared__ int s_fail;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x;
+  const int64_t npair = n >> 1;
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBlock * PER + tid;
+  double2 y[PER], U[PER], D[PER], P[PER];
+  auto load = [&](double2 (&r)[PER], const double* v) {
+    const double2* v2 = reinterpret_cast<const double2*>(v);
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (p0 + k * kBlock < npair) r[k] = v2[p0 + k * kBlock];
+  };
+  const unsigned base = *epoch;
+  load(y, w);
+  load(U, Q);
+  if (j >= 1) load(D, Q + pitch);
+  const bool tail = (n & 1) && blockIdx.x == 0 && tid == 0;  // odd element: workgroup 0, lane 0
+  double yt = 0.0, ut = 0.0, dt = 0.0, pt = 0.0;
+  if (tail) {
+    yt = w[n - 1];
+    ut = Q[n - 1];
+    if (j >= 1) dt = Q[pitch + n - 1];
+  }
+  if (tid == 0) s_fail = 0;
+  double h = sum_partials(part_in, n_in, s_wave);
+  if (blockIdx.x == 0 && tid == 0) hcol[0] = h;
+  if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
+    const double t = sum_partials(xpart, n_x, s_wave);
+    if (tid == 0) publish(x_out, t, flag, seq);
+  }
+  for (int i = 0; i <= j; ++i) {
+    const bool last = i == j;
+    double part = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (p0 + k * kBlock < npair) {
+        const double a0 = h * U[k].x, a1 = h * U[k].y;
+        y[k].x = y[k].x - a0;
+        y[k].y = y[k].y - a1;
+        if (!last) {
+          part += D[k].x * y[k].x;
+          part += D[k].y * y[k].y;
+        } else {
+          part += y[k].x * y[k].x;
+          part += y[k].y * y[k].y;
+        }
+      }
+    }
+    if (tail) {
+      const double a = h * ut;
+      yt = yt - a;
+      part += last ? yt * yt : dt * yt;
+    }
+    if (i + 2 <= j) {  // q_{i+2}: in flight behind the exchange
+      load(P, Q + static_cast<int64_t>(i + 2) * pitch);
+      if (tail) pt = Q[static_cast<int64_t>(i + 2) * pitch + n - 1];
+    }
+    const double tot = block_sum(part, s_wave);
+    const unsigned tag = base + static_cast<unsigned>(i) + 1u;
+    unsigned long long* slots = gran + static_cast<size_t>(i & 1) * 2 * kChainMaxWG;
+    if (tid == 0) {
+      const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(tot));
+      chain_store(slots + 2 * blockIdx.x, tag, static_cast<unsigned>(bits));
+      chain_store(slots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bits >> 32));
+    }
+    if (tid < 64) {  // wave 0: gather every workgroup's partial (granule 2g = lo, 2g + 1 = hi)
+      unsigned long long g[8];
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok = false;
+      for (unsigned spins = 0;; ++spins) {
+        ok = true;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int idx = tid + 64 * k;
+          g[k] = idx < 2 * G ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
+          ok &= static_cast<unsigned>(g[k] >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+      }
+      const bool all_ok = __all(ok);
+      // fixed order: lane pairs (2m, 2m+1) of round k hold partial (64 k + 2 m) / 2; sum k-major
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const unsigned lo = static_cast<unsigned>(g[k]);
+        const unsigned hi = static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
+        const double v = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+        if ((tid & 1) == 0 && tid + 64 * k < 2 * G) acc += v;
+      }
+      acc = wave_sum(acc);
+      if (tid == 0) {
+        s_h = acc;
+        if (!all_ok) {
+          s_fail = 1;
+          atomicOr(err, 1u);
+        }
+      }
+    }
+    __syncthreads();
+    const double hn = s_h;
+    if (s_fail) break;  // uniform: a workgroup never arrived; the host reports it
+    if (!last) {
+      h = hn;
+      if (blockIdx.x == 0 && tid == 0) hcol[i + 1] = hn;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        U[k] = D[k];
+        D[k] = P[k];
+      }
+      ut = dt;
+      dt = pt;
+    } else {  // K3: h_{j+1,j} = ||y||, q_{j+1} = y / h (zeros on breakdown, as normalize_kernel)
+      const double hh = sqrt(hn);
+      if (blockIdx.x == 0 && tid == 0) hcol[j + 1] = hh;
+      double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (p0 + k * kBlock < npair)
+          q2[p0 + k * kBlock] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+      if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
+}
+
+hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
+                            int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
+                            hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
+                            unsigned long long* flag, const unsigned long long* seq) {
+  const int64_t npair = n >> 1;
+  if (npair > kChainMaxPairs || !aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
+  const int per = npair <= int64_t(kChainMaxWG) * kBlock * 2   ? 2
+                  : npair <= int64_t(kChainMaxWG) * kBlock * 4 ? 4
+                  : npair <= int64_t(kChainMaxWG) * kBlock * 8 ? 8
+                                                               : 16;
+  const int64_t span = int64_t(kBlock) * per;
+  const int G = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
+#define SPIS_CHAIN(PER_)                                                                                   \
+  launch_k(mgs_chain_kernel<PER_>, dim3(G), dim3(kBlock), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, hcol, \
+           gran, epoch, err, xpart, n_x, x_out, flag, seq)
+  switch (per) {
+    case 2: SPIS_CHAIN(2); break;
+    case 4: SPIS_CHAIN(4); break;
+    case 8: SPIS_CHAIN(8); break;
+    default: SPIS_CHAIN(16); break;
+  }
+#undef SPIS_CHAIN
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // K3: h_{j+1,j} = ||y|| = sqrt(y.y) (numpy's norm), q_{j+1} = y / h (true division, :198).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const double* __restrict__ y,

@@ -122,6 +122,11 @@ struct spis_context {
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   bool ell_gram = true;             // K7 on the sliced-ELL copy (SPIS_OPT_ELL_GRAM)
+  bool mgs_chain = true;            // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN)
+  unsigned long long* chain_gran = nullptr;  // 2 parities x kChainMaxWG x 2 granules
+  unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
+  unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
+  unsigned* chain_err_dev = nullptr;
   bool use_graphs = false;          // replay captured Arnoldi steps (opt-in: each replay's boundary
                                     // costs ~5 us of GPU time, more than the host launches it saves)
   std::vector<hipEvent_t> ev_free;
@@ -201,8 +206,10 @@ struct spis_workspace {
     const double* pinned_dev = nullptr;
     int gs = 0, gb = 0;
     bool cgs2 = false;
+    bool chain = false;
     bool operator==(const GraphKey& o) const {
-      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb && cgs2 == o.cgs2;
+      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb && cgs2 == o.cgs2 &&
+             chain == o.chain;
     }
   } graph_key;
 };
@@ -411,6 +418,13 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
+    HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * 4 * kChainMaxWG));
+    HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * 4 * kChainMaxWG));
+    HIP_TRY(hipMalloc(&c->chain_epoch, 16));
+    HIP_TRY(hipMemset(c->chain_epoch, 0, 16));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->chain_err), 16, hipHostMallocMapped));
+    *c->chain_err = 0;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->chain_err_dev), c->chain_err, 0));
     ST_TRY(ensure_pinned(c.get(), 4 * kMaxK + 2 * np));
     // pipeline events only order host reads of the coherent pinned slots: device-scope release
     // (a system-scope one writes back and invalidates L2 at every iteration, ~8 us each);
@@ -467,6 +481,9 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->dscal);
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
+    (void)hipFree(c->chain_gran);
+    (void)hipFree(c->chain_epoch);
+    if (c->chain_err) (void)hipHostFree(c->chain_err);
     if (c->gram_part) (void)hipFree(c->gram_part);
     if (c->gram_G) (void)hipFree(c->gram_G);
     if (c->gram_ptrs) (void)hipFree(c->gram_ptrs);
@@ -509,6 +526,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
       case SPIS_OPT_ELL_GRAM: c->ell_gram = value != 0; return SPIS_OK;
+      case SPIS_OPT_MGS_CHAIN: c->mgs_chain = value != 0; return SPIS_OK;
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
@@ -1444,6 +1462,12 @@ struct Solver {
     ProfEv pm(c, SPIS_PROF_MGS);  // start on the first MGS step, stop on the normalise
     const LaunchEv e_first = pm.first();
     const LaunchEv e_last = pm.last();
+    if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n)) {  // K2p: the chain in one launch
+      const LaunchEv both{e_first.start, e_last.stop};
+      HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
+                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq));
+      return SPIS_OK;
+    }
     double* src = c->partA;
     double* dst = c->partB;
     int n_in = gs;
@@ -1566,7 +1590,7 @@ struct Solver {
   // captured once per workspace and step index; every pointer in it is a workspace / context /
   // matrix pointer (graph_key), the per-call values (seq) are read from pinned memory
   int arn_graph(int ja, hipGraphExec_t* out) {
-    const spis_workspace::GraphKey key{A->uid, c->pinned_dev, gs, gb, c->cgs2};
+    const spis_workspace::GraphKey key{A->uid, c->pinned_dev, gs, gb, c->cgs2, c->mgs_chain};
     if (!(ws->graph_key == key)) {
       drop_graphs(ws);
       ws->graph_key = key;
@@ -1859,6 +1883,12 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     HIP_TRY(hipStreamSynchronize(s));  // speculative Arnoldi steps finish before x / ws are used
     prof_drain(c);
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
+    if (*reinterpret_cast<volatile unsigned*>(c->chain_err) != 0) {  // never on a healthy device
+      *c->chain_err = 0;
+      c->mgs_chain = false;
+      return fail(SPIS_ERR_STATE, "persistent MGS chain: a workgroup never reached an exchange (the chain is "
+                                  "now disabled on this context; rerun the solve)");
+    }
     if (stamps) {
       stamps[4 * k] = t_start;
       stamps[4 * k + 1] = now_s();

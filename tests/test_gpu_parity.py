@@ -637,3 +637,37 @@ def test_distributed_code_path_self_halo(spis):
     np.testing.assert_allclose(r["res"][1:], ds["res"], rtol=1e-8, atol=1e-12 * r["res"][0])
     del r, Ad, bd, x0d, cons  # release device objects before the context goes
     ctx.close()
+
+
+@pytest.mark.parametrize("n", [1001, 300_001, 600_002, 2_000_001])
+def test_mgs_chain_matches_per_step_launches(spis, n):
+    """K2p (SPIS_OPT_MGS_CHAIN): the persistent MGS chain against one launch per MGS step, on
+    sizes that select each register tiling (PER = 2, 4, 8, 16 double2 per thread) and an odd
+    tail element.  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
+    agree to 1e-11 relative; the chain is bitwise reproducible run to run; orthogonality as MGS's."""
+    from structurepreservingiterativesolvers_amd import _lib, solvers
+    from structurepreservingiterativesolvers_amd.device import get_context
+
+    ctx = get_context()
+    rng = np.random.default_rng(n)
+    A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
+                   0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
+    b = rng.standard_normal(n)
+    k = 12
+    runs = []
+    for chain in (1, 1, 0):
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
+        try:
+            x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
+        finally:
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 1), "spis_set_option")
+        runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
+    (x1, r1, Q1), (x2, r2, Q2), (x0, r0, Q0) = runs
+    assert np.array_equal(x1, x2) and np.array_equal(r1, r2) and np.array_equal(Q1, Q2)
+    assert np.linalg.norm(x1 - x0) <= 1e-11 * np.linalg.norm(x0)
+    np.testing.assert_allclose(r1, r0, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(Q1, Q0, rtol=0, atol=1e-11)
+    # orthogonality: MGS's own loss, the same with either grouping of the partial dots
+    loss1 = np.abs(Q1 @ Q1.T - np.eye(k)).max()
+    loss0 = np.abs(Q0 @ Q0.T - np.eye(k)).max()
+    assert loss1 <= 4 * loss0 + 1e-14, (loss1, loss0)
