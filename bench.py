@@ -44,10 +44,11 @@ def spmv_bytes(n_rows, nnz):
     return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
-def mgs_bytes(n, p):
-    """Algorithmic bytes of one MGS chain over p basis vectors + normalise (fused form:
-    per step read y, q_i, q_{i+1}, write y; normalise reads y, writes q)."""
-    return 32 * n * p + 16 * n
+def mgs_bytes(n, p, chain=True):
+    """Algorithmic bytes of one MGS chain over p basis vectors + normalise.  Persistent chain
+    (K2p): y and q_0 read once, each further q_i once, q_p written; per-step launches: per step
+    read y, q_i, q_{i+1}, write y; normalise reads y, writes q."""
+    return 8 * n * (p + 2) if chain else 32 * n * p + 16 * n
 
 
 def dual_bytes(n_rows, nnz):
@@ -222,7 +223,7 @@ def main():
     sampled = [j + 1 for j in range(0, args.k, max(args.prof_period, 1))]
     p_mean = float(np.mean(sampled))  # basis size of the sampled (timed) MGS chains
     mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
-    mgs_gbs = mgs_bytes(n, p_mean) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
+    mgs_gbs = mgs_bytes(n, p_mean, n // 2 <= 256 * 256 * 8) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
     # the committed PMC summaries were measured on the C3 matrix: reported for that workload only

@@ -129,7 +129,7 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  * SPIS_OPT_ELL_GRAM (default 1): the fused constraint reduction (p + 1 <= 32) reads a sliced-ELL
  *   copy of each constraint matrix, built once on first use (static row boundaries).
  * SPIS_OPT_MGS_CHAIN (default 1): each Arnoldi step's MGS chain + normalise runs as one persistent
- *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^23); 0 = one
+ *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 0 = one
  *   launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
  *   so results differ from the per-step launches at roundoff level. */
 enum spis_option {

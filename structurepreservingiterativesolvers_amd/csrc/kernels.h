@@ -73,12 +73,12 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // with flag (host memory), it then publishes *seq there after a system-scope release
 // h = sqrt(sum(part_in)); q_next = y / h (if h != 0)
 // K2p: the whole MGS chain of one Arnoldi step (j+1 steps + normalise, solvers.py:193-198) in ONE
-// persistent launch: w and three basis-vector slices live in registers, each step's partial dot is
-// handed to every workgroup through 8-byte {tag, half} granules (sc1 stores / polls), summed in the
-// same fixed order everywhere.  Per step HBM reads q_{i+1} only (8 N), prefetched behind the
-// previous step's exchange; w is not written back (q_{j+1} = w / h is).  Single GPU.
+// persistent launch: w and three basis-vector slices live in registers, each step's partial dots
+// are gathered by workgroup 0 through 8-byte {tag, half} granules (sc1 stores / polls), summed in
+// a fixed order and handed back the same way.  Per step HBM reads q_{i+1} only (8 N), prefetched behind the
+// previous step's exchange; w is not written back (q_{j+1} = w / h is).  Single GPU, N <= 2^20.
 constexpr int kChainMaxWG = 256;                       // <= 256 partials per exchange
-constexpr int64_t kChainMaxPairs = int64_t(kChainMaxWG) * kBlock * 16;  // PER <= 16 double2
+constexpr int64_t kChainMaxPairs = int64_t(kChainMaxWG) * kBlock * 8;  // PER <= 8 double2 (N <= 2^20)
 inline bool mgs_chain_fits(int64_t n) { return (n >> 1) <= kChainMaxPairs; }
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,

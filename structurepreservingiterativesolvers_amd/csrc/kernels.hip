@@ -381,12 +381,16 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2p: persistent MGS chain (kernels.h).  Workgroup g owns pairs [g*256*PER, (g+1)*256*PER); thread
-// t holds pairs t + 256 k.  Per step i (h_i known everywhere):
+// K2p: persistent MGS chain (kernels.h).  Workgroup g owns pairs [g*256*PER, (g+1)*256*PER); data
+// thread t (waves 0-3) holds pairs t + 256 k in registers; wave 4 runs the exchange.  Per step i
+// (h_i known everywhere):
 //   y -= h_i q_i ; part = q_{i+1}.y (or y.y at the last step) — MGS's arithmetic, contraction off
-//   block_sum -> the workgroup's partial -> two granules {tag, lo32} {tag, hi32}, slot parity i&1
-//   wave 0 sweeps all partials' granules until every tag matches, sums them in a fixed order
-//   (identical in every workgroup) -> h_{i+1}; q_{i+2} loads are in flight meanwhile
+//   DPP wave sums + fixed combine -> the workgroup's partial -> two granules {tag, lo32} {tag,
+//   hi32} in slot parity i&1 (sc1 stores, from a data wave)
+//   workgroup 0's exchange wave sweeps all partials' granules until every tag matches, sums them
+//   in a fixed order and publishes h_{i+1} as two granules; the other workgroups' exchange waves
+//   poll those two (256 workgroups sweeping 512 granules each cost 15% of the chain in polling
+//   traffic); q_{i+2} loads of the data waves are in flight meanwhile
 // Tags are base + i + 1 with base read from a device counter the previous chain advanced, so no
 // per-call reset is needed and a replayed graph stays valid.  A slot parity is rewritten two steps
 // later, after every workgroup has read it (it cannot publish step i+2 before step i+1's exchange
@@ -404,8 +408,48 @@ __device__ __forceinline__ unsigned long long chain_load(const unsigned long lon
   return __hip_atomic_load((chain_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// wave sum on DPP moves only (ALU latency; __shfl_xor is ds_bpermute, LDS latency): xor 1, xor 2,
+// half-row and row mirrors make each 16-lane row uniform, row_bcast15/31 fold the rows into lane
+// 63, s_readlane broadcasts it.  A fixed order: every workgroup gets the same bits for the same
+// inputs (the chain relies on that for h).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1>(v);        // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);        // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);       // row_half_mirror
+  v += dpp_f64<0x140>(v);       // row_mirror: every lane of a row holds the row's sum
+  v += dpp_f64<0x142, 0xA>(v);  // row_bcast15 into rows 1, 3 (rows 0, 2 add 0)
+  v += dpp_f64<0x143, 0xC>(v);  // row_bcast31 into rows 2, 3: lane 63 holds the total
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
+}
+
+constexpr int kChainThreads = kBlock + 64;  // 4 data waves + 1 exchange wave
+
+// sum_partials' exact arithmetic (same per-thread loop, same shuffle wave sums, same combine) on
+// the 4 data waves, with the exchange wave joining the barriers: the first h and the piggybacked
+// residual get the same bits as from the per-step kernels and finalize_kernel
+__device__ __forceinline__ double chain_sum_partials(const double* __restrict__ part, int n, double* s_wave) {
+  const int tid = threadIdx.x;
+  double v = 0.0;
+  if (tid < kBlock)
+    for (int i = tid; i < n; i += kBlock) v += part[i];
+  v = wave_sum(v);
+  if (tid < kBlock && (tid & 63) == 0) s_wave[tid >> 6] = v;
+  __syncthreads();
+  const double t = ((s_wave[0] + s_wave[1]) + s_wave[2]) + s_wave[3];
+  __syncthreads();
+  return t;
+}
+
 template <int PER>
-__global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
+__global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
@@ -416,14 +460,17 @@ __global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
   __shared__ int s_fail;
   const int G = gridDim.x;
   const int tid = threadIdx.x;
+  const bool data = tid < kBlock;     // waves 0-3 hold the slices; wave 4 runs the exchange
   const int64_t npair = n >> 1;
   const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBlock * PER + tid;
+  // U = q_i (update), D = q_{i+1} (dot), P = q_{i+2} (in flight behind the exchange; a second
+  // vector of lead time measured no faster)
   double2 y[PER], U[PER], D[PER], P[PER];
   auto load = [&](double2 (&r)[PER], const double* v) {
     const double2* v2 = reinterpret_cast<const double2*>(v);
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (p0 + k * kBlock < npair) r[k] = v2[p0 + k * kBlock];
+      if (data && p0 + k * kBlock < npair) r[k] = v2[p0 + k * kBlock];
   };
   const unsigned base = *epoch;
   load(y, w);
@@ -437,10 +484,10 @@ __global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
     if (j >= 1) dt = Q[pitch + n - 1];
   }
   if (tid == 0) s_fail = 0;
-  double h = sum_partials(part_in, n_in, s_wave);
+  double h = chain_sum_partials(part_in, n_in, s_wave);
   if (blockIdx.x == 0 && tid == 0) hcol[0] = h;
   if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
-    const double t = sum_partials(xpart, n_x, s_wave);
+    const double t = chain_sum_partials(xpart, n_x, s_wave);
     if (tid == 0) publish(x_out, t, flag, seq);
   }
   for (int i = 0; i <= j; ++i) {
@@ -448,7 +495,7 @@ __global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
     double part = 0.0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (p0 + k * kBlock < npair) {
+      if (data && p0 + k * kBlock < npair) {
         const double a0 = h * U[k].x, a1 = h * U[k].y;
         y[k].x = y[k].x - a0;
         y[k].y = y[k].y - a1;
@@ -466,46 +513,77 @@ __global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
       yt = yt - a;
       part += last ? yt * yt : dt * yt;
     }
-    if (i + 2 <= j) {  // q_{i+2}: in flight behind the exchange
+    if (i + 2 <= j) {  // q_{i+2}: in flight behind the exchange (the exchange wave holds no loads)
       load(P, Q + static_cast<int64_t>(i + 2) * pitch);
       if (tail) pt = Q[static_cast<int64_t>(i + 2) * pitch + n - 1];
     }
-    const double tot = block_sum(part, s_wave);
+    {  // workgroup partial: DPP wave sums of the data waves, fixed combine
+      const double wv = wave_sum_dpp(part);
+      if (data && (tid & 63) == 0) s_wave[tid >> 6] = wv;
+    }
+    __syncthreads();
     const unsigned tag = base + static_cast<unsigned>(i) + 1u;
     unsigned long long* slots = gran + static_cast<size_t>(i & 1) * 2 * kChainMaxWG;
-    if (tid == 0) {
+    if (tid == 0) {  // publish from a data wave: the exchange wave's polls never wait on these stores
+      const double tot = ((s_wave[0] + s_wave[1]) + s_wave[2]) + s_wave[3];
       const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(tot));
       chain_store(slots + 2 * blockIdx.x, tag, static_cast<unsigned>(bits));
       chain_store(slots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bits >> 32));
     }
-    if (tid < 64) {  // wave 0: gather every workgroup's partial (granule 2g = lo, 2g + 1 = hi)
-      unsigned long long g[8];
+    if (tid >= kBlock) {  // exchange wave
+      const int lane = tid - kBlock;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      bool ok = false;
-      for (unsigned spins = 0;; ++spins) {
-        ok = true;
+      bool all_ok = false;
+      double acc = 0.0;
+      if (blockIdx.x == 0) {  // workgroup 0 gathers every workgroup's partial (granule 2g = lo, 2g+1 = hi)
+        unsigned long long g[8];
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int idx = lane + 64 * k;
+            g[k] = idx < 2 * G ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
+            ok &= static_cast<unsigned>(g[k] >> 32) == tag;
+          }
+          if (__all(ok)) {
+            all_ok = true;
+            break;
+          }
+          if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+        }
+        // fixed order: lane pairs (2m, 2m+1) of round k hold partial (64 k + 2 m) / 2; k-major
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int idx = tid + 64 * k;
-          g[k] = idx < 2 * G ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
-          ok &= static_cast<unsigned>(g[k] >> 32) == tag;
+          const unsigned lo = static_cast<unsigned>(g[k]);
+          const unsigned hi =
+              static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
+          const double v =
+              __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+          if ((lane & 1) == 0 && lane + 64 * k < 2 * G) acc += v;
         }
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-        if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+        acc = wave_sum_dpp(acc);
+        if (lane == 0) {  // and hands the sum to every other workgroup
+          const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(acc));
+          unsigned long long* hs = gran + 4 * kChainMaxWG + 2 * (i & 1);
+          chain_store(hs, tag, static_cast<unsigned>(bits));
+          chain_store(hs + 1, tag, static_cast<unsigned>(bits >> 32));
+        }
+      } else {  // the others poll workgroup 0's two granules (few pollers: the q stream keeps its bandwidth)
+        const unsigned long long* hs = gran + 4 * kChainMaxWG + 2 * (i & 1);
+        unsigned long long g = 0;
+        for (unsigned spins = 0;; ++spins) {
+          g = lane < 2 ? chain_load(hs + lane) : (static_cast<unsigned long long>(tag) << 32);
+          if (__all(static_cast<unsigned>(g >> 32) == tag)) {
+            all_ok = true;
+            break;
+          }
+          if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+        }
+        const unsigned lo = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 0, 64));
+        const unsigned hi = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 1, 64));
+        acc = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
       }
-      const bool all_ok = __all(ok);
-      // fixed order: lane pairs (2m, 2m+1) of round k hold partial (64 k + 2 m) / 2; sum k-major
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const unsigned lo = static_cast<unsigned>(g[k]);
-        const unsigned hi = static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
-        const double v = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
-        if ((tid & 1) == 0 && tid + 64 * k < 2 * G) acc += v;
-      }
-      acc = wave_sum(acc);
-      if (tid == 0) {
+      if (lane == 0) {
         s_h = acc;
         if (!all_ok) {
           s_fail = 1;
@@ -532,7 +610,7 @@ __global__ __launch_bounds__(kBlock, 1) void mgs_chain_kernel(
       double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (p0 + k * kBlock < npair)
+        if (data && p0 + k * kBlock < npair)
           q2[p0 + k * kBlock] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
       if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
     }
@@ -546,20 +624,16 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             unsigned long long* flag, const unsigned long long* seq) {
   const int64_t npair = n >> 1;
   if (npair > kChainMaxPairs || !aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
-  const int per = npair <= int64_t(kChainMaxWG) * kBlock * 2   ? 2
-                  : npair <= int64_t(kChainMaxWG) * kBlock * 4 ? 4
-                  : npair <= int64_t(kChainMaxWG) * kBlock * 8 ? 8
-                                                               : 16;
+  const int per = npair <= int64_t(kChainMaxWG) * kBlock * 2 ? 2 : npair <= int64_t(kChainMaxWG) * kBlock * 4 ? 4 : 8;
   const int64_t span = int64_t(kBlock) * per;
   const int G = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
 #define SPIS_CHAIN(PER_)                                                                                   \
-  launch_k(mgs_chain_kernel<PER_>, dim3(G), dim3(kBlock), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, hcol, \
+  launch_k(mgs_chain_kernel<PER_>, dim3(G), dim3(kChainThreads), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, hcol, \
            gran, epoch, err, xpart, n_x, x_out, flag, seq)
   switch (per) {
     case 2: SPIS_CHAIN(2); break;
     case 4: SPIS_CHAIN(4); break;
-    case 8: SPIS_CHAIN(8); break;
-    default: SPIS_CHAIN(16); break;
+    default: SPIS_CHAIN(8); break;
   }
 #undef SPIS_CHAIN
   return hipGetLastError();

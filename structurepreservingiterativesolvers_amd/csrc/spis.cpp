@@ -418,8 +418,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
-    HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * 4 * kChainMaxWG));
-    HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * 4 * kChainMaxWG));
+    HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * (4 * kChainMaxWG + 8)));
+    HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * (4 * kChainMaxWG + 8)));
     HIP_TRY(hipMalloc(&c->chain_epoch, 16));
     HIP_TRY(hipMemset(c->chain_epoch, 0, 16));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->chain_err), 16, hipHostMallocMapped));

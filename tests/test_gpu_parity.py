@@ -639,11 +639,11 @@ def test_distributed_code_path_self_halo(spis):
     ctx.close()
 
 
-@pytest.mark.parametrize("n", [1001, 300_001, 600_002, 2_000_001])
+@pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_048_575, 2_000_001])
 def test_mgs_chain_matches_per_step_launches(spis, n):
     """K2p (SPIS_OPT_MGS_CHAIN): the persistent MGS chain against one launch per MGS step, on
-    sizes that select each register tiling (PER = 2, 4, 8, 16 double2 per thread) and an odd
-    tail element.  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
+    sizes that select each register tiling (PER = 2, 4, 8 double2 per thread), the largest N the
+    chain takes (odd: a tail element) and one beyond it (per-step launches either way).  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
     agree to 1e-11 relative; the chain is bitwise reproducible run to run; orthogonality as MGS's."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
     from structurepreservingiterativesolvers_amd.device import get_context
