@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kBlock) void spmv_rowblock_kernel(
 // are read once; each product array and each row sum is exactly K1's (bit-identical rows).  It
 // runs on row blocks of <= CAP nnz (kDualCap: two CAP-long product arrays in LDS).
 // ---------------------------------------------------------------------------------------------
-template <int CAP>
+template <int CAP, int SWZ = 0>
 __global__ __launch_bounds__(kBlock) void spmv_dual_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ x1,
@@ -157,7 +157,19 @@ __global__ __launch_bounds__(kBlock) void spmv_dual_kernel(
   __shared__ double s_p2[CAP];
   __shared__ double s_wave[4];
   double pt1 = 0.0, pt2 = 0.0;
-  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+  // SWZ (tuning): 1 = XCD-swizzled logical workgroup id, grid-stride; 2 = swizzled id, one
+  // contiguous chunk of row blocks per workgroup (each XCD then owns an eighth of the rows)
+  const int G = gridDim.x;
+  int L = blockIdx.x;
+  if (SWZ && (G & 7) == 0) L = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  int b0 = L, b1 = n_blk, bs = G;
+  if (SWZ == 2) {
+    const int c = (n_blk + G - 1) / G;
+    b0 = L * c;
+    b1 = min(n_blk, b0 + c);
+    bs = 1;
+  }
+  for (int blk = b0; blk < b1; blk += bs) {
     const int r0 = blk_row[blk];
     const int r1 = blk_row[blk + 1];
     const int nz0 = rp[r0];

@@ -500,6 +500,14 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&dpr, 8 * 8192));
       CK(hipMemcpy(dx2, hx.data(), 8 * pitch, hipMemcpyHostToDevice));
       for (int i = 0; i < 5; ++i) CK(launch_spmv_dual(Ad, dx, dy, dpr, dx2, dw, dQ, dpart, g, s));
+      const int nbd = Ad.n_blk;
+      const int gd = nbd < 2048 ? nbd : 2048;
+      for (int i = 0; i < 5; ++i)
+        hipLaunchKernelGGL((spmv_dual_kernel<1024, 1>), dim3(gd), dim3(kBlock), 0, s, drp, dci, dva, dblkd, nbd, dx, dy,
+                           dpr, dx2, dw, dQ, dpart);
+      for (int i = 0; i < 5; ++i)
+        hipLaunchKernelGGL((spmv_dual_kernel<1024, 2>), dim3(gd), dim3(kBlock), 0, s, drp, dci, dva, dblkd, nbd, dx, dy,
+                           dpr, dx2, dw, dQ, dpart);
       CK(hipStreamSynchronize(s));
     }
     for (int i = 0; i < 5; ++i)
@@ -602,6 +610,18 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(spmv_dual_il<2048>, dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb,
                                reinterpret_cast<const double2*>(dxz), dy, dpr, dw, dQ, dpart);
         });
+        if (cap == 1024) {
+          snprintf(nm, sizeof nm, "spmv dual swz1 cap=%d grid=%d", cap, gg);
+          timeit(nm, 50, SD, [&] {
+            hipLaunchKernelGGL((spmv_dual_kernel<1024, 1>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx,
+                               dy, dpr, dx2, dw, dQ, dpart);
+          });
+          snprintf(nm, sizeof nm, "spmv dual swz2 cap=%d grid=%d", cap, gg);
+          timeit(nm, 50, SD, [&] {
+            hipLaunchKernelGGL((spmv_dual_kernel<1024, 2>), dim3(gg), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx,
+                               dy, dpr, dx2, dw, dQ, dpart);
+          });
+        }
         snprintf(nm, sizeof nm, "spmv dual cap=%d grid=%d", cap, gg);
         timeit(nm, 50, SD, [&] {
           if (cap == 1024)
