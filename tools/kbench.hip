@@ -469,6 +469,40 @@ int main(int argc, char** argv) {
     run("copy + hipStreamWriteValue64 to host", 8);
     return 0;
   }
+  if (argc > 2 && std::string(argv[2]) == "gap") {
+    // kernel-boundary gaps around the persistent MGS chain (read them from a rocprofv3 kernel
+    // trace): 20 x [chain(j=15) -> gemv(p=16)], 20 x [chain -> copy], 20 x [copy -> gemv]
+    unsigned long long* gran;
+    unsigned *ep, *err;
+    CK(hipMalloc(&gran, 8 * (4 * kChainMaxWG + 8)));
+    CK(hipMemset(gran, 0, 8 * (4 * kChainMaxWG + 8)));
+    CK(hipMalloc(&ep, 16));
+    CK(hipMemset(ep, 0, 16));
+    CK(hipMalloc(&err, 16));
+    CK(hipMemset(err, 0, 16));
+    double* dhost;
+    CK(hipHostMalloc(reinterpret_cast<void**>(&dhost), 8 * 64, hipHostMallocMapped));
+    double* dhost_dev;
+    CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dhost_dev), dhost, 0));
+    std::vector<double> y(16, 0.01);
+    const int64_t m = (n / 2);
+    auto chain = [&](double* hc) {
+      CK(launch_mgs_chain(n, dy, dQ, pitch, 15, dpart, 1024, hc, gran, ep, err, s, nullptr, nullptr, 0, nullptr,
+                          nullptr, nullptr));
+    };
+    auto gemv = [&] { CK(launch_gemv(n, 16, dQ, pitch, y.data(), true, dx, dy, s, nullptr)); };
+    auto copy = [&] {
+      hipLaunchKernelGGL(copy2_kernel, dim3(2048), dim3(kBlock), 0, s, m, reinterpret_cast<const double2*>(dx),
+                         reinterpret_cast<double2*>(dy));
+    };
+    for (int r = 0; r < 20; ++r) { chain(dhost_dev); gemv(); }
+    for (int r = 0; r < 20; ++r) { chain(dhost_dev); copy(); }
+    for (int r = 0; r < 20; ++r) { chain(dh); copy(); }  // H column in device memory
+    for (int r = 0; r < 20; ++r) { copy(); gemv(); }
+    CK(hipStreamSynchronize(s));
+    printf("gap mode done\n");
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "pmc") {
     // PMC mode: 3 calibration streams of 1 GiB each (known bytes), then 5 Arnoldi SpMVs
     const int64_t m8 = int64_t(1) << 27;
