@@ -100,6 +100,7 @@ struct spis_context {
   double* pinned_dev = nullptr;  // the same memory as seen from the device
   size_t pinned_len = 0;     // doubles
   hipEvent_t ev_arn = nullptr, ev_upd[2] = {nullptr, nullptr};  // solver pipeline events
+  hipEvent_t ev_gram = nullptr;  // constrained step: the Gram tile has reached pinned memory
   unsigned long long seq = 0;  // last completion sequence number handed to a publishing kernel
   double* gram_part = nullptr;
   size_t gram_part_len = 0;
@@ -437,6 +438,7 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_arn, evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
     *out = c.release();
     return SPIS_OK;
   })
@@ -495,7 +497,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
       (void)hipEventDestroy(p.b);
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1]})
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1154,7 +1156,8 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                    use_ell ? &ev : nullptr));
     const int cnt = np1 * np1 + nvv * np1;
     HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
+    ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
     Gm[ci].assign(c->gram_pinned, c->gram_pinned + np1 * np1);
     if (!v_done) {
       std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + cnt, Gv.begin());
@@ -1166,7 +1169,8 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
     HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
     HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * (np1 * np1 + nvv * np1), hipMemcpyDeviceToHost,
                            c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));
+    ST_TRY(wait_event(c->ev_gram));
     std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + np1 * np1 + nvv * np1, Gv.begin());
   }
   for (int ci = 0; ci < m; ++ci) {
@@ -1719,7 +1723,17 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)
+    // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
+    // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
+    if (stamps) stamps[0] = now_s();
+    ST_TRY(S.enqueue_arnoldi(0));
+    HIP_TRY(hipEventRecord(c->ev_arn, s));
+    if (k > 1) {
+      if (stamps) stamps[1] = now_s();
+      ST_TRY(S.enqueue_arnoldi(1));
+    }
+    ST_TRY(wait_event(c->ev_gram));
     const double beta = *beta_slot;
     int n_res = 0;
     out->res_host[n_res++] = beta;
@@ -1736,14 +1750,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     if (beta == 0.0) {  // x0 solves the system: q0 would be 0/0 (reference: NaNs); report breakdown
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
       ws->broke_at_start = true;
-    } else {
-      if (stamps) stamps[0] = now_s();
-      ST_TRY(S.enqueue_arnoldi(0));
-      HIP_TRY(hipEventRecord(c->ev_arn, s));
-      if (k > 1) {
-        if (stamps) stamps[1] = now_s();
-        ST_TRY(S.enqueue_arnoldi(1));
-      }
     }
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
       ST_TRY(j == 0 ? wait_event(c->ev_arn) : S.wait_update(j - 1));
