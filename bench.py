@@ -152,6 +152,7 @@ def main():
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
+    ap.add_argument("--no-overlap", action="store_true", help="update GEMV on the main stream (no side stream)")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
                     help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
@@ -180,6 +181,8 @@ def main():
     conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1 if args.graphs else 0), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 0 if args.no_fuse else 1), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 0 if args.no_overlap else 1),
+               "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
                "spis_set_option")
 

@@ -131,14 +131,17 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  * SPIS_OPT_MGS_CHAIN (default 1): each Arnoldi step's MGS chain + normalise runs as one persistent
  *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 0 = one
  *   launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
- *   so results differ from the per-step launches at roundoff level. */
+ *   so results differ from the per-step launches at roundoff level.
+ * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
+ *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
   SPIS_OPT_GRAPHS = 3,
   SPIS_OPT_ORTHOG = 4,
   SPIS_OPT_ELL_GRAM = 5,
-  SPIS_OPT_MGS_CHAIN = 6
+  SPIS_OPT_MGS_CHAIN = 6,
+  SPIS_OPT_OVERLAP_GEMV = 7
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

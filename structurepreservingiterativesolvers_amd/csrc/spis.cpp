@@ -124,6 +124,9 @@ struct spis_context {
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   bool ell_gram = true;             // K7 on the sliced-ELL copy (SPIS_OPT_ELL_GRAM)
   bool mgs_chain = true;            // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN)
+  bool overlap_gemv = true;         // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_gemv = nullptr;
   unsigned long long* chain_gran = nullptr;  // 2 parities x kChainMaxWG x 2 granules
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
@@ -412,6 +415,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     std::unique_ptr<spis_context> c(new spis_context());
     c->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_gemv, hipEventDisableTiming | hipEventReleaseToDevice));
     const int np = std::max(kSpmvGrid, kRedGrid);
     HIP_TRY(hipMalloc(&c->partA, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
@@ -497,9 +502,11 @@ extern "C" int spis_context_destroy(spis_context* c) {
       (void)hipEventDestroy(p.b);
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram})
+    (void)hipStreamSynchronize(c->stream2);
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_gemv})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream2);
     delete c;
     return SPIS_OK;
   })
@@ -529,6 +536,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
       case SPIS_OPT_ELL_GRAM: c->ell_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN: c->mgs_chain = value != 0; return SPIS_OK;
+      case SPIS_OPT_OVERLAP_GEMV: c->overlap_gemv = value != 0; return SPIS_OK;
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
@@ -1529,8 +1537,8 @@ struct Solver {
   }
 
   // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
-  int update_gemv(int j, int p, const double* y) {  // solvers.py:287
-    hipStream_t s = c->stream;
+  int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr) {  // solvers.py:287
+    hipStream_t s = s_gemv ? s_gemv : c->stream;
     c->prof_iter = j;
     {
       ProfEv pg(c, SPIS_PROF_GEMV);
@@ -1622,7 +1630,17 @@ struct Solver {
 
   // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
   int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
-    ST_TRY(update_gemv(j, p, y));
+    if (c->overlap_gemv && !c->comm && p <= kYArg) {
+      // U_j's GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM
+      // traffic) still running on the main stream; the dual SpMV waits for it.  Safe: every
+      // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
+      // published U_{j-1}'s residual started, and the GEMV's inputs were written before that.
+      ST_TRY(update_gemv(j, p, y, c->stream2));
+      HIP_TRY(hipEventRecord(c->ev_gemv, c->stream2));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_gemv, 0));
+    } else {
+      ST_TRY(update_gemv(j, p, y));
+    }
     ST_TRY(arnoldi_pre(ja));
     if (!c->comm) next_seq(j);
     const bool sampled = c->prof && ((j % c->prof_period) == 0 || (ja % c->prof_period) == 0);
@@ -1890,7 +1908,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
     }
-    HIP_TRY(hipStreamSynchronize(s));  // speculative Arnoldi steps finish before x / ws are used
+    // speculative Arnoldi steps finish before x / ws are used (event spin: a blocking synchronize
+    // wakes the host up tens of us late, per solve)
+    HIP_TRY(hipEventRecord(c->ev_gram, s));
+    ST_TRY(wait_event(c->ev_gram));
     prof_drain(c);
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
     if (*reinterpret_cast<volatile unsigned*>(c->chain_err) != 0) {  // never on a healthy device

@@ -54,6 +54,7 @@ _OPTIONS = {
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
     "ell_gram": (_lib.OPT_ELL_GRAM, None),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, None),
+    "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, None),
 }
 
 
@@ -67,6 +68,7 @@ def set_option(name, value, ctx=None):
     * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
     * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix;
     * ``mgs_chain`` (True): each Arnoldi step's MGS chain + normalise as one persistent launch;
+    * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
     * ``device_ilu`` ("auto"): how a SuperLU ``pre`` (``spilu``/``splu``) is applied — True on
       the device (K8), False by its host ``pre.solve`` through the callback (as the reference
       does), "auto" on the device when the plan's cost model predicts it is faster

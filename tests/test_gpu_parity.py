@@ -231,9 +231,10 @@ def test_fused_and_generic_constraint_reduction_agree(spis):
 
 
 def test_fused_dual_spmv_bit_identical(spis):
-    """SPIS_OPT_FUSE_SPMV / SPIS_OPT_GRAPHS: the true-residual SpMV of U_j fused with the Arnoldi
-    SpMV of A_{j+2} (matrix read once), and the Arnoldi steps replayed from captured graphs, give
-    bit-identical iterates, residuals, LS solutions and basis."""
+    """SPIS_OPT_FUSE_SPMV / SPIS_OPT_GRAPHS / SPIS_OPT_OVERLAP_GEMV: the true-residual SpMV of U_j
+    fused with the Arnoldi SpMV of A_{j+2} (matrix read once), the Arnoldi steps replayed from
+    captured graphs, and the update GEMV on a second stream give bit-identical iterates,
+    residuals, LS solutions and basis."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
     from structurepreservingiterativesolvers_amd.device import get_context
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
@@ -250,14 +251,17 @@ def test_fused_dual_spmv_bit_identical(spis):
             c = Case("lkdv_m50_cgmres_tol1e-19")
             A, b, cons = c.A, c.b, c.conlist()
         runs = []
-        for fuse, graphs in ((0, 0), (1, 0), (1, 1), (1, 1)):  # the last run replays cached graphs
+        # the last run replays cached graphs; OVERLAP_GEMV moves the update GEMV to a second stream
+        for fuse, graphs, overlap in ((0, 0, 0), (1, 0, 0), (1, 0, 1), (1, 1, 1), (1, 1, 1)):
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, graphs), "spis_set_option")
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, overlap), "spis_set_option")
             try:
                 x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
             finally:  # back to the defaults
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 1), "spis_set_option")
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 0), "spis_set_option")
+                _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 1), "spis_set_option")
             runs.append((x, np.asarray(d["res"]), np.concatenate(d["x"].y), d["x"].basis(25), np.asarray(d["x"])))
         for r in runs[1:]:
             for a, bb in zip(runs[0], r):
