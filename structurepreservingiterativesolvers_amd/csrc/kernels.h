@@ -41,6 +41,11 @@ struct CsrView {
   const double* vals;
   const int32_t* blk_row;  // row-block boundaries [n_blk + 1]
   int32_t n_blk;
+  // XCD-swizzled block walk: workgroups dealt to XCD x (blockIdx % 8) take a contiguous eighth of
+  // each grid-stride round of row blocks.  On the dual SpMV's 1024 table it cuts the reads from
+  // 287 to 223 MB per launch and runs 46.7 -> 45.5 us alone (kbench), but 51 -> 52-53 us inside
+  // the solver: off.  K1 launches on a swizzled table follow it, so partials group alike.
+  bool swz = false;
 };
 
 // grid sizes (a fixed count when partials are all-reduced across ranks)

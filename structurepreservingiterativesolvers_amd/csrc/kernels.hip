@@ -76,15 +76,20 @@ static void launch_k(F kernel, dim3 g, dim3 b, uint32_t shm, hipStream_t s, cons
 // (strided partials + fixed-order tree: deterministic, not SciPy's order).
 // Workgroups loop over row blocks (grid-stride) so the epilogue leaves <= kSpmvGrid partials.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int swizzled_block(bool swz) {
+  const int G = gridDim.x;
+  return (swz && (G & 7) == 0) ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(kBlock) void spmv_rowblock_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ x,
-    double* __restrict__ y, const double* __restrict__ aux, double* __restrict__ partials) {
+    double* __restrict__ y, const double* __restrict__ aux, double* __restrict__ partials, bool swz) {
   __shared__ double s_prod[kNnzCap];
   __shared__ double s_wave[4];
   double part = 0.0;
-  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+  for (int blk = swizzled_block(swz); blk < n_blk; blk += gridDim.x) {
     const int r0 = blk_row[blk];
     const int r1 = blk_row[blk + 1];
     const int nz0 = rp[r0];
@@ -238,8 +243,12 @@ __global__ __launch_bounds__(kBlock) void spmv_dual_kernel(
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev) {
-  launch_k(spmv_dual_kernel<kDualCap>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
-           A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
+  if (A.swz)
+    launch_k(spmv_dual_kernel<kDualCap, 1>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
+             A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
+  else
+    launch_k(spmv_dual_kernel<kDualCap, 0>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
+             A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
   return hipGetLastError();
 }
 
@@ -262,19 +271,19 @@ hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, co
   switch (epi) {
     case kEpiPlain:
       launch_k(spmv_rowblock_kernel<kEpiPlain>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
-               x, y, aux, partials);
+               x, y, aux, partials, A.swz);
       break;
     case kEpiDot:
       launch_k(spmv_rowblock_kernel<kEpiDot>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
-               x, y, aux, partials);
+               x, y, aux, partials, A.swz);
       break;
     case kEpiResNorm:
       launch_k(spmv_rowblock_kernel<kEpiResNorm>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row,
-               A.n_blk, x, y, aux, partials);
+               A.n_blk, x, y, aux, partials, A.swz);
       break;
     default:
       launch_k(spmv_rowblock_kernel<kEpiR0>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_row, A.n_blk,
-               x, y, aux, partials);
+               x, y, aux, partials, A.swz);
       break;
   }
   return hipGetLastError();

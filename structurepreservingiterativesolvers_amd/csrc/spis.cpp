@@ -170,7 +170,7 @@ struct spis_matrix {
   int32_t* send_idx = nullptr;
   double* send_buf = nullptr;
   CsrView view() const { return CsrView{n_rows, indptr, indices, vals, blk_row, n_blk}; }
-  CsrView dual_view() const { return CsrView{n_rows, indptr, indices, vals, blk_row_d, n_blk_d}; }
+  CsrView dual_view() const { return CsrView{n_rows, indptr, indices, vals, blk_row_d, n_blk_d, false}; }
 };
 
 struct ConCache {
