@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
     ap.add_argument("--no-overlap", action="store_true", help="update GEMV on the main stream (no side stream)")
+    ap.add_argument("--spmv-pipe", default="xcd", choices=["off", "stride", "xcd", "stride2", "xcd2"],
+                    help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
+                         "pipelined XCD-local walk")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
                     help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
@@ -184,6 +187,8 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 0 if args.no_overlap else 1),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
+               "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}[args.spmv_pipe]),
                "spis_set_option")
 
     if wl["cycles"] > 1:

@@ -133,7 +133,12 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
  *   so results differ from the per-step launches at roundoff level.
  * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
- *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical. */
+ *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
+ * SPIS_OPT_SPMV_PIPE (default 2): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
+ *   software-pipelined row-block kernels; 2 = each XCD's workgroups walk a contiguous eighth of
+ *   the row blocks (its share of the gathered vectors stays in its own L2), 1 = grid-stride walk,
+ *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight.  Rows are bit-identical in every mode; the reduction partials
+ *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -141,7 +146,8 @@ enum spis_option {
   SPIS_OPT_ORTHOG = 4,
   SPIS_OPT_ELL_GRAM = 5,
   SPIS_OPT_MGS_CHAIN = 6,
-  SPIS_OPT_OVERLAP_GEMV = 7
+  SPIS_OPT_OVERLAP_GEMV = 7,
+  SPIS_OPT_SPMV_PIPE = 8
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

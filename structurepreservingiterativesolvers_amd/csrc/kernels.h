@@ -13,6 +13,7 @@ constexpr int kNnzCap = 2048;    // nnz staged in LDS per row block (16 KiB fp64
 constexpr int kItemCap = 2048;   // merge items (rows + nnz) per row block
 constexpr int kDualCap = 1024;   // nnz / items per row block of the fused dual SpMV (2 x 8 KiB LDS)
 constexpr int kSpmvGrid = 2048;  // max SpMV workgroups (= max epilogue partials)
+constexpr int kPipeGridFixed = 1280;  // pipelined SpMV workgroups on several ranks (MI355X: 256 CUs x 5 resident)
 constexpr int kRedGrid = 1024;   // max BLAS-1 workgroups (= max reduction partials)
 constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's LDS copy of y
 constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
@@ -46,6 +47,13 @@ struct CsrView {
   // 287 to 223 MB per launch and runs 46.7 -> 45.5 us alone (kbench), but 51 -> 52-53 us inside
   // the solver: off.  K1 launches on a swizzled table follow it, so partials group alike.
   bool swz = false;
+  // Pipelined SpMV (K1p / K1dp): with a (row start, nz start) table per row block, the
+  // launch_spmv* entry points run the software-pipelined kernels instead (next block's val/col and
+  // row data loaded while the current block's gathers are in flight).  walk: 0 = grid-stride over
+  // blockIdx; 1 = XCD-local (workgroups blockIdx % 8 == x walk the x-th eighth of the blocks).
+  const int2* blk_meta = nullptr;
+  int walk = 0;
+  int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
 };
 
 // grid sizes (a fixed count when partials are all-reduced across ranks)
@@ -68,6 +76,11 @@ hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, co
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev = nullptr);
+// K1p / K1dp (A.blk_meta on a kDualCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
+// part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi)
+hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
+                            double* part1, const double* x2, const double* aux2, double* y2, double* part2,
+                            int grid, hipStream_t s, const LaunchEv* ev = nullptr);
 // y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,

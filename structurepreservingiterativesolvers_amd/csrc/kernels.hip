@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace spis {
@@ -240,9 +242,328 @@ __global__ __launch_bounds__(kBlock) void spmv_dual_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1p / K1dp: software-pipelined SpMV on row blocks of <= CAP nnz with a (row start, nz start)
+// table.  Per block the unpipelined kernels pay ~5 dependent memory round trips (block table ->
+// indptr -> val/col -> x gathers -> indptr/aux of the rows); here the block table is scalar,
+// and block i+1's val/col, row bounds and row aux values are loaded while block i's gathers are in
+// flight, so a workgroup waits about one memory latency per block.  Each row sum is K1's (left
+// to right over the rounded products): rows are bit-identical to K1 / K1d.  MODE 0-3 = a single
+// SpMV with K1's epilogue of that number; MODE 4 = K1d's dual (residual of x1, Arnoldi of x2).
+// ---------------------------------------------------------------------------------------------
+template <int CAP>
+struct PipeStage {
+  static constexpr int kPer = CAP / kBlock;
+  int r0, r1, nz0, nnz;
+  int cols[kPer];
+  double vals[kPer];
+  int rs, re;     // this thread's row bounds relative to nz0 (rows r0 + threadIdx.x)
+  double a1, a2;  // the row's aux values (b / q0 / aux)
+};
+
+template <int CAP, int MODE, bool NT = false>
+__device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int blk,
+                                          const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                          const double* __restrict__ va, const double* __restrict__ aux1,
+                                          const double* __restrict__ aux2) {
+  const int2 m0 = meta[blk];
+  const int2 m1 = meta[blk + 1];
+  st.r0 = m0.x;
+  st.r1 = m1.x;
+  st.nz0 = m0.y;
+  st.nnz = m1.y - m0.y;
+  if (st.nnz > CAP) return;  // long row: read directly by the workgroup-wide path
+#pragma unroll
+  for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
+    const int i = threadIdx.x + u * kBlock;
+    if (NT) {  // streamed once: keep L2 for the gathered vectors
+      st.cols[u] = i < st.nnz ? __builtin_nontemporal_load(ci + st.nz0 + i) : 0;
+      st.vals[u] = i < st.nnz ? __builtin_nontemporal_load(va + st.nz0 + i) : 0.0;
+    } else {
+      st.cols[u] = i < st.nnz ? ci[st.nz0 + i] : 0;
+      st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
+    }
+  }
+  const int r = st.r0 + threadIdx.x;
+  if (r < st.r1) {
+    st.rs = rp[r] - st.nz0;
+    st.re = rp[r + 1] - st.nz0;
+    if (MODE != kEpiPlain) st.a1 = aux1[r];
+    if (MODE == 4) st.a2 = aux2[r];
+  } else {
+    st.rs = st.re = 0;
+  }
+}
+
+__device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1, int& bs) {
+  const int G = gridDim.x;
+  if (walk == 1 && (G & 7) == 0) {
+    const int x = blockIdx.x & 7;
+    b0 = static_cast<int>((static_cast<int64_t>(n_blk) * x) >> 3) + (blockIdx.x >> 3);
+    b1 = static_cast<int>((static_cast<int64_t>(n_blk) * (x + 1)) >> 3);
+    bs = G >> 3;
+  } else {
+    b0 = blockIdx.x;
+    b1 = n_blk;
+    bs = G;
+  }
+}
+
+// x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
+// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half
+template <int CAP, int MODE, bool NT = false, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void spmv_pipe_kernel(
+    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
+    const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
+    const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
+    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
+    double* __restrict__ part2) {
+  constexpr bool DUAL = MODE == 4;
+  constexpr int kPer = PipeStage<CAP>::kPer;
+  // products at padded index i + i/16: one thread per row reads its row left to right, and rows
+  // of 16 entries (swe's edge rows) would otherwise put a wave's lanes 256 B apart, all in one
+  // LDS bank group; the pad staggers them
+  __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
+  __shared__ double s_wave[4];
+  double pt1 = 0.0, pt2 = 0.0;
+  int b0, b1, bs;
+  block_walk(n_blk, walk, b0, b1, bs);
+  PipeStage<CAP> cur;
+  if (b0 < b1) pipe_load<CAP, MODE, NT>(cur, meta, b0, rp, ci, va, aux1, aux2);
+  for (int blk = b0; blk < b1; blk += bs) {
+    const int nb = blk + bs;
+    if (cur.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
+      double s1 = 0.0, s2 = 0.0;
+      {
+        double acc1 = 0.0, acc2 = 0.0;
+        for (int i = cur.nz0 + threadIdx.x; i < cur.nz0 + cur.nnz; i += kBlock) {
+          acc1 += va[i] * x1[ci[i]];
+          if (DUAL) acc2 += va[i] * x2[ci[i]];
+        }
+        s1 = block_sum(acc1, s_wave);
+        if (DUAL) s2 = block_sum(acc2, s_wave);
+      }
+      if (threadIdx.x == 0) {
+        const int r0 = cur.r0;
+        if (DUAL) {
+          const double t = s1 - aux1[r0];
+          pt1 += t * t;
+          y2[r0] = s2;
+          pt2 += aux2[r0] * s2;
+        }
+        if (MODE == kEpiPlain) y1[r0] = s1;
+        if (MODE == kEpiDot) { y1[r0] = s1; pt1 += aux1[r0] * s1; }
+        if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
+        if (MODE == kEpiR0) { const double t = aux1[r0] - s1; y1[r0] = t; pt1 += t * t; }
+      }
+      if (nb < b1) pipe_load<CAP, MODE, NT>(cur, meta, nb, rp, ci, va, aux1, aux2);
+      continue;
+    }
+    // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
+    // include the prefetch, and the prefetch is in flight through the LDS phase below
+    double g1[kPer], g2[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      g1[u] = x1[cur.cols[u]];
+      if (DUAL) g2[u] = x2[cur.cols[u]];
+    }
+    PipeStage<CAP> nxt;
+    nxt.nnz = 0;
+    if (nb < b1) pipe_load<CAP, MODE, NT>(nxt, meta, nb, rp, ci, va, aux1, aux2);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < cur.nnz) {
+        if constexpr (DUAL)
+          s_p[i + (i >> 4)] = make_double2(cur.vals[u] * g1[u], cur.vals[u] * g2[u]);
+        else
+          s_p[i + (i >> 4)] = cur.vals[u] * g1[u];
+      }
+    }
+    __syncthreads();
+    const int r = cur.r0 + threadIdx.x;
+    if (r < cur.r1) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int t = cur.rs; t < cur.re; ++t) {
+        if constexpr (DUAL) {
+          const double2 pp = s_p[t + (t >> 4)];
+          s1 += pp.x;
+          s2 += pp.y;
+        } else {
+          s1 += s_p[t + (t >> 4)];
+        }
+      }
+      if (DUAL) {
+        const double t = s1 - cur.a1;
+        pt1 += t * t;
+        y2[r] = s2;
+        pt2 += cur.a2 * s2;
+      }
+      if (MODE == kEpiPlain) y1[r] = s1;
+      if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
+      if (MODE == kEpiResNorm) { const double t = s1 - cur.a1; pt1 += t * t; }
+      if (MODE == kEpiR0) { const double t = cur.a1 - s1; y1[r] = t; pt1 += t * t; }
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+  if (MODE != kEpiPlain) {
+    const double tot1 = block_sum(pt1, s_wave);
+    double tot2 = 0.0;
+    if (DUAL) tot2 = block_sum(pt2, s_wave);
+    if (threadIdx.x == 0) {
+      part1[blockIdx.x] = tot1;
+      if (DUAL) part2[blockIdx.x] = tot2;
+    }
+  }
+}
+
+// Two-deep variant: block i+1's gathers and block i+2's val/col loads are in flight while block
+// i's products go through LDS, so a workgroup's wait per block is max(memory latency, LDS phase)
+// rather than their sum (~110 VGPRs: 4 workgroups per CU).  Same arithmetic as above.
+template <int CAP, int MODE>
+struct PipeGath {
+  double g1[CAP / kBlock], g2[CAP / kBlock];
+};
+
+template <int CAP, int MODE>
+__device__ __forceinline__ void pipe_gather(PipeGath<CAP, MODE>& G, const PipeStage<CAP>& st,
+                                            const double* __restrict__ x1, const double* __restrict__ x2) {
+  if (st.nnz > CAP) return;
+#pragma unroll
+  for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
+    G.g1[u] = x1[st.cols[u]];
+    if (MODE == 4) G.g2[u] = x2[st.cols[u]];
+  }
+}
+
+template <int CAP, int MODE>
+__global__ __launch_bounds__(kBlock) void spmv_pipe2_kernel(
+    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
+    const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
+    const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
+    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
+    double* __restrict__ part2) {
+  constexpr bool DUAL = MODE == 4;
+  constexpr int kPer = PipeStage<CAP>::kPer;
+  __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
+  __shared__ double s_wave[4];
+  double pt1 = 0.0, pt2 = 0.0;
+  int b0, b1, bs;
+  block_walk(n_blk, walk, b0, b1, bs);
+  PipeStage<CAP> s0, s1;
+  PipeGath<CAP, MODE> g0, g1n;
+  s0.nnz = 0;
+  s1.nnz = 0;
+  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0, rp, ci, va, aux1, aux2);
+  if (b0 < b1) pipe_gather<CAP, MODE>(g0, s0, x1, x2);
+  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, b0 + bs, rp, ci, va, aux1, aux2);
+  for (int blk = b0; blk < b1; blk += bs) {
+    // in flight from the previous round: g0 (block blk) and s1 (block blk + bs)
+    if (blk + bs < b1) pipe_gather<CAP, MODE>(g1n, s1, x1, x2);
+    PipeStage<CAP> s2;
+    s2.nnz = 0;
+    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, blk + 2 * bs, rp, ci, va, aux1, aux2);
+    if (s0.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
+      double acc1 = 0.0, acc2 = 0.0;
+      for (int i = s0.nz0 + threadIdx.x; i < s0.nz0 + s0.nnz; i += kBlock) {
+        acc1 += va[i] * x1[ci[i]];
+        if (DUAL) acc2 += va[i] * x2[ci[i]];
+      }
+      const double s1v = block_sum(acc1, s_wave);
+      const double s2v = DUAL ? block_sum(acc2, s_wave) : 0.0;
+      if (threadIdx.x == 0) {
+        const int r0 = s0.r0;
+        if (DUAL) {
+          const double t = s1v - aux1[r0];
+          pt1 += t * t;
+          y2[r0] = s2v;
+          pt2 += aux2[r0] * s2v;
+        }
+        if (MODE == kEpiPlain) y1[r0] = s1v;
+        if (MODE == kEpiDot) { y1[r0] = s1v; pt1 += aux1[r0] * s1v; }
+        if (MODE == kEpiResNorm) { const double t = s1v - aux1[r0]; pt1 += t * t; }
+        if (MODE == kEpiR0) { const double t = aux1[r0] - s1v; y1[r0] = t; pt1 += t * t; }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int i = threadIdx.x + u * kBlock;
+        if (i < s0.nnz) {
+          if constexpr (DUAL)
+            s_p[i + (i >> 4)] = make_double2(s0.vals[u] * g0.g1[u], s0.vals[u] * g0.g2[u]);
+          else
+            s_p[i + (i >> 4)] = s0.vals[u] * g0.g1[u];
+        }
+      }
+      __syncthreads();
+      const int r = s0.r0 + threadIdx.x;
+      if (r < s0.r1) {
+        double sa = 0.0, sb = 0.0;
+        for (int t = s0.rs; t < s0.re; ++t) {
+          if constexpr (DUAL) {
+            const double2 pp = s_p[t + (t >> 4)];
+            sa += pp.x;
+            sb += pp.y;
+          } else {
+            sa += s_p[t + (t >> 4)];
+          }
+        }
+        if (DUAL) {
+          const double t = sa - s0.a1;
+          pt1 += t * t;
+          y2[r] = sb;
+          pt2 += s0.a2 * sb;
+        }
+        if (MODE == kEpiPlain) y1[r] = sa;
+        if (MODE == kEpiDot) { y1[r] = sa; pt1 += s0.a1 * sa; }
+        if (MODE == kEpiResNorm) { const double t = sa - s0.a1; pt1 += t * t; }
+        if (MODE == kEpiR0) { const double t = s0.a1 - sa; y1[r] = t; pt1 += t * t; }
+      }
+      __syncthreads();
+    }
+    s0 = s1;
+    g0 = g1n;
+    s1 = s2;
+  }
+  if (MODE != kEpiPlain) {
+    const double tot1 = block_sum(pt1, s_wave);
+    double tot2 = 0.0;
+    if (DUAL) tot2 = block_sum(pt2, s_wave);
+    if (threadIdx.x == 0) {
+      part1[blockIdx.x] = tot1;
+      if (DUAL) part2[blockIdx.x] = tot2;
+    }
+  }
+}
+
+hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
+                            double* part1, const double* x2, const double* aux2, double* y2, double* part2,
+                            int grid, hipStream_t s, const LaunchEv* ev) {
+  dim3 g(grid), b(kBlock);
+#define SPIS_PIPE(M)                                                                                            \
+  if (A.depth == 2)                                                                                             \
+    launch_k(spmv_pipe2_kernel<kDualCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
+  else                                                                                                          \
+    launch_k(spmv_pipe_kernel<kDualCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2)
+  switch (mode) {
+    case 0: SPIS_PIPE(0); break;
+    case 1: SPIS_PIPE(1); break;
+    case 2: SPIS_PIPE(2); break;
+    case 3: SPIS_PIPE(3); break;
+    default: SPIS_PIPE(4); break;
+  }
+#undef SPIS_PIPE
+  return hipGetLastError();
+}
+
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev) {
+  if (A.blk_meta != nullptr)
+    return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
   if (A.swz)
     launch_k(spmv_dual_kernel<kDualCap, 1>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
              A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
@@ -252,9 +573,28 @@ hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b,
   return hipGetLastError();
 }
 
+// resident workgroups of the pipelined kernels (all of them fit at once: each walks its blocks)
+template <typename F>
+static int resident_grid(F kernel) {
+  int dev = 0, cus = 256, per = 1;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, 0) != hipSuccess || per < 1) per = 1;
+  const int t = (cus * per) & ~7;
+  return t < 8 ? 8 : (t > kSpmvGrid ? kSpmvGrid : t);
+}
+
+static int pipe_grid_max(int depth) {
+  static const int g1 = resident_grid(spmv_pipe_kernel<kDualCap, 4>);
+  static const int g2 = resident_grid(spmv_pipe2_kernel<kDualCap, 4>);
+  return depth == 2 ? g2 : g1;
+}
+
 int spmv_grid(const CsrView& A, bool fixed) {
-  if (fixed) return kSpmvGrid;
-  int g = A.n_blk < kSpmvGrid ? A.n_blk : kSpmvGrid;
+  // fixed (multi-GPU: partial arrays all-reduced element-wise) = the same count on every rank
+  if (fixed) return A.blk_meta != nullptr ? kPipeGridFixed : kSpmvGrid;
+  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth) : kSpmvGrid;
+  int g = A.n_blk < cap ? A.n_blk : cap;
+  if (A.blk_meta != nullptr && g > 8) g &= ~7;  // the XCD-local walk deals workgroups 8 at a time
   return g < 1 ? 1 : g;
 }
 
@@ -267,6 +607,8 @@ int blas_grid(int64_t n, bool fixed) {
 
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
                        double* partials, int grid, hipStream_t s, const LaunchEv* ev) {
+  if (A.blk_meta != nullptr)
+    return launch_spmv_pipe(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
   dim3 g(grid), b(kBlock);
   switch (epi) {
     case kEpiPlain:

@@ -125,6 +125,7 @@ struct spis_context {
   bool ell_gram = true;             // K7 on the sliced-ELL copy (SPIS_OPT_ELL_GRAM)
   bool mgs_chain = true;            // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN)
   bool overlap_gemv = true;         // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV)
+  int spmv_pipe = 2;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep
   hipStream_t stream2 = nullptr;
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
   uint64_t gemv_seq = 0;
@@ -158,6 +159,7 @@ struct spis_matrix {
   int32_t n_blk = 0, n_long = 0;
   int32_t* blk_row_d = nullptr;  // row blocks of <= kDualCap nnz / items for the fused dual SpMV
   int32_t n_blk_d = 0;
+  int2* blk_meta_d = nullptr;    // the same blocks as (row start, nz start): the pipelined kernels' table
   // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
@@ -170,7 +172,7 @@ struct spis_matrix {
   int32_t* send_idx = nullptr;
   double* send_buf = nullptr;
   CsrView view() const { return CsrView{n_rows, indptr, indices, vals, blk_row, n_blk}; }
-  CsrView dual_view() const { return CsrView{n_rows, indptr, indices, vals, blk_row_d, n_blk_d, false}; }
+  CsrView dual_view() const;
 };
 
 struct ConCache {
@@ -229,6 +231,17 @@ static void drop_graphs(spis_workspace* ws) {
 // helpers
 // ------------------------------------------------------------------------------------------------
 static bool fixed_grid(const spis_context* c) { return c->comm != nullptr; }
+
+// the solver's SpMV table: kDualCap row blocks, run by the pipelined kernels unless disabled
+CsrView spis_matrix::dual_view() const {
+  CsrView v{n_rows, indptr, indices, vals, blk_row_d, n_blk_d, false};
+  if (ctx->spmv_pipe > 0) {
+    v.blk_meta = blk_meta_d;
+    v.walk = (ctx->spmv_pipe & 1) == 0 ? 1 : 0;
+    v.depth = ctx->spmv_pipe >= 3 ? 2 : 1;
+  }
+  return v;
+}
 
 // ---- live kernel timing ------------------------------------------------------------------------
 static hipEvent_t prof_event(spis_context* c) {
@@ -540,6 +553,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_ELL_GRAM: c->ell_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN: c->mgs_chain = value != 0; return SPIS_OK;
       case SPIS_OPT_OVERLAP_GEMV: c->overlap_gemv = value != 0; return SPIS_OK;
+      case SPIS_OPT_SPMV_PIPE:
+        if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 4", (long long)value);
+        c->spmv_pipe = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
@@ -707,6 +724,10 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       M->n_blk_d = static_cast<int32_t>(blk.size()) - 1;
       HIP_TRY(hipMalloc(&M->blk_row_d, sizeof(int32_t) * blk.size()));
       HIP_TRY(hipMemcpy(M->blk_row_d, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+      std::vector<int2> meta(blk.size());
+      for (size_t i = 0; i < blk.size(); ++i) meta[i] = make_int2(blk[i], indptr[blk[i]]);
+      HIP_TRY(hipMalloc(&M->blk_meta_d, sizeof(int2) * meta.size()));
+      HIP_TRY(hipMemcpy(M->blk_meta_d, meta.data(), sizeof(int2) * meta.size(), hipMemcpyHostToDevice));
     }
     if (halo && halo->n_neighbors > 0) {
       M->n_ghost = n_ghost;
@@ -748,6 +769,7 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->vals);
     (void)hipFree(M->blk_row);
     (void)hipFree(M->blk_row_d);
+    (void)hipFree(M->blk_meta_d);
     if (M->ell_col) (void)hipFree(M->ell_col);
     if (M->ell_val) (void)hipFree(M->ell_val);
     if (M->ell_off) (void)hipFree(M->ell_off);
@@ -981,7 +1003,8 @@ extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) 
   ABI_GUARD({
     if (!c || !A || !x || !y) return fail(SPIS_ERR_ARG, "null argument");
     ST_TRY(exchange(c, A, x));
-    HIP_TRY(launch_spmv(A->view(), kEpiPlain, x, y, nullptr, nullptr, spmv_grid(A->view(), fixed_grid(c)), c->stream));
+    HIP_TRY(launch_spmv(A->dual_view(), kEpiPlain, x, y, nullptr, nullptr, spmv_grid(A->dual_view(), fixed_grid(c)),
+                        c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SPIS_OK;
   })
@@ -991,8 +1014,8 @@ extern "C" int spis_residual_norm(spis_context* c, spis_matrix* A, double* x, co
   ABI_GUARD({
     if (!c || !A || !x || !b || !out) return fail(SPIS_ERR_ARG, "null argument");
     ST_TRY(exchange(c, A, x));
-    const int g = spmv_grid(A->view(), fixed_grid(c));
-    HIP_TRY(launch_spmv(A->view(), kEpiResNorm, x, nullptr, b, c->partA, g, c->stream));
+    const int g = spmv_grid(A->dual_view(), fixed_grid(c));
+    HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, x, nullptr, b, c->partA, g, c->stream));
     ST_TRY(allreduce(c, c->partA, g));
     HIP_TRY(launch_finalize(c->partA, g, c->dscal, 1, c->stream));
     HIP_TRY(hipMemcpyAsync(out, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));

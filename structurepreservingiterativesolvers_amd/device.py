@@ -55,6 +55,7 @@ _OPTIONS = {
     "ell_gram": (_lib.OPT_ELL_GRAM, None),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, None),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, None),
+    "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}),
 }
 
 
@@ -69,6 +70,9 @@ def set_option(name, value, ctx=None):
     * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix;
     * ``mgs_chain`` (True): each Arnoldi step's MGS chain + normalise as one persistent launch;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
+    * ``spmv_pipe`` ("xcd"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of
+      the row blocks, "stride" pipelined grid-stride, "off" unpipelined (rows bit-identical in
+      every mode; reduction partials grouped per workgroup);
     * ``device_ilu`` ("auto"): how a SuperLU ``pre`` (``spilu``/``splu``) is applied — True on
       the device (K8), False by its host ``pre.solve`` through the callback (as the reference
       does), "auto" on the device when the plan's cost model predicts it is faster

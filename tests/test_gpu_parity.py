@@ -61,7 +61,7 @@ def _matrices():
     rng = np.random.default_rng(3)
     n = 6000
     lens = rng.integers(0, 30, size=n)
-    lens[[5, 100, 2500]] = [3000, 5000, 2049]  # long rows -> workgroup-wide reduction
+    lens[[5, 100, 2500, 4000]] = [3000, 5000, 2049, 1500]  # long rows -> workgroup-wide reduction
     lens[[7, 8, 9]] = 0  # empty rows
     indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
     indices = np.concatenate([np.sort(rng.choice(n, size=l, replace=False)) for l in lens]).astype(np.int32)
@@ -69,20 +69,58 @@ def _matrices():
     return out
 
 
-def test_spmv_bit_exact_vs_scipy(spis):
+@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd2", "stride2", "off"])
+def test_spmv_bit_exact_vs_scipy(spis, pipe):
+    """Every SpMV kernel (SPIS_OPT_SPMV_PIPE: pipelined XCD-local / grid-stride walk, unpipelined)
+    is bit-exact vs SciPy on rows that fit a row block (<= 1024 nnz: the solver's table); longer
+    rows take the workgroup-wide reduction (1e-12)."""
     from structurepreservingiterativesolvers_amd import primitives as P
+    from structurepreservingiterativesolvers_amd.device import set_option
 
     rng = np.random.default_rng(0)
-    for name, A in _matrices().items():
-        x = rng.normal(size=A.shape[1])
-        y = P.spmv(A, x)
-        yref = A @ x
-        long_rows = np.flatnonzero(np.diff(A.indptr) > 2048)
-        mask = np.ones(A.shape[0], dtype=bool)
-        mask[long_rows] = False
-        assert np.array_equal(y[mask], yref[mask]), name
-        if long_rows.size:
-            np.testing.assert_allclose(y[long_rows], yref[long_rows], rtol=1e-12)
+    set_option("spmv_pipe", pipe)
+    try:
+        for name, A in _matrices().items():
+            x = rng.normal(size=A.shape[1])
+            y = P.spmv(A, x)
+            yref = A @ x
+            long_rows = np.flatnonzero(np.diff(A.indptr) > 1024)
+            mask = np.ones(A.shape[0], dtype=bool)
+            mask[long_rows] = False
+            assert np.array_equal(y[mask], yref[mask]), name
+            if long_rows.size:
+                np.testing.assert_allclose(y[long_rows], yref[long_rows], rtol=1e-12)
+            r = P.residual_norm(A, x, yref + 1e-3)
+            np.testing.assert_allclose(r, np.linalg.norm(A @ x - (yref + 1e-3)), rtol=1e-12)
+    finally:
+        set_option("spmv_pipe", "xcd")
+
+
+def test_spmv_pipe_modes_solver_agree(spis):
+    """The solver with each SpMV kernel family: identical steps and branches, iterates equal at
+    roundoff (the modes group the residual / first-dot partial sums per workgroup differently)."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+    A, b = dic["A"], dic["b"]
+    runs = {}
+    try:
+        for pipe in ("off", "stride", "xcd", "stride2", "xcd2"):
+            set_option("spmv_pipe", pipe)
+            x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
+            runs[pipe] = (x, np.asarray(d["res"]), d["steps"], d["x"].trace)
+    finally:
+        set_option("spmv_pipe", "xcd")
+    x0, r0, s0, t0 = runs["off"]
+    for pipe in ("stride", "xcd", "stride2", "xcd2"):
+        x, r, st, tr = runs[pipe]
+        assert st == s0 and tr == t0, pipe
+        assert np.linalg.norm(x - x0) <= 1e-9 * np.linalg.norm(x0), pipe
+        np.testing.assert_allclose(r, r0, rtol=1e-6, atol=1e-12 * r0[0])
 
 
 def test_residual_norm_and_blas1(spis):

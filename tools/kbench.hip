@@ -567,6 +567,225 @@ int main(int argc, char** argv) {
     printf("%-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
            100.0 * bytes / (us * 1e-6) / 8e12);
   };
+  if (argc > 2 && std::string(argv[2]) == "pipe") {
+    // pipelined K1p / K1dp vs the current kernels: bit-identity check, then timings
+    std::vector<int32_t> blk;
+    blocks(n, rp.data(), kDualCap, 256, kDualCap, blk);
+    const int nb = static_cast<int>(blk.size()) - 1;
+    std::vector<int2> meta(nb + 1);
+    for (int i = 0; i <= nb; ++i) meta[i] = make_int2(blk[i], rp[blk[i]]);
+    int32_t* dblkd;
+    int2* dmeta;
+    CK(hipMalloc(&dblkd, 4 * blk.size()));
+    CK(hipMalloc(&dmeta, 8 * meta.size()));
+    CK(hipMemcpy(dblkd, blk.data(), 4 * blk.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dmeta, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice));
+    double *dx2, *dw, *dw2, *db, *pa, *pb, *pc, *pd;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&dw2, 8 * pitch));
+    CK(hipMalloc(&db, 8 * pitch));
+    for (double** p : {&pa, &pb, &pc, &pd}) CK(hipMalloc(p, 8 * 16384));
+    std::vector<double> h2(pitch);
+    for (int64_t i = 0; i < pitch; ++i) h2[i] = i < n ? 1e-3 * ((i * 104729) % 997) - 0.4 : 0.0;
+    CK(hipMemcpy(dx2, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CsrView A0{n, drp, dci, dva, dblkd, nb};
+    CsrView AP = A0;
+    AP.blk_meta = dmeta;
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    // bit identity (walk 0 groups partials exactly as the current kernel at the same grid)
+    {
+      const int g = 2048;
+      CK(launch_spmv_dual(A0, dx, db, pa, dx2, dw, dQ, pb, g, s));
+      CK(launch_spmv_dual(AP, dx, db, pc, dx2, dw2, dQ, pd, g, s));
+      CK(hipStreamSynchronize(s));
+      std::vector<double> w1(n), w2(n), a(g), b2(g), c(g), d(g);
+      CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(w2.data(), dw2, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(a.data(), pa, 8 * g, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b2.data(), pb, 8 * g, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(c.data(), pc, 8 * g, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(d.data(), pd, 8 * g, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+      int pbad = 0;
+      for (int i = 0; i < g; ++i) pbad += (a[i] != c[i]) + (b2[i] != d[i]);
+      printf("pipe dual vs dual: %lld rows differ, %d partials differ\n", (long long)bad, pbad);
+      CK(launch_spmv(A0, kEpiDot, dx, dw, dQ, pa, g, s));
+      CK(launch_spmv(AP, kEpiDot, dx, dw2, dQ, pc, g, s));
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(w2.data(), dw2, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(a.data(), pa, 8 * g, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(c.data(), pc, 8 * g, hipMemcpyDeviceToHost));
+      bad = 0;
+      for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+      pbad = 0;
+      for (int i = 0; i < g; ++i) pbad += a[i] != c[i];
+      printf("pipe K1 dot vs K1 dot: %lld rows differ, %d partials differ\n", (long long)bad, pbad);
+    }
+    char nm[128];
+    for (int g : {1024, 2048}) {
+      snprintf(nm, sizeof nm, "dual cur grid=%d", g);
+      timeit(nm, 50, SD, [&] { (void)launch_spmv_dual(A0, dx, db, pa, dx2, dw, dQ, pb, g, s); });
+    }
+    for (int walk : {0, 1})
+      for (int g : {1024, 1280, 1536, 2048, 2560, 4096, 8192}) {
+        AP.walk = walk;
+        snprintf(nm, sizeof nm, "dual pipe walk=%d grid=%d", walk, g);
+        timeit(nm, 50, SD, [&] { (void)launch_spmv_dual(AP, dx, db, pa, dx2, dw, dQ, pb, g, s); });
+      }
+    {
+      AP.walk = 1;
+      const int2* mt = dmeta;
+#define VAR(NAME, CAPV, NTV, WPEV, G)                                                                         \
+  snprintf(nm, sizeof nm, "dual pipe walk=1 %s grid=%d", NAME, G);                                            \
+  timeit(nm, 50, SD, [&] {                                                                                    \
+    hipLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, drp, dci, dva, mt, \
+                       nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);                                  \
+  })
+      VAR("nt", 1024, true, 1, 1280);
+      for (int g : {768, 1024, 1280, 2048}) {
+        snprintf(nm, sizeof nm, "dual pipe2 walk=1 grid=%d", g);
+        timeit(nm, 50, SD, [&] {
+          hipLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                             nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+        });
+        snprintf(nm, sizeof nm, "K1 dot pipe2 walk=1 grid=%d", g);
+        timeit(nm, 50, S, [&] {
+          hipLaunchKernelGGL((spmv_pipe2_kernel<1024, 1>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                             nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);
+        });
+      }
+      {  // pipe2 bit identity vs pipe at the same grid / walk
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+        hipLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pc, dx2, dQ, dw2, pd);
+        CK(hipStreamSynchronize(s));
+        std::vector<double> w1(n), w2(n), a(4096), c(4096);
+        CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(w2.data(), dw2, 8 * n, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(a.data(), pa, 8 * 1024, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(c.data(), pc, 8 * 1024, hipMemcpyDeviceToHost));
+        int64_t bad = 0;
+        for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+        int pbad = 0;
+        for (int i = 0; i < 1024; ++i) pbad += a[i] != c[i];
+        printf("pipe2 vs pipe: %lld rows differ, %d partials differ\n", (long long)bad, pbad);
+      }
+      {  // cold: 1 GiB of reads evict L2 and the 256 MB Infinity Cache before every launch (as the
+         // MGS chain and GEMV between two dual SpMVs do in the solver); kernel time from the
+         // dispatch's own events
+        const int64_t big = int64_t(1) << 26;  // doubles per buffer (512 MiB)
+        double *bx, *by;
+        CK(hipMalloc(&bx, 8 * big));
+        CK(hipMalloc(&by, 8 * big));
+        CK(hipMemset(bx, 0, 8 * big));
+        CK(hipMemset(by, 0, 8 * big));
+        CK(hipStreamSynchronize(s));
+        auto cold = [&](const char* name, double bytes, auto&& launch) {
+          double tot = 0;
+          const int reps = 20;
+          for (int r = 0; r < reps + 2; ++r) {
+            hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                               reinterpret_cast<const double2*>(bx), pd + 8192);
+            hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                               reinterpret_cast<const double2*>(by), pd + 8192);
+            launch();
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) tot += ms;
+          }
+          const double us = 1e3 * tot / reps;
+          printf("COLD %-39s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
+                 100.0 * bytes / (us * 1e-6) / 8e12);
+        };
+        cold("dual cur grid=2048", SD, [&] {
+          hipExtLaunchKernelGGL((spmv_dual_kernel<1024, 0>), dim3(2048), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva,
+                                dblkd, nb, dx, db, pa, dx2, dw, dQ, pb);
+        });
+        for (int g : {1024, 1280, 2560}) {
+          snprintf(nm, sizeof nm, "dual pipe walk=1 grid=%d", g);
+          cold(nm, SD, [&] {
+            hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
+                                  dci, dva, mt, nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+          });
+        }
+        for (int g : {768, 1024, 2048}) {
+          snprintf(nm, sizeof nm, "dual pipe2 walk=1 grid=%d", g);
+          cold(nm, SD, [&] {
+            hipExtLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva,
+                                  mt, nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+          });
+          snprintf(nm, sizeof nm, "dual pipe2 walk=0 grid=%d", g);
+          cold(nm, SD, [&] {
+            hipExtLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva,
+                                  mt, nb, 0, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+          });
+        }
+        for (double mb : {150.0, 170.0, 186.0}) {
+          const int64_t m2 = static_cast<int64_t>(mb * 1e6 / 16);
+          snprintf(nm, sizeof nm, "plain read %.0f MB", mb);
+          cold(nm, 16.0 * m2, [&] {
+            hipExtLaunchKernelGGL(read2_kernel, dim3(2048), dim3(kBlock), 0, s, e0, e1, 0, m2,
+                                  reinterpret_cast<const double2*>(bx + (big >> 1)), pd + 8192);
+          });
+        }
+        for (int g : {1024, 1280}) {
+          snprintf(nm, sizeof nm, "K1 dot pipe walk=1 grid=%d", g);
+          cold(nm, S, [&] {
+            hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
+                                  dci, dva, mt, nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);
+          });
+          snprintf(nm, sizeof nm, "K1 dot pipe2 walk=1 grid=%d", g);
+          cold(nm, S, [&] {
+            hipExtLaunchKernelGGL((spmv_pipe2_kernel<1024, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva,
+                                  mt, nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);
+          });
+        }
+        CK(hipFree(bx));
+        CK(hipFree(by));
+      }
+      snprintf(nm, sizeof nm, "dual pipe walk=1 x2=x1 grid=1280");
+      timeit(nm, 50, SD, [&] {
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+      });
+      snprintf(nm, sizeof nm, "dual pipe walk=1 q0=b grid=1280");
+      timeit(nm, 50, SD, [&] {
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pa, dx2, db, dw, pb);
+      });
+      snprintf(nm, sizeof nm, "single pipe walk=1 ResNorm grid=1280");
+      timeit(nm, 50, S, [&] {
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+      });
+      snprintf(nm, sizeof nm, "2x single pipe walk=1 (ResNorm + Dot) grid=1280");
+      timeit(nm, 50, SD, [&] {
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+                           nb, 1, dx2, dQ, dw, pb, dx, dQ, dw, pb);
+      });
+#undef VAR
+    }
+    AP.walk = 0;
+    for (int g : {2048}) {
+      snprintf(nm, sizeof nm, "K1 dot cur cap1024 grid=%d", g);
+      timeit(nm, 50, S, [&] { (void)launch_spmv(A0, kEpiDot, dx, dw, dQ, pa, g, s); });
+    }
+    for (int walk : {0, 1})
+      for (int g : {1024, 1280, 2048, 4096}) {
+        AP.walk = walk;
+        snprintf(nm, sizeof nm, "K1 dot pipe walk=%d grid=%d", walk, g);
+        timeit(nm, 50, S, [&] { (void)launch_spmv(AP, kEpiDot, dx, dw, dQ, pa, g, s); });
+      }
+    return 0;
+  }
   // ---- SpMV
   for (int cap : {1024, 2048}) {
     std::vector<int32_t> blk;
