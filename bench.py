@@ -237,15 +237,19 @@ def main():
     # the committed PMC summaries were measured on the C3 matrix: reported for that workload only
     c3 = args.config == "c3" and args.M in (None, 289)
     fused = cnt[_lib.PROF_SPMV_DUAL] > 0
-    traffic = load_traffic("spmv_dual_traffic.json" if fused else "spmv_traffic.json") if c3 else None
+    # the PMC summaries were measured on the default kernels (pipelined, XCD-local walk)
+    traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and args.spmv_pipe == "xcd" else None
+    kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<1024, 4> (grid-stride walk)",
+             "xcd": "spmv_pipe_kernel<1024, 4> (XCD-local walk)", "stride2": "spmv_pipe2_kernel<1024, 4>",
+             "xcd2": "spmv_pipe2_kernel<1024, 4> (XCD-local walk)"}[args.spmv_pipe]
     if fused:  # the dominant SpMV launch: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
-        roof = {"kernel": "spmv_dual_kernel (true-residual SpMV of x_j, solvers.py:290, fused with the "
-                          "Arnoldi SpMV of z_{j+2}, :191; matrix read once)",
+        roof = {"kernel": kname + ": true-residual SpMV of x_j, solvers.py:290, fused with the "
+                          "Arnoldi SpMV of z_{j+2}, :191; matrix read once",
                 "bound": "hbm", "achieved": dual_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dual_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": SD,
                 "avg_launch_us": 1e3 * dual_ms, "launches": int(cnt[_lib.PROF_SPMV_DUAL])}
     else:
-        roof = {"kernel": "spmv_rowblock_kernel<kEpiDot> (Arnoldi SpMV, solvers.py:191)",
+        roof = {"kernel": kname.replace("dual", "rowblock").replace(", 4>", ", 1>") + ": Arnoldi SpMV, solvers.py:191",
                 "bound": "hbm", "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": spmv_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": S,
                 "avg_launch_us": 1e3 * spmv_ms, "launches": int(cnt[_lib.PROF_SPMV])}
@@ -275,6 +279,7 @@ def main():
         "roofline": roof,
         "kernels": {
             "spmv_arnoldi_us": 1e3 * spmv_ms,
+            "spmv_arnoldi_GBs": spmv_gbs,
             "spmv_dual_us": 1e3 * dual_ms,
             "spmv_dual_GBs": dual_gbs,
             "spmv_residual_us": 1e3 * res_ms,

@@ -117,6 +117,7 @@ struct spis_context {
   bool prof = false;
   int prof_period = 1;            // time every prof_period-th Arnoldi iteration
   int prof_iter = 0;              // iteration counter for the sampling
+  int prof_phase = 0;             // advanced per solve: the sampled iterations rotate through every position
   bool force_generic_gram = false;  // tests: take the MZ + tiled-Gram path
   bool fuse_spmv = true;            // residual SpMV of U_j + Arnoldi SpMV of A_{j+2} in one launch
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
@@ -262,7 +263,7 @@ struct ProfEv {
   int kind;
   hipEvent_t a = nullptr, b = nullptr;
   ProfEv(spis_context* c_, int kind_) : c(c_), kind(kind_) {
-    if (c->prof && (c->prof_iter % c->prof_period) == 0) {
+    if (c->prof && ((c->prof_iter + c->prof_phase) % c->prof_period) == 0) {
       a = prof_event(c);
       b = prof_event(c);
     }
@@ -574,6 +575,7 @@ extern "C" int spis_profile_enable(spis_context* c, int32_t on) {
     c->prof = on > 0;
     c->prof_period = on > 0 ? on : 1;
     c->prof_iter = 0;
+    c->prof_phase = 0;
     c->force_generic_gram = on < 0;  // (negative: test hook selecting the generic Gram path)
     for (int i = 0; i < SPIS_PROF_KINDS; ++i) {
       c->prof_ms[i] = 0.0;
@@ -1672,7 +1674,8 @@ struct Solver {
     }
     ST_TRY(arnoldi_pre(ja));
     if (!c->comm) next_seq(j);
-    const bool sampled = c->prof && ((j % c->prof_period) == 0 || (ja % c->prof_period) == 0);
+    const bool sampled =
+        c->prof && (((j + c->prof_phase) % c->prof_period) == 0 || ((ja + c->prof_phase) % c->prof_period) == 0);
     if (graphable() && !sampled) {
       hipGraphExec_t ge = nullptr;
       ST_TRY(arn_graph(ja, &ge));
@@ -1726,6 +1729,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     if (!out->res_host || !out->y_host || !out->branch_host || !out->events_host || !out->msg_host)
       return fail(SPIS_ERR_ARG, "output arrays missing");
     const int64_t n = A->n_rows;
+    if (c->prof) ++c->prof_phase;
     if (o->pre_matrix && o->pre_matrix->n_rows != n) return fail(SPIS_ERR_ARG, "preconditioner size mismatch");
     if (o->pre_ilu && o->pre_ilu->n != n) return fail(SPIS_ERR_ARG, "ILU preconditioner size mismatch");
     if (o->pre_ilu && c->comm) return fail(SPIS_ERR_ARG, "the device ILU preconditioner is single-GPU");

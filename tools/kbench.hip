@@ -543,6 +543,26 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((spmv_dual_kernel<1024, 2>), dim3(gd), dim3(kBlock), 0, s, drp, dci, dva, dblkd, nbd, dx, dy,
                            dpr, dx2, dw, dQ, dpart);
       CK(hipStreamSynchronize(s));
+      // the solver's pipelined dual (XCD-local walk, 1280 workgroups): 5 back to back ("warm"),
+      // then 5 each behind 1 GiB of reads that evict L2 and the Infinity Cache ("cold")
+      std::vector<int2> meta(blkd.size());
+      for (size_t i = 0; i < blkd.size(); ++i) meta[i] = make_int2(blkd[i], rp[blkd[i]]);
+      int2* dmeta;
+      CK(hipMalloc(&dmeta, 8 * meta.size()));
+      CK(hipMemcpy(dmeta, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice));
+      const int64_t big = int64_t(1) << 27;
+      double* bx;
+      CK(hipMalloc(&bx, 8 * big));
+      CK(hipMemset(bx, 0, 8 * big));
+      for (int i = 0; i < 10; ++i) {
+        if (i >= 5)
+          hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
+                             dpr + 4096);
+        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, dmeta,
+                           nbd, 1, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+      }
+      CK(hipStreamSynchronize(s));
+      CK(hipFree(bx));
     }
     for (int i = 0; i < 5; ++i)
       hipLaunchKernelGGL((spmv_v1<kEpiDot, 8, 1, false>), dim3(g), dim3(kBlock), 0, s, drp, dci, dva, dblk, nb, dx, dy, dQ, dpart);
