@@ -153,6 +153,11 @@ def main():
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
     ap.add_argument("--no-overlap", action="store_true", help="update GEMV on the main stream (no side stream)")
+    ap.add_argument("--gemv-sync", type=int, default=1, choices=[1, 2],
+                    help="how the dual SpMV waits for the side-stream GEMV (SPIS_OPT_OVERLAP_GEMV): "
+                         "1 stream write/wait on a device word, 2 the GEMV launch's completion event")
+    ap.add_argument("--gram", default="ell", choices=["staged", "ell", "csr"],
+                    help="constraint-Gram matrix form (SPIS_OPT_ELL_GRAM)")
     ap.add_argument("--spmv-pipe", default="xcd", choices=["off", "stride", "xcd", "stride2", "xcd2"],
                     help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
                          "pipelined XCD-local walk")
@@ -184,9 +189,11 @@ def main():
     conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1 if args.graphs else 0), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 0 if args.no_fuse else 1), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 0 if args.no_overlap else 1),
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 0 if args.no_overlap else args.gemv_sync),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
+               "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}[args.spmv_pipe]),
                "spis_set_option")

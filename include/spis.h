@@ -126,14 +126,19 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   1 = CGS2, classical Gram-Schmidt with one re-orthogonalisation pass (3 reductions per
  *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
  *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only.
- * SPIS_OPT_ELL_GRAM (default 1): the fused constraint reduction (p + 1 <= 32) reads a sliced-ELL
- *   copy of each constraint matrix, built once on first use (static row boundaries).
+ * SPIS_OPT_ELL_GRAM (default 1): how the fused constraint reduction (p + 1 <= 32) reads each
+ *   constraint matrix, from a copy built once on first use: 1 = sliced ELL (static row
+ *   boundaries), 2 = row chunks with their distinct columns (the basis rows of those columns
+ *   staged in LDS once per chunk; a matrix with a row of > 64 entries or > 176 distinct columns
+ *   falls back to 1; measured 12% slower than 1 at C3), 0 = the CSR itself.
  * SPIS_OPT_MGS_CHAIN (default 1): each Arnoldi step's MGS chain + normalise runs as one persistent
  *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 0 = one
  *   launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
  *   so results differ from the per-step launches at roundoff level.
  * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
  *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
+ *   The dual SpMV waits for it through a stream write / wait on a device word (1) or through the
+ *   GEMV launch's own completion event (2; measured equal end to end); 0 = main stream.
  * SPIS_OPT_SPMV_PIPE (default 2): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
  *   software-pipelined row-block kernels; 2 = each XCD's workgroups walk a contiguous eighth of
  *   the row blocks (its share of the gathered vectors stays in its own L2), 1 = grid-stride walk,

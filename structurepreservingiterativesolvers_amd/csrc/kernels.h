@@ -137,6 +137,30 @@ struct EllView {
 };
 constexpr int kEllRows = 16;
 
+// K7s: row chunks of a constraint matrix with the sorted distinct columns they touch (the chunk's
+// own rows included): the Ut rows of those columns are staged in LDS once per chunk, so each
+// nonzero reads its Ut row from LDS instead of gathering it from L2.  A chunk holds <= kStgRows
+// rows as 16-row slices in ELL order (entry (slice s, t, row i) at slice base + 16 t + i, padded
+// with zeros), <= kStgNz entries and <= kStgUmax distinct columns.
+constexpr int kStgRows = 64;
+constexpr int kStgNz = 1024;
+constexpr int kStgUmax = 176;
+struct StgView {
+  const int32_t* row;      // [nch + 1] first row of each chunk
+  const int32_t* uoff;     // [nch + 1] offsets into uniq
+  const int32_t* uniq;     // distinct columns per chunk, ascending
+  const int32_t* eoff;     // [nch + 1] offsets into loc / val
+  const int32_t* width;    // [4 nch] entries per row of each of the chunk's (up to 4) slices
+  const uint16_t* loc;     // per entry: its column's index in the chunk's uniq list
+  const double* val;       // per entry: the value (0 in padding)
+  const uint16_t* rowloc;  // per row: the row's own index in its chunk's uniq list
+  int32_t nch;
+};
+// K7s launch (np1 <= 32): M's StgView; Ut as for K7
+hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, const double* Ut,
+                                      int nvv, const double* const* v, double* partials, double* G,
+                                      hipStream_t s);
+
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
                                   const double* const* v, double* partials, double* G, hipStream_t s,
                                   const EllView* ell = nullptr);

@@ -1617,6 +1617,9 @@ hipError_t launch_gram(int64_t n, int nu, const double* const* U, int nv, const 
 //     sums the block partials in block order (deterministic).  G = U^T M U gives term2 = G[:p,:p]/2, x0'MZ = G[p,:p],
 //     x0'Mx0 = G[p,p]; Gv gives v'Z and v.x0.
 // ---------------------------------------------------------------------------------------------
+// Ut row stride: 32 doubles (256 B, 16-B aligned rows) for np1 <= 32, else 64; zero padded
+__host__ __device__ __forceinline__ int ut_ld(int np1) { return np1 <= 32 ? 32 : 64; }
+
 __global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int p,
                                                                  const double* __restrict__ Z,
                                                                  int64_t pitch,
@@ -1631,10 +1634,11 @@ __global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int 
     if (r < rows) tile[a * 65 + r] = a < p ? Z[a * pitch + r0 + r] : x0[r0 + r];
   }
   __syncthreads();
-  double* out = Ut + r0 * np1;
-  for (int idx = threadIdx.x; idx < rows * np1; idx += kBlock) {
-    const int r = idx / np1, a = idx - (idx / np1) * np1;
-    out[idx] = tile[a * 65 + r];
+  const int ld = ut_ld(np1);
+  double* out = Ut + r0 * ld;
+  for (int idx = threadIdx.x; idx < rows * ld; idx += kBlock) {
+    const int r = idx / ld, a = idx - (idx / ld) * ld;
+    out[idx] = a < np1 ? tile[a * 65 + r] : 0.0;
   }
 }
 
@@ -1732,7 +1736,7 @@ __global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kern
     // rows of U for the update (unconditional, clamped: in flight during the gathers)
     double u[kConRows];
 #pragma unroll
-    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * np1 + lac];
+    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * ut_ld(np1) + lac];
     double vc[4] = {0.0, 0.0, 0.0, 0.0};
     if (lane < nr) {
       if (nvv > 0) vc[0] = v0[r0 + lane];
@@ -1767,7 +1771,7 @@ __global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kern
           for (int q = 0; q < kConBatch; ++q) {
             const int t = tb + P * q + h;
             const int col = sc[t < wl ? t : 0];
-            g[q] = Ut[static_cast<int64_t>(col) * np1 + lac];  // valid address for every lane
+            g[q] = Ut[static_cast<int64_t>(col) * ut_ld(np1) + lac];  // valid address for every lane
           }
 #pragma unroll
           for (int q = 0; q < kConBatch; ++q) {
@@ -1879,7 +1883,7 @@ __global__ __launch_bounds__(kBlock, 3) void constraint_gram_ell_kernel(
     const int64_t cg = r0 / kConRows;  // global slice index (g0 is a multiple of 16)
     double u[kConRows];
 #pragma unroll
-    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * np1 + lac];
+    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * ut_ld(np1) + lac];
     double vc[4] = {0.0, 0.0, 0.0, 0.0};
     if (lane < nr) {
       if (nvv > 0) vc[0] = v0[r0 + lane];
@@ -1912,7 +1916,7 @@ __global__ __launch_bounds__(kBlock, 3) void constraint_gram_ell_kernel(
           double g[kConRows / 2];
 #pragma unroll
           for (int r = 0; r < kConRows / 2; ++r)
-            g[r] = Ut[static_cast<int64_t>(sc[t * kConRows + 2 * r + h]) * np1 + lac];
+            g[r] = Ut[static_cast<int64_t>(sc[t * kConRows + 2 * r + h]) * ut_ld(np1) + lac];
 #pragma unroll
           for (int r = 0; r < kConRows / 2; ++r) wr[r] += sv[t * kConRows + 2 * r + h] * g[r];
         }
@@ -1967,6 +1971,203 @@ __global__ __launch_bounds__(kBlock, 3) void constraint_gram_ell_kernel(
       out[idx] = s_acc[a * (SEG + 4) + SEG + c];
     }
   }
+}
+
+// K7s: chunk-staged constraint Gram (p + 1 <= 32), software-pipelined over the chunks of a
+// workgroup.  Per chunk (<= 64 rows = <= 4 slices of 16):
+//   A. the registers holding the chunk (its distinct columns' Ut rows, its ELL entries, row
+//      locations, linear-term values) go to LDS; the next chunk's column list (loaded a round
+//      earlier) goes to the second column-list buffer;  barrier;
+//   B. the next chunk's loads are issued into registers (they stay in flight through C);
+//   C. wave w takes slice w: lane (a, h) accumulates w_r[a] = sum_t val * U[loc][a] for its 8
+//      rows r = 2i + h of the slice (8 independent chains, LDS operands only), the rows' w go to
+//      the wave's W tile, then K7's rank-16 update G[a][b] += U_r[a] W[r][b] and linear terms.
+// Chunks of XCD group g (blockIdx % 8) are a contiguous eighth of the chunk list, dealt
+// round-robin to its workgroups (speed only: chunk -> workgroup is a fixed function of the grid
+// and chunk count, so the partial sums are deterministic).
+template <int RU>
+__global__ __launch_bounds__(kBlock, 2) void constraint_gram_stg_kernel(
+    int np1, StgView S, const double* __restrict__ Ut, int nvv, const double* __restrict__ v0,
+    const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ v3,
+    double* __restrict__ partials) {
+  constexpr int NP = 32, SEG = 16, NW = kBlock / 64;
+  constexpr int kQ = kStgUmax * NP / 2 / kBlock;  // staged Ut double2 per thread (11)
+  constexpr int kE = kStgNz / kBlock;         // staged entries per thread (4)
+  __shared__ __attribute__((aligned(16))) double s_u[kStgUmax * NP];
+  __shared__ double s_val[kStgNz];
+  __shared__ uint16_t s_loc[kStgNz];
+  __shared__ uint16_t s_rl[kStgRows];
+  __shared__ double s_v[4][kStgRows];
+  __shared__ int s_uq[2][kStgUmax];
+  __shared__ __attribute__((aligned(16))) double s_w[NW][16][NP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int la = lane % NP;
+  const int h = lane / NP;
+  const bool on = la < np1;
+  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int grp = blockIdx.x % ngrp;
+  const int cs = static_cast<int>(gridDim.x) / ngrp;
+  const int cb = static_cast<int>((static_cast<int64_t>(S.nch) * grp) / ngrp) + static_cast<int>(blockIdx.x) / ngrp;
+  const int ce = static_cast<int>((static_cast<int64_t>(S.nch) * (grp + 1)) / ngrp);
+  double acc[SEG];
+#pragma unroll
+  for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
+  double gv[4] = {0.0, 0.0, 0.0, 0.0};
+  // staged registers of the next chunk
+  double2 ru[kQ];
+  double rv[kE];
+  uint16_t rloc[kE];
+  uint16_t rrl = 0;
+  double rvc[4] = {0.0, 0.0, 0.0, 0.0};
+  int ruq = 0;  // the column list one chunk further ahead
+  auto load_uq = [&](int ch) {
+    if (ch < ce) {
+      const int u0 = S.uoff[ch], nu = S.uoff[ch + 1] - u0;
+      if (tid < nu) ruq = S.uniq[u0 + tid];
+    }
+  };
+  auto stage = [&](int ch, int buf) {  // loads only: values land in registers
+    const int row0 = S.row[ch], nr = S.row[ch + 1] - row0;
+    const int nu = S.uoff[ch + 1] - S.uoff[ch];
+    const int e0 = S.eoff[ch], ne = S.eoff[ch + 1] - e0;
+    const int* uq = s_uq[buf];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {  // 16 lanes per 256-B Ut row (zero padded beyond np1)
+      const int idx = tid + q * kBlock;
+      const int t = idx >> 4, a = 2 * (idx & 15);
+      ru[q] = t < nu ? *reinterpret_cast<const double2*>(Ut + static_cast<int64_t>(uq[t]) * NP + a)
+                     : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int q = 0; q < kE; ++q) {
+      const int e = tid + q * kBlock;
+      rv[q] = e < ne ? S.val[e0 + e] : 0.0;
+      rloc[q] = e < ne ? S.loc[e0 + e] : 0;
+    }
+    if (tid < nr) {
+      rrl = S.rowloc[row0 + tid];
+      if (nvv > 0) rvc[0] = v0[row0 + tid];
+      if (nvv > 1) rvc[1] = v1[row0 + tid];
+      if (nvv > 2) rvc[2] = v2[row0 + tid];
+      if (nvv > 3) rvc[3] = v3[row0 + tid];
+    }
+  };
+  int buf = 0;
+  if (cb < ce) {
+    load_uq(cb);
+    if (tid < kStgUmax) s_uq[0][tid] = ruq;
+    __syncthreads();
+    stage(cb, 0);
+    load_uq(cb + cs);
+  }
+  for (int ch = cb; ch < ce; ch += cs) {
+    const int row0 = S.row[ch], nr = S.row[ch + 1] - row0;
+    // A: this chunk's registers -> LDS; the next chunk's column list -> the other buffer
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) reinterpret_cast<double2*>(s_u)[tid + q * kBlock] = ru[q];
+#pragma unroll
+    for (int q = 0; q < kE; ++q) {
+      s_val[tid + q * kBlock] = rv[q];
+      s_loc[tid + q * kBlock] = rloc[q];
+    }
+    if (tid < kStgRows) {
+      s_rl[tid] = rrl;
+      s_v[0][tid] = rvc[0];
+      s_v[1][tid] = rvc[1];
+      s_v[2][tid] = rvc[2];
+      s_v[3][tid] = rvc[3];
+    }
+    if (tid < kStgUmax) s_uq[buf ^ 1][tid] = ruq;
+    __syncthreads();
+    // B: the next chunk's loads (in flight through C), and the column list after it
+    if (ch + cs < ce) {
+      stage(ch + cs, buf ^ 1);
+      load_uq(ch + 2 * cs);
+    }
+    // C: slice wid of this chunk
+    const int ns = (nr + 15) >> 4;
+    if (wid < ns) {
+      int sb = 0;
+      for (int s2 = 0; s2 < wid; ++s2) sb += 16 * S.width[4 * ch + s2];
+      const int width = S.width[4 * ch + wid];
+      double wr[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wr[i] = 0.0;
+      for (int t = 0; t < width; ++t) {
+        const int eb = sb + 16 * t + h;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wr[i] += s_val[eb + 2 * i] * s_u[s_loc[eb + 2 * i] * NP + la];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s_w[wid][2 * i + h][la] = on ? wr[i] : 0.0;
+      __builtin_amdgcn_wave_barrier();
+      const int rows = nr - 16 * wid < 16 ? nr - 16 * wid : 16;
+#pragma unroll RU
+      for (int ii = 0; ii < 16; ++ii) {
+        const bool rv_ok = ii < rows;
+        const int i = 16 * wid + ii;
+        const double ui = (on && rv_ok) ? s_u[s_rl[i] * NP + la] : 0.0;
+        const double2* wrow = reinterpret_cast<const double2*>(&s_w[wid][ii][SEG * h]);
+#pragma unroll
+        for (int j = 0; j < SEG; j += 2) {
+          const double2 x2 = wrow[j >> 1];
+          acc[j] += ui * x2.x;
+          acc[j + 1] += ui * x2.y;
+        }
+        if (h == 0 && rv_ok) {
+          if (nvv > 0) gv[0] += ui * s_v[0][i];
+          if (nvv > 1) gv[1] += ui * s_v[1][i];
+          if (nvv > 2) gv[2] += ui * s_v[2][i];
+          if (nvv > 3) gv[3] += ui * s_v[3][i];
+        }
+      }
+    }
+    buf ^= 1;
+    __syncthreads();
+  }
+  // combine the block's waves in wave order through LDS (s_u reused), one partial per block
+  double* s_acc = s_u;  // 64 x (SEG + 4) doubles
+  for (int w = 0; w < NW; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) s_acc[lane * (SEG + 4) + j] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + j]) + acc[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        s_acc[lane * (SEG + 4) + SEG + c] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + SEG + c]) + gv[c];
+    }
+    __syncthreads();
+  }
+  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
+  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
+  for (int idx = tid; idx < stride; idx += kBlock) {
+    if (idx < np1 * np1) {
+      const int a = idx / np1, b = idx - (idx / np1) * np1;
+      out[idx] = s_acc[(a + NP * (b / SEG)) * (SEG + 4) + (b % SEG)];
+    } else {
+      const int k2 = idx - np1 * np1;
+      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
+      out[idx] = s_acc[a * (SEG + 4) + SEG + c];
+    }
+  }
+}
+
+hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, const double* Ut, int nvv,
+                                      const double* const* v, double* partials, double* G, hipStream_t s) {
+  (void)n;
+  if (np1 > 32 || nvv > 4) return hipErrorInvalidValue;
+  const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int c = 0; c < nvv; ++c) vv[c] = v[c];
+  const int grid = 256 * 2;  // resident: 2 workgroups per CU (LDS-bound), a multiple of 8
+  // (rank-update unroll 2 measured equal: 1)
+  hipLaunchKernelGGL(constraint_gram_stg_kernel<1>, dim3(grid), dim3(kBlock), 0, s, np1, S, Ut, nvv, vv[0], vv[1],
+                     vv[2], vv[3], partials);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int npairs = np1 * np1 + nvv * np1;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs, grid, partials, G);
+  return hipGetLastError();
 }
 
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,

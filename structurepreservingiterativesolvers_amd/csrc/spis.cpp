@@ -123,9 +123,13 @@ struct spis_context {
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
-  bool ell_gram = true;             // K7 on the sliced-ELL copy (SPIS_OPT_ELL_GRAM)
+  int ell_gram = 1;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy (SPIS_OPT_ELL_GRAM)
   bool mgs_chain = true;            // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN)
-  bool overlap_gemv = true;         // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV)
+  // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
+  // waits for it through 1 a stream write / wait on a device word, 2 the GEMV launch's own
+  // completion event (hipStreamWaitEvent: no blit kernels)
+  int overlap_gemv = 1;
+  hipEvent_t ev_gemv = nullptr;
   int spmv_pipe = 2;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep
   hipStream_t stream2 = nullptr;
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
@@ -165,6 +169,12 @@ struct spis_matrix {
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
   int64_t* ell_off = nullptr;
+  // chunk-staged copy for K7s (built on first use; stg_state -1 unknown, 0 not stageable, 1 built)
+  int stg_state = -1;
+  int32_t *stg_row = nullptr, *stg_uoff = nullptr, *stg_uniq = nullptr, *stg_eoff = nullptr, *stg_width = nullptr;
+  uint16_t *stg_loc = nullptr, *stg_rowloc = nullptr;
+  double* stg_val = nullptr;
+  int32_t stg_nch = 0;
   bool all_zero = false;
   // halo plan
   int32_t n_ghost = 0;
@@ -460,6 +470,7 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_gemv, hipEventDisableTiming | hipEventReleaseToDevice));
     *out = c.release();
     return SPIS_OK;
   })
@@ -520,7 +531,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->stream2);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram})
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_gemv})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
@@ -551,9 +562,15 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_FUSE_SPMV: c->fuse_spmv = value != 0; return SPIS_OK;
       case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
-      case SPIS_OPT_ELL_GRAM: c->ell_gram = value != 0; return SPIS_OK;
+      case SPIS_OPT_ELL_GRAM:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "ell gram %lld: 0, 1 or 2", (long long)value);
+        c->ell_gram = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN: c->mgs_chain = value != 0; return SPIS_OK;
-      case SPIS_OPT_OVERLAP_GEMV: c->overlap_gemv = value != 0; return SPIS_OK;
+      case SPIS_OPT_OVERLAP_GEMV:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "overlap gemv %lld: 0, 1 or 2", (long long)value);
+        c->overlap_gemv = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
         if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 4", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
@@ -775,6 +792,10 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     if (M->ell_col) (void)hipFree(M->ell_col);
     if (M->ell_val) (void)hipFree(M->ell_val);
     if (M->ell_off) (void)hipFree(M->ell_off);
+    for (void* p : {static_cast<void*>(M->stg_row), static_cast<void*>(M->stg_uoff), static_cast<void*>(M->stg_uniq),
+                    static_cast<void*>(M->stg_eoff), static_cast<void*>(M->stg_width), static_cast<void*>(M->stg_loc),
+                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc)})
+      if (p) (void)hipFree(p);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
     delete M;
@@ -1146,6 +1167,124 @@ static int ensure_ell(spis_context* c, spis_matrix* M, EllView* out) {
   return SPIS_OK;
 }
 
+// One-time chunking of a constraint matrix for K7s: greedy row chunks of <= kStgRows rows,
+// <= kStgNz ELL entries (16-row slices, each padded to its longest row) and <= kStgUmax distinct
+// columns (the chunk's own rows counted as columns: the rank-1 update reads U_r from the same LDS
+// image).  *ok = false if a single row does not fit (the ELL / CSR kernels then serve the matrix).
+static int ensure_stg(spis_context* c, spis_matrix* M, StgView* out, bool* ok) {
+  if (M->stg_state < 0) {
+    const int64_t n = M->n_rows, nnz = M->nnz;
+    std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
+    std::vector<double> va(std::max<int64_t>(nnz, 1));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+    if (nnz > 0) {
+      HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+    }
+    std::vector<int32_t> mark(static_cast<size_t>(std::max<int64_t>(M->n_cols, n)), -1), pos(mark.size(), 0);
+    std::vector<int32_t> row{0}, uoff{0}, uniq, eoff{0}, width;
+    std::vector<uint16_t> eloc, rowloc(std::max<int64_t>(n, 1));
+    std::vector<double> evals;
+    std::vector<int32_t> cur;  // the open chunk's distinct columns
+    int64_t slice_max[kStgRows / 16] = {0, 0, 0, 0};
+    int64_t padded = 0;  // the open chunk's ELL entries
+    bool good = true;
+    int32_t chunk = 0;
+    int64_t r0 = 0;
+    auto close = [&](int64_t r1) {  // sort the chunk's columns, then its ELL slices
+      std::sort(cur.begin(), cur.end());
+      for (size_t t = 0; t < cur.size(); ++t) pos[cur[t]] = static_cast<int32_t>(t);
+      for (int64_t r = r0; r < r1; ++r) rowloc[r] = static_cast<uint16_t>(pos[r]);
+      for (int sl = 0; sl < kStgRows / 16; ++sl) {
+        const int64_t w = slice_max[sl];
+        width.push_back(static_cast<int32_t>(w));
+        for (int64_t t = 0; t < w; ++t)
+          for (int i = 0; i < 16; ++i) {
+            const int64_t r = r0 + 16 * sl + i;
+            const bool in = r < r1 && t < rp[r + 1] - rp[r];
+            eloc.push_back(in ? static_cast<uint16_t>(pos[ci[rp[r] + t]]) : 0);
+            evals.push_back(in ? va[rp[r] + t] : 0.0);
+          }
+        slice_max[sl] = 0;
+      }
+      uniq.insert(uniq.end(), cur.begin(), cur.end());
+      uoff.push_back(static_cast<int32_t>(uniq.size()));
+      eoff.push_back(static_cast<int32_t>(eloc.size()));
+      row.push_back(static_cast<int32_t>(r1));
+      cur.clear();
+      ++chunk;
+      r0 = r1;
+      padded = 0;
+    };
+    std::vector<int32_t> fresh;  // distinct columns row r adds to the open chunk
+    auto probe = [&](int64_t r) {
+      const int32_t tag = -2 - static_cast<int32_t>(r & 0x3fffffff);  // never a chunk id or -1
+      fresh.clear();
+      auto one = [&](int32_t col) {
+        if (mark[col] != chunk && mark[col] != tag) {
+          mark[col] = tag;
+          fresh.push_back(col);
+        }
+      };
+      one(static_cast<int32_t>(r));
+      for (int64_t e = rp[r]; e < rp[r + 1]; ++e) one(ci[e]);
+    };
+    for (int64_t r = 0; r < n; ++r) {
+      const int64_t len = rp[r + 1] - rp[r];
+      probe(r);
+      int64_t rows = r - r0;
+      auto grown = [&](int64_t rw) {  // the chunk's ELL entries with row r at position rw
+        const int sl = static_cast<int>(rw / 16);
+        return padded + 16 * (std::max(slice_max[sl], len) - slice_max[sl]);
+      };
+      if (rows > 0 && (rows + 1 > kStgRows || grown(rows) > kStgNz ||
+                       static_cast<int64_t>(cur.size() + fresh.size()) > kStgUmax)) {
+        for (int32_t col : fresh) mark[col] = -1;
+        close(r);
+        probe(r);
+        rows = 0;
+      }
+      if (16 * len > kStgNz || static_cast<int64_t>(fresh.size()) > kStgUmax) {
+        good = false;
+        break;
+      }
+      padded = grown(rows);
+      slice_max[rows / 16] = std::max(slice_max[rows / 16], len);
+      for (int32_t col : fresh) {
+        mark[col] = chunk;
+        cur.push_back(col);
+      }
+    }
+    if (good && r0 < n) close(n);
+    if (!good || eloc.size() >= (size_t(1) << 31)) {
+      M->stg_state = 0;
+    } else {
+      M->stg_nch = chunk;
+      auto up = [&](auto** dst, const auto& v) -> int {
+        using T = typename std::remove_reference<decltype(v)>::type::value_type;
+        HIP_TRY(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
+        if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+        return SPIS_OK;
+      };
+      ST_TRY(up(&M->stg_row, row));
+      ST_TRY(up(&M->stg_uoff, uoff));
+      ST_TRY(up(&M->stg_uniq, uniq));
+      ST_TRY(up(&M->stg_eoff, eoff));
+      ST_TRY(up(&M->stg_width, width));
+      ST_TRY(up(&M->stg_loc, eloc));
+      ST_TRY(up(&M->stg_val, evals));
+      ST_TRY(up(&M->stg_rowloc, rowloc));
+      M->stg_state = 1;
+    }
+  }
+  *ok = M->stg_state == 1;
+  if (*ok)
+    *out = StgView{M->stg_row, M->stg_uoff, M->stg_uniq, M->stg_eoff, M->stg_width,
+                   M->stg_loc, M->stg_val,  M->stg_rowloc, M->stg_nch};
+  return SPIS_OK;
+}
+
 static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
                                   int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   QuadCon* out) {
@@ -1186,10 +1325,16 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
     const CsrView mv = cons[ci].M->view();
     const int nvv = v_done ? 0 : static_cast<int>(vlist.size());
     EllView ev{};
-    const bool use_ell = np1 <= 32 && c->ell_gram;
+    StgView sv{};
+    bool use_stg = false;
+    if (np1 <= 32 && c->ell_gram == 2) ST_TRY(ensure_stg(c, cons[ci].M, &sv, &use_stg));
+    const bool use_ell = !use_stg && np1 <= 32 && c->ell_gram >= 1;
     if (use_ell) ST_TRY(ensure_ell(c, cons[ci].M, &ev));
-    HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream,
-                                   use_ell ? &ev : nullptr));
+    if (use_stg)
+      HIP_TRY(launch_constraint_gram_stg(n, np1, sv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
+    else
+      HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream,
+                                     use_ell ? &ev : nullptr));
     const int cnt = np1 * np1 + nvv * np1;
     HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
@@ -1565,12 +1710,18 @@ struct Solver {
   }
 
   // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
-  int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr) {  // solvers.py:287
+  // done (optional): the GEMV launch carries a completion event, returned here (the sampled
+  // profiling stop event when this launch is timed, else ev_gemv)
+  int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr, hipEvent_t* done = nullptr) {  // :287
     hipStream_t s = s_gemv ? s_gemv : c->stream;
     c->prof_iter = j;
     {
       ProfEv pg(c, SPIS_PROF_GEMV);
-      const LaunchEv le = pg.both();
+      LaunchEv le = pg.both();
+      if (done != nullptr) {
+        if (le.stop == nullptr) le.stop = c->ev_gemv;
+        *done = le.stop;
+      }
       if (p <= kYArg) {
         HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, ws->xj, s, &le));
       } else {
@@ -1663,12 +1814,20 @@ struct Solver {
       // traffic) still running on the main stream; the dual SpMV waits for it.  Safe: every
       // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
       // published U_{j-1}'s residual started, and the GEMV's inputs were written before that.
-      ST_TRY(update_gemv(j, p, y, c->stream2));
-      // cross-stream order through a stream memory write / wait on a device word (~1.5% faster
-      // end to end than hipEventRecord + hipStreamWaitEvent)
-      ++c->gemv_seq;
-      HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
-      HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
+      if (c->overlap_gemv == 2) {
+        // cross-stream order through the GEMV dispatch's own completion event: no marker packet
+        // and no stream-ops blit kernels (those cost ~4.7 us on the main stream per iteration)
+        hipEvent_t done = nullptr;
+        ST_TRY(update_gemv(j, p, y, c->stream2, &done));
+        HIP_TRY(hipStreamWaitEvent(c->stream, done, 0));
+      } else {
+        ST_TRY(update_gemv(j, p, y, c->stream2));
+        // cross-stream order through a stream memory write / wait on a device word (~1.5% faster
+        // end to end than hipEventRecord + hipStreamWaitEvent)
+        ++c->gemv_seq;
+        HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
+        HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
+      }
     } else {
       ST_TRY(update_gemv(j, p, y));
     }

@@ -52,9 +52,9 @@ _OPTIONS = {
     "generic_gram": (_lib.OPT_GENERIC_GRAM, None),
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
-    "ell_gram": (_lib.OPT_ELL_GRAM, None),
+    "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2}),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, None),
-    "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, None),
+    "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}),
 }
 
@@ -67,7 +67,10 @@ def set_option(name, value, ctx=None):
     * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
       low-synchronisation option (3 reductions per step; not MGS's rounding);
     * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
-    * ``ell_gram`` (True): fused constraint reduction on a sliced-ELL copy of each matrix;
+    * ``ell_gram`` ("ell"): the fused constraint reduction reads each constraint matrix as "ell"
+      (sliced ELL; True), "staged" (row chunks whose distinct columns' basis rows are staged in
+      LDS; falls back to "ell" for a matrix with a row that does not fit a chunk) or "csr"
+      (False);
     * ``mgs_chain`` (True): each Arnoldi step's MGS chain + normalise as one persistent launch;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
     * ``spmv_pipe`` ("xcd"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of

@@ -258,14 +258,65 @@ def test_fused_and_generic_constraint_reduction_agree(spis):
         xg, dg = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
     finally:
         _lib.check(ctx.L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
-    set_option("ell_gram", False)  # K7 on the CSR (row-boundary walk) instead of the sliced ELL
+    outs = {}
     try:
-        xc, dc = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
+        for mode in ("csr", "staged"):  # K7 on the CSR (row-boundary walk) / the chunk-staged copy
+            set_option("ell_gram", mode)
+            outs[mode] = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
     finally:
-        set_option("ell_gram", True)
-    assert df["x"].trace == dg["x"].trace == dc["x"].trace
+        set_option("ell_gram", "ell")
+    for xc, dc in outs.values():
+        assert df["x"].trace == dg["x"].trace == dc["x"].trace
+        np.testing.assert_allclose(xc, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
     np.testing.assert_allclose(xf, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
-    np.testing.assert_allclose(xc, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
+
+
+@pytest.mark.parametrize("mode", ["staged", "ell", "csr"])
+def test_constraint_terms_kernels_vs_reference(spis, mode):
+    """Every K7 matrix form against constraint_container's host algebra (solvers.py:33-36):
+    a field-major banded matrix with ragged and empty rows (staged: many chunks, chunk limits hit
+    by rows, distinct columns and nonzeros), and one with a 1500-entry row (staged falls back to
+    ELL), for p + 1 = 2, 10, 32."""
+    from oracle.cgmres_port import ConstraintTerms
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+
+    rng = np.random.default_rng(7)
+    n = 6000
+
+    def banded(long_row):
+        lens = rng.integers(0, 16, size=n)
+        lens[[3, 4, 5000]] = 0
+        rows = []
+        for r in range(n):
+            near = rng.integers(max(0, r - 40), min(n, r + 40), size=lens[r])
+            far = (r * 7 + 2500 + rng.integers(0, 30, size=lens[r] // 3)) % n  # a second window
+            rows.append(np.unique(np.concatenate([near, far])))
+        if long_row:
+            rows[1234] = np.unique(rng.integers(0, n, size=1500))
+        indptr = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+        A = sps.csr_matrix((rng.normal(size=indptr[-1]), np.concatenate(rows).astype(np.int32), indptr), shape=(n, n))
+        return (A + A.T).tocsr()
+
+    class Con:
+        pass
+
+    set_option("ell_gram", mode)
+    try:
+        for long_row in (False, True):
+            con = Con()
+            con.M, con.v, con.c = banded(long_row), rng.normal(size=n), 0.3
+            for p in (1, 9, 31):
+                Z = rng.normal(size=(n, p))
+                x0 = rng.normal(size=n)
+                ref = ConstraintTerms(con, x0, Z)
+                got = solvers.constraint_container(con, x0, Z)
+                scale = np.abs(con.M).sum() * 10
+                np.testing.assert_allclose(got.term0, ref.term0, rtol=1e-12, atol=1e-12 * scale)
+                np.testing.assert_allclose(got.term1, ref.term1, rtol=1e-12, atol=1e-12 * scale)
+                np.testing.assert_allclose(got.term2, ref.term2, rtol=1e-12, atol=1e-12 * scale)
+    finally:
+        set_option("ell_gram", "ell")
 
 
 def test_fused_dual_spmv_bit_identical(spis):
@@ -290,7 +341,8 @@ def test_fused_dual_spmv_bit_identical(spis):
             A, b, cons = c.A, c.b, c.conlist()
         runs = []
         # the last run replays cached graphs; OVERLAP_GEMV moves the update GEMV to a second stream
-        for fuse, graphs, overlap in ((0, 0, 0), (1, 0, 0), (1, 0, 1), (1, 1, 1), (1, 1, 1)):
+        # (overlap 1 / 2: the dual SpMV waits on a device word / on the GEMV's completion event)
+        for fuse, graphs, overlap in ((0, 0, 0), (1, 0, 0), (1, 0, 1), (1, 0, 2), (1, 1, 2), (1, 1, 1), (1, 1, 1)):
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, graphs), "spis_set_option")
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, overlap), "spis_set_option")
