@@ -97,11 +97,14 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // previous step's exchange; w is not written back (q_{j+1} = w / h is).  Single GPU, N <= 2^20.
 constexpr int kChainMaxWG = 256;                       // <= 256 partials per exchange
 constexpr int64_t kChainMaxPairs = int64_t(kChainMaxWG) * kBlock * 8;  // PER <= 8 double2 (N <= 2^20)
-inline bool mgs_chain_fits(int64_t n) { return (n >> 1) <= kChainMaxPairs; }
+// with a dedicated gathering workgroup, 255 workgroups hold the slices
+inline bool mgs_chain_fits(int64_t n, bool aggregator = false) {
+  return (n >> 1) <= (aggregator ? kChainMaxPairs - int64_t(kBlock) * 8 : kChainMaxPairs);
+}
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
-                            unsigned long long* flag, const unsigned long long* seq);
+                            unsigned long long* flag, const unsigned long long* seq, bool aggregator = false);
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
 

@@ -813,14 +813,19 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
-    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq) {
+    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, int agg_wg) {
 #pragma clang fp contract(off)
   __shared__ double s_wave[4];
   __shared__ double s_h;
   __shared__ int s_fail;
+  // agg_wg >= 0: that workgroup (the last) holds no slice and only gathers the partials of the
+  // others (its polls never queue behind q loads of its own CU); else workgroup 0 gathers
   const int G = gridDim.x;
   const int tid = threadIdx.x;
-  const bool data = tid < kBlock;     // waves 0-3 hold the slices; wave 4 runs the exchange
+  const bool agg = static_cast<int>(blockIdx.x) == agg_wg;
+  const int gat = agg_wg >= 0 ? agg_wg : 0;          // the gathering workgroup
+  const int GD = agg_wg >= 0 ? G - 1 : G;            // workgroups publishing partials
+  const bool data = tid < kBlock && !agg;  // waves 0-3 hold the slices; wave 4 runs the exchange
   const int64_t npair = n >> 1;
   const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBlock * PER + tid;
   // U = q_i (update), D = q_{i+1} (dot), P = q_{i+2} (in flight behind the exchange; a second
@@ -884,7 +889,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     __syncthreads();
     const unsigned tag = base + static_cast<unsigned>(i) + 1u;
     unsigned long long* slots = gran + static_cast<size_t>(i & 1) * 2 * kChainMaxWG;
-    if (tid == 0) {  // publish from a data wave: the exchange wave's polls never wait on these stores
+    if (tid == 0 && !agg) {  // publish from a data wave: the exchange wave's polls never wait on these stores
       const double tot = ((s_wave[0] + s_wave[1]) + s_wave[2]) + s_wave[3];
       const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(tot));
       chain_store(slots + 2 * blockIdx.x, tag, static_cast<unsigned>(bits));
@@ -895,14 +900,14 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       bool all_ok = false;
       double acc = 0.0;
-      if (blockIdx.x == 0) {  // workgroup 0 gathers every workgroup's partial (granule 2g = lo, 2g+1 = hi)
+      if (static_cast<int>(blockIdx.x) == gat) {  // gathers every data workgroup's partial (granule 2g = lo, 2g+1 = hi)
         unsigned long long g[8];
         for (unsigned spins = 0;; ++spins) {
           bool ok = true;
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const int idx = lane + 64 * k;
-            g[k] = idx < 2 * G ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
+            g[k] = idx < 2 * GD ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
             ok &= static_cast<unsigned>(g[k] >> 32) == tag;
           }
           if (__all(ok)) {
@@ -919,7 +924,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
               static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
           const double v =
               __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
-          if ((lane & 1) == 0 && lane + 64 * k < 2 * G) acc += v;
+          if ((lane & 1) == 0 && lane + 64 * k < 2 * GD) acc += v;
         }
         acc = wave_sum_dpp(acc);
         if (lane == 0) {  // and hands the sum to every other workgroup
@@ -928,7 +933,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
           chain_store(hs, tag, static_cast<unsigned>(bits));
           chain_store(hs + 1, tag, static_cast<unsigned>(bits >> 32));
         }
-      } else {  // the others poll workgroup 0's two granules (few pollers: the q stream keeps its bandwidth)
+      } else {  // the others poll the gatherer's two granules (few pollers: the q stream keeps its bandwidth)
         const unsigned long long* hs = gran + 4 * kChainMaxWG + 2 * (i & 1);
         unsigned long long g = 0;
         for (unsigned spins = 0;; ++spins) {
@@ -981,15 +986,19 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
-                            unsigned long long* flag, const unsigned long long* seq) {
+                            unsigned long long* flag, const unsigned long long* seq, bool aggregator) {
   const int64_t npair = n >> 1;
   if (npair > kChainMaxPairs || !aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
-  const int per = npair <= int64_t(kChainMaxWG) * kBlock * 2 ? 2 : npair <= int64_t(kChainMaxWG) * kBlock * 4 ? 4 : 8;
+  const int64_t wmax = kChainMaxWG - (aggregator ? 1 : 0);  // one workgroup per CU in all
+  const int per = npair <= wmax * kBlock * 2 ? 2 : npair <= wmax * kBlock * 4 ? 4 : 8;
   const int64_t span = int64_t(kBlock) * per;
-  const int G = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
+  const int GD = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
+  if (GD > wmax) return hipErrorInvalidValue;
+  const int G = GD + (aggregator ? 1 : 0);
+  const int agg_wg = aggregator ? GD : -1;
 #define SPIS_CHAIN(PER_)                                                                                   \
   launch_k(mgs_chain_kernel<PER_>, dim3(G), dim3(kChainThreads), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, hcol, \
-           gran, epoch, err, xpart, n_x, x_out, flag, seq)
+           gran, epoch, err, xpart, n_x, x_out, flag, seq, agg_wg)
   switch (per) {
     case 2: SPIS_CHAIN(2); break;
     case 4: SPIS_CHAIN(4); break;

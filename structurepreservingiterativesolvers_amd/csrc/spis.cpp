@@ -124,7 +124,7 @@ struct spis_context {
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   int ell_gram = 1;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy (SPIS_OPT_ELL_GRAM)
-  bool mgs_chain = true;            // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN)
+  int mgs_chain = 2;                // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 on, 2 with a dedicated gathering workgroup
   // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
   // waits for it through 1 a stream write / wait on a device word, 2 the GEMV launch's own
   // completion event (hipStreamWaitEvent: no blit kernels)
@@ -224,7 +224,7 @@ struct spis_workspace {
     const double* pinned_dev = nullptr;
     int gs = 0, gb = 0;
     bool cgs2 = false;
-    bool chain = false;
+    int chain = 0;
     bool operator==(const GraphKey& o) const {
       return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb && cgs2 == o.cgs2 &&
              chain == o.chain;
@@ -566,7 +566,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "ell gram %lld: 0, 1 or 2", (long long)value);
         c->ell_gram = static_cast<int>(value);
         return SPIS_OK;
-      case SPIS_OPT_MGS_CHAIN: c->mgs_chain = value != 0; return SPIS_OK;
+      case SPIS_OPT_MGS_CHAIN:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0, 1 or 2", (long long)value);
+        c->mgs_chain = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_OVERLAP_GEMV:
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "overlap gemv %lld: 0, 1 or 2", (long long)value);
         c->overlap_gemv = static_cast<int>(value);
@@ -1647,10 +1650,11 @@ struct Solver {
     ProfEv pm(c, SPIS_PROF_MGS);  // start on the first MGS step, stop on the normalise
     const LaunchEv e_first = pm.first();
     const LaunchEv e_last = pm.last();
-    if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n)) {  // K2p: the chain in one launch
+    const bool agg = c->mgs_chain == 2;
+    if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
-                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq));
+                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg));
       return SPIS_OK;
     }
     double* src = c->partA;
@@ -2108,7 +2112,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
     if (*reinterpret_cast<volatile unsigned*>(c->chain_err) != 0) {  // never on a healthy device
       *c->chain_err = 0;
-      c->mgs_chain = false;
+      c->mgs_chain = 0;
       return fail(SPIS_ERR_STATE, "persistent MGS chain: a workgroup never reached an exchange (the chain is "
                                   "now disabled on this context; rerun the solve)");
     }

@@ -53,7 +53,7 @@ _OPTIONS = {
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
     "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2}),
-    "mgs_chain": (_lib.OPT_MGS_CHAIN, None),
+    "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 2, "gather0": 1, "aggregator": 2}),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}),
 }
@@ -71,7 +71,9 @@ def set_option(name, value, ctx=None):
       (sliced ELL; True), "staged" (row chunks whose distinct columns' basis rows are staged in
       LDS; falls back to "ell" for a matrix with a row that does not fit a chunk) or "csr"
       (False);
-    * ``mgs_chain`` (True): each Arnoldi step's MGS chain + normalise as one persistent launch;
+    * ``mgs_chain`` (True = "aggregator"): each Arnoldi step's MGS chain + normalise as one persistent
+      launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
+      ("gather0"); False = one launch per MGS step;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
     * ``spmv_pipe`` ("xcd"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of
       the row blocks, "stride" pipelined grid-stride, "off" unpipelined (rows bit-identical in

@@ -749,19 +749,22 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
     b = rng.standard_normal(n)
     k = 12
     runs = []
-    for chain in (1, 1, 0):
+    # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 0: per-step launches
+    for chain in (1, 1, 2, 2, 0):
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
         try:
             x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
         finally:
-            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 1), "spis_set_option")
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 2), "spis_set_option")
         runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
-    (x1, r1, Q1), (x2, r2, Q2), (x0, r0, Q0) = runs
+    (x1, r1, Q1), (x2, r2, Q2), (x3, r3, Q3), (x4, r4, Q4), (x0, r0, Q0) = runs
     assert np.array_equal(x1, x2) and np.array_equal(r1, r2) and np.array_equal(Q1, Q2)
-    assert np.linalg.norm(x1 - x0) <= 1e-11 * np.linalg.norm(x0)
-    np.testing.assert_allclose(r1, r0, rtol=1e-10, atol=0)
-    np.testing.assert_allclose(Q1, Q0, rtol=0, atol=1e-11)
-    # orthogonality: MGS's own loss, the same with either grouping of the partial dots
-    loss1 = np.abs(Q1 @ Q1.T - np.eye(k)).max()
+    assert np.array_equal(x3, x4) and np.array_equal(r3, r4) and np.array_equal(Q3, Q4)
     loss0 = np.abs(Q0 @ Q0.T - np.eye(k)).max()
-    assert loss1 <= 4 * loss0 + 1e-14, (loss1, loss0)
+    for x, r, Q in ((x1, r1, Q1), (x3, r3, Q3)):
+        assert np.linalg.norm(x - x0) <= 1e-11 * np.linalg.norm(x0)
+        np.testing.assert_allclose(r, r0, rtol=1e-10, atol=0)
+        np.testing.assert_allclose(Q, Q0, rtol=0, atol=1e-11)
+        # orthogonality: MGS's own loss, the same with either grouping of the partial dots
+        loss = np.abs(Q @ Q.T - np.eye(k)).max()
+        assert loss <= 4 * loss0 + 1e-14, (loss, loss0)
