@@ -159,6 +159,9 @@ def main():
     ap.add_argument("--chain", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
                          "workgroup 0, 2 with a dedicated gathering workgroup")
+    ap.add_argument("--early-con", type=int, default=2, choices=[0, 1, 2],
+                    help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
+                         "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
     ap.add_argument("--gram", default="ell", choices=["staged", "ell", "csr"],
                     help="constraint-Gram matrix form (SPIS_OPT_ELL_GRAM)")
     ap.add_argument("--spmv-pipe", default="xcd", choices=["off", "stride", "xcd", "stride2", "xcd2"],
@@ -197,6 +200,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, args.chain), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}[args.spmv_pipe]),

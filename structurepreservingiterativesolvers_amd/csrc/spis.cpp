@@ -132,6 +132,15 @@ struct spis_context {
   hipEvent_t ev_gemv = nullptr;
   int spmv_pipe = 2;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep
   hipStream_t stream2 = nullptr;
+  // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
+  // on stream3 as soon as its basis exists, beside the last Arnoldi step and update
+  int early_con = 2;  // 0 off; launched once A_{k-2} (1: measured 5% slower, it delays A_{k-1}'s chain) / A_{k-1} (2)
+  hipStream_t stream3 = nullptr;
+  hipEvent_t ev_pre_in = nullptr, ev_pre_done = nullptr;
+  double* pre_pinned = nullptr;  // the early reduction's results
+  size_t pre_pinned_len = 0;
+  double* con_pinned = nullptr;  // the synchronous reduction's results
+  size_t con_pinned_len = 0;
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
   uint64_t gemv_seq = 0;
   unsigned long long* chain_gran = nullptr;  // 2 parities x kChainMaxWG x 2 granules
@@ -441,6 +450,7 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     c->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&c->gemv_flag, 16));
     HIP_TRY(hipMemset(c->gemv_flag, 0, 16));
     const int np = std::max(kSpmvGrid, kRedGrid);
@@ -471,6 +481,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gemv, hipEventDisableTiming | hipEventReleaseToDevice));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_pre_in, hipEventDisableTiming | hipEventReleaseToDevice));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_pre_done, hipEventDisableTiming));  // system scope: host reads
     *out = c.release();
     return SPIS_OK;
   })
@@ -531,10 +543,14 @@ extern "C" int spis_context_destroy(spis_context* c) {
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->stream2);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_gemv})
+    (void)hipStreamSynchronize(c->stream3);
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_gemv, c->ev_pre_in, c->ev_pre_done})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
+    (void)hipStreamDestroy(c->stream3);
+    if (c->pre_pinned) (void)hipHostFree(c->pre_pinned);
+    if (c->con_pinned) (void)hipHostFree(c->con_pinned);
     delete c;
     return SPIS_OK;
   })
@@ -573,6 +589,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_OVERLAP_GEMV:
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "overlap gemv %lld: 0, 1 or 2", (long long)value);
         c->overlap_gemv = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_EARLY_CON:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "early con %lld: 0, 1 or 2", (long long)value);
+        c->early_con = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
         if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 4", (long long)value);
@@ -1288,9 +1308,28 @@ static int ensure_stg(spis_context* c, spis_matrix* M, StgView* out, bool* ok) {
   return SPIS_OK;
 }
 
-static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
-                                  int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
-                                  QuadCon* out) {
+// host buffer of one step's reductions: constraint ci's G (np1 x np1) at ci * np1^2, then the
+// linear terms (one np1 row per constraint with a v) at m * np1^2
+static size_t con_result_len(int m, int p) {
+  const size_t np1 = static_cast<size_t>(p) + 1;
+  return static_cast<size_t>(m) * np1 * np1 + 4 * np1;
+}
+
+static int ensure_host_buf(double** buf, size_t* len, size_t need) {
+  if (*len >= need) return SPIS_OK;
+  if (*buf) HIP_TRY(hipHostFree(*buf));
+  *buf = nullptr;
+  *len = 0;
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(buf), sizeof(double) * need, hipHostMallocDefault));
+  *len = need;
+  return SPIS_OK;
+}
+
+// Enqueues the transpose and every constraint matrix's Gram of one step on stream st, each result
+// copied to dst (layout: con_result_len).  One-time buffers and matrix copies are made first
+// (they may synchronise the main stream, on first use only).
+static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
+                            int p, const double* Z, int64_t pitch, const double* x0, hipStream_t st, double* dst) {
   const int np1 = p + 1;
   const int ut_cols = np1 <= 32 ? 32 : 64;  // Ut is N x np1 row-major: size for this p bucket
   if (ws->Ut && ws->Ut_cols < ut_cols) {
@@ -1308,62 +1347,61 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
     c->cg_part_len = need;
   }
   if (!c->cg_G) HIP_TRY(hipMalloc(&c->cg_G, sizeof(double) * (64 * 64 + 4 * 64)));
-  if (!c->gram_pinned)
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->gram_pinned), sizeof(double) * (64 * 64 + 2 * kGramMaxVec),
-                          hipHostMallocDefault));
-  HIP_TRY(launch_transpose_basis(n, p, Z, pitch, x0, ws->Ut, c->stream));
   std::vector<const double*> vlist;
-  std::vector<int> vidx(m, -1);
   for (int ci = 0; ci < m; ++ci)
-    if (cons[ci].v_dev) {
-      vidx[ci] = static_cast<int>(vlist.size());
-      vlist.push_back(cons[ci].v_dev);
-    }
-  std::vector<double> Gv(static_cast<size_t>(vlist.size()) * np1, 0.0);
-  std::vector<std::vector<double>> Gm(m);
-  bool v_done = vlist.empty();
+    if (cons[ci].v_dev) vlist.push_back(cons[ci].v_dev);
+  struct Launch {
+    int ci;
+    bool stg, ell;
+    EllView ev;
+    StgView sv;
+  };
+  std::vector<Launch> plan;
   for (int ci = 0; ci < m; ++ci) {
-    const bool mzero = cons[ci].M == nullptr || cons[ci].M->all_zero;
-    if (mzero) continue;
-    const CsrView mv = cons[ci].M->view();
-    const int nvv = v_done ? 0 : static_cast<int>(vlist.size());
-    EllView ev{};
-    StgView sv{};
-    bool use_stg = false;
-    if (np1 <= 32 && c->ell_gram == 2) ST_TRY(ensure_stg(c, cons[ci].M, &sv, &use_stg));
-    const bool use_ell = !use_stg && np1 <= 32 && c->ell_gram >= 1;
-    if (use_ell) ST_TRY(ensure_ell(c, cons[ci].M, &ev));
-    if (use_stg)
-      HIP_TRY(launch_constraint_gram_stg(n, np1, sv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
+    if (cons[ci].M == nullptr || cons[ci].M->all_zero) continue;
+    Launch L{ci, false, false, {}, {}};
+    if (np1 <= 32 && c->ell_gram == 2) ST_TRY(ensure_stg(c, cons[ci].M, &L.sv, &L.stg));
+    L.ell = !L.stg && np1 <= 32 && c->ell_gram >= 1;
+    if (L.ell) ST_TRY(ensure_ell(c, cons[ci].M, &L.ev));
+    plan.push_back(L);
+  }
+  const size_t voff = static_cast<size_t>(m) * np1 * np1;
+  const int nv = static_cast<int>(vlist.size());
+  HIP_TRY(launch_transpose_basis(n, p, Z, pitch, x0, ws->Ut, st));
+  bool v_done = nv == 0;
+  for (const Launch& L : plan) {
+    const CsrView mv = cons[L.ci].M->view();
+    const int nvv = v_done ? 0 : nv;
+    if (L.stg)
+      HIP_TRY(launch_constraint_gram_stg(n, np1, L.sv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st));
     else
-      HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream,
-                                     use_ell ? &ev : nullptr));
-    const int cnt = np1 * np1 + nvv * np1;
-    HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
-    ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
-    Gm[ci].assign(c->gram_pinned, c->gram_pinned + np1 * np1);
-    if (!v_done) {
-      std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + cnt, Gv.begin());
-      v_done = true;
-    }
+      HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st,
+                                     L.ell ? &L.ev : nullptr));
+    HIP_TRY(hipMemcpyAsync(dst + static_cast<size_t>(L.ci) * np1 * np1, c->cg_G, sizeof(double) * np1 * np1,
+                           hipMemcpyDeviceToHost, st));
+    if (nvv > 0)
+      HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + np1 * np1, sizeof(double) * nvv * np1, hipMemcpyDeviceToHost, st));
+    v_done = true;
   }
-  if (!v_done) {
-    const int nvv = static_cast<int>(vlist.size());
-    HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->gram_pinned, c->cg_G, sizeof(double) * (np1 * np1 + nvv * np1), hipMemcpyDeviceToHost,
-                           c->stream));
-    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));
-    ST_TRY(wait_event(c->ev_gram));
-    std::copy(c->gram_pinned + np1 * np1, c->gram_pinned + np1 * np1 + nvv * np1, Gv.begin());
+  if (!v_done) {  // linear terms only
+    HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nv, vlist.data(), c->cg_part, c->cg_G, st));
+    HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + np1 * np1, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
   }
+  return SPIS_OK;
+}
+
+// term0 / term1 / term2 of every constraint (solvers.py:34-36) from con_gram_enqueue's results
+static void con_terms_assemble(int m, const spis_constraint_desc* cons, int p, const double* src, QuadCon* out) {
+  const int np1 = p + 1;
+  const double* gvall = src + static_cast<size_t>(m) * np1 * np1;
+  int iv = 0;
   for (int ci = 0; ci < m; ++ci) {
     QuadCon& q = out[ci];
     q.term1.assign(p, 0.0);
     q.term2.assign(static_cast<size_t>(p) * p, 0.0);
-    const std::vector<double>& G = Gm[ci];
-    const bool hasM = !G.empty();
-    const double* gv = vidx[ci] >= 0 ? Gv.data() + static_cast<size_t>(vidx[ci]) * np1 : nullptr;
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    const double* G = src + static_cast<size_t>(ci) * np1 * np1;
+    const double* gv = cons[ci].v_dev ? gvall + static_cast<size_t>(iv++) * np1 : nullptr;
     const double x0Mx0 = hasM ? G[static_cast<size_t>(p) * np1 + p] : 0.0;
     const double vx0 = gv ? gv[p] : 0.0;
     q.term0 = 0.5 * x0Mx0 + cons[ci].c + vx0;  // solvers.py:34
@@ -1373,6 +1411,17 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
       for (int a = 0; a < p; ++a)
         for (int b = 0; b < p; ++b) q.term2[static_cast<size_t>(a) * p + b] = 0.5 * G[static_cast<size_t>(a) * np1 + b];
   }
+}
+
+// fused path, synchronous: every launch of the step, then one wait
+static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
+                                  int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                  QuadCon* out) {
+  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
+  ST_TRY(con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned));
+  HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
+  ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
+  con_terms_assemble(m, cons, p, c->con_pinned, out);
   return SPIS_OK;
 }
 
@@ -1960,6 +2009,24 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     std::vector<QuadCon> cons(std::max(o->n_constraints, 0));
     bool have_x = false;   // ws->xj holds x[-1] (else x[-1] = r0)
     int pending = -1;      // iteration whose update U_j is in flight and not yet read
+    // early reduction of the final forced constrained step (j = k-1, solvers.py:230): launched on
+    // stream3 once A_{k-2} (the producer of its last basis vector) is queued; class-form
+    // constraints on the fused single-GPU path, no separate preconditioned basis
+    int nlin = 0;
+    for (int i = 0; i < (use_cb ? 0 : o->n_constraints); ++i) nlin += o->constraints[i].v_dev ? 1 : 0;
+    const bool early = c->early_con && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && !c->comm &&
+                       k + 1 <= 64 && nlin <= 4 && !c->force_generic_gram && ws->Zb == ws->Q && k >= 4;
+    bool pre_launched = false;
+    auto launch_early = [&]() -> int {
+      ST_TRY(ensure_host_buf(&c->pre_pinned, &c->pre_pinned_len, con_result_len(o->n_constraints, k)));
+      HIP_TRY(hipEventRecord(c->ev_pre_in, s));
+      HIP_TRY(hipStreamWaitEvent(c->stream3, c->ev_pre_in, 0));
+      ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, k, ws->Zb, ws->pitch, ws->x0, c->stream3,
+                              c->pre_pinned));
+      HIP_TRY(hipEventRecord(c->ev_pre_done, c->stream3));
+      pre_launched = true;
+      return SPIS_OK;
+    };
 
     if (beta == 0.0) {  // x0 solves the system: q0 would be 0/0 (reference: NaNs); report breakdown
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
@@ -2027,9 +2094,14 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       } else {
         // class-form constraints reduced on the device (:242-247), KKT on the host (:251-255)
         if (stamps) stamps[2 * k + j] = now_s();
-        if (m_active > 0)
+        if (m_active > 0 && pre_launched && p == k && m_active == o->n_constraints) {
+          ST_TRY(wait_event(c->ev_pre_done));  // reduced early, beside the last Arnoldi step
+          con_terms_assemble(m_active, o->constraints, p, c->pre_pinned, cons.data());
+        } else if (m_active > 0) {
+          if (pre_launched) HIP_TRY(hipStreamWaitEvent(s, c->ev_pre_done, 0));  // shares Ut / Gram buffers
           ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
                                       cons.data()));
+        }
         if (stamps) stamps[3 * k + j] = now_s();
         bool failed = false;
         if (m_active == 0) {
@@ -2090,6 +2162,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           ST_TRY(S.enqueue_arnoldi(j + 2));
         }
       }
+      if (early && !pre_launched && j + 2 == k - 3 + c->early_con) ST_TRY(launch_early());  // A_{k-2} / A_{k-1} queued
       have_x = true;
       pending = j;
     }
@@ -2104,8 +2177,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
     }
-    // speculative Arnoldi steps finish before x / ws are used (event spin: a blocking synchronize
-    // wakes the host up tens of us late, per solve)
+    // speculative Arnoldi steps (and an unused early reduction) finish before x / ws are used
+    // (event spin: a blocking synchronize wakes the host up tens of us late, per solve)
+    if (pre_launched) HIP_TRY(hipStreamWaitEvent(s, c->ev_pre_done, 0));
     HIP_TRY(hipEventRecord(c->ev_gram, s));
     ST_TRY(wait_event(c->ev_gram));
     prof_drain(c);

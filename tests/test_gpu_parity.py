@@ -319,6 +319,36 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
         set_option("ell_gram", "ell")
 
 
+def test_early_constraint_reduction_bit_identical(spis):
+    """SPIS_OPT_EARLY_CON: the final step's constraint reduction launched early on a third stream
+    (after A_{k-2} or A_{k-1} is queued) gives the same bits as reducing when the step is reached,
+    also when constrained steps start earlier (they wait for it) and when the solve stops before
+    the final step (the early reduction goes unused)."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=20)
+    cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+    A, b = dic["A"], dic["b"]
+    k = 25
+    _, d = solvers.cgmres(A, b, np.zeros_like(b), k, tol=1e-19, conlist=cons)
+    tols = (1e-19, d["res"][20] / 10)  # all k steps / constrained steps from j ~ 21 on, early stop
+    try:
+        for tol in tols:
+            runs = []
+            for mode in (0, 1, 2, 1):
+                set_option("early_con", {0: False, 1: "a_k-2", 2: "a_k-1"}[mode])
+                x, d = solvers.cgmres(A, b, np.zeros_like(b), k, tol=tol, conlist=cons)
+                runs.append((x, np.asarray(d["res"]), d["steps"], d["x"].trace))
+            for r in runs[1:]:
+                assert np.array_equal(r[0], runs[0][0]) and np.array_equal(r[1], runs[0][1]), tol
+                assert r[2:] == runs[0][2:], tol
+    finally:
+        set_option("early_con", True)
+
+
 def test_fused_dual_spmv_bit_identical(spis):
     """SPIS_OPT_FUSE_SPMV / SPIS_OPT_GRAPHS / SPIS_OPT_OVERLAP_GEMV: the true-residual SpMV of U_j
     fused with the Arnoldi SpMV of A_{j+2} (matrix read once), the Arnoldi steps replayed from
