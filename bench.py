@@ -159,7 +159,7 @@ def main():
     ap.add_argument("--chain", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
                          "workgroup 0, 2 with a dedicated gathering workgroup")
-    ap.add_argument("--early-con", type=int, default=2, choices=[0, 1, 2],
+    ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],
                     help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
                          "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
     ap.add_argument("--gram", default="ell", choices=["staged", "ell", "csr"],

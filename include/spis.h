@@ -145,10 +145,11 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   the row blocks (its share of the gathered vectors stays in its own L2), 1 = grid-stride walk,
  *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight.  Rows are bit-identical in every mode; the reduction partials
  *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.
- * SPIS_OPT_EARLY_CON (default 2): the constraint reduction of CGMRES's forced final constrained
- *   step (j = k-1) is launched on a third stream once A_{k-1} (2) or A_{k-2} (1: the earliest,
- *   A_{k-2} writes the last basis vector it needs; measured slower, it delays A_{k-1}'s persistent
- *   chain) is queued, beside the last update; 0 = when the step is reached.  Results identical. */
+ * SPIS_OPT_EARLY_CON (default 0): the constraint reduction of CGMRES's forced final constrained
+ *   step (j = k-1) is launched on a third stream once A_{k-1} (2; measured equal to 0 at C3) or
+ *   A_{k-2} (1: the earliest, A_{k-2} writes the last basis vector it needs; measured 5% slower,
+ *   it delays A_{k-1}'s persistent chain) is queued; 0 = when the step is reached.  Results
+ *   identical. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,

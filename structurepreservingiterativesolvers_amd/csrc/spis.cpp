@@ -134,7 +134,7 @@ struct spis_context {
   hipStream_t stream2 = nullptr;
   // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
   // on stream3 as soon as its basis exists, beside the last Arnoldi step and update
-  int early_con = 2;  // 0 off; launched once A_{k-2} (1: measured 5% slower, it delays A_{k-1}'s chain) / A_{k-1} (2)
+  int early_con = 0;  // 0 off; launched once A_{k-2} (1: measured 5% slower, it delays A_{k-1}'s chain) / A_{k-1} (2: equal)
   hipStream_t stream3 = nullptr;
   hipEvent_t ev_pre_in = nullptr, ev_pre_done = nullptr;
   double* pre_pinned = nullptr;  // the early reduction's results

@@ -346,7 +346,7 @@ def test_early_constraint_reduction_bit_identical(spis):
                 assert np.array_equal(r[0], runs[0][0]) and np.array_equal(r[1], runs[0][1]), tol
                 assert r[2:] == runs[0][2:], tol
     finally:
-        set_option("early_con", True)
+        set_option("early_con", False)
 
 
 def test_fused_dual_spmv_bit_identical(spis):
