@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--chain", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
                          "workgroup 0, 2 with a dedicated gathering workgroup")
+    ap.add_argument("--nt-basis", type=int, default=2, choices=[0, 1, 2],
+                    help="MGS chain basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
     ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],
                     help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
                          "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
@@ -201,6 +203,7 @@ def main():
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, args.chain), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}[args.spmv_pipe]),

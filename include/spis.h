@@ -149,7 +149,11 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   step (j = k-1) is launched on a third stream once A_{k-1} (2; measured equal to 0 at C3) or
  *   A_{k-2} (1: the earliest, A_{k-2} writes the last basis vector it needs; measured 5% slower,
  *   it delays A_{k-1}'s persistent chain) is queued; 0 = when the step is reached.  Results
- *   identical. */
+ *   identical.
+ * SPIS_OPT_NT_BASIS (default 2): the persistent MGS chain loads basis vectors with nontemporal
+ *   loads, so re-streaming the basis every Arnoldi step does not evict the matrix from the
+ *   256 MB Infinity Cache before the next SpMV; 2 = when the matrix and the k+1 basis vectors
+ *   exceed 256 MB, 1 = always, 0 = never.  Results identical. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -159,7 +163,8 @@ enum spis_option {
   SPIS_OPT_MGS_CHAIN = 6,
   SPIS_OPT_OVERLAP_GEMV = 7,
   SPIS_OPT_SPMV_PIPE = 8,
-  SPIS_OPT_EARLY_CON = 9
+  SPIS_OPT_EARLY_CON = 9,
+  SPIS_OPT_NT_BASIS = 10
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -25,6 +25,7 @@ PROF_KINDS = 5
 OPT_FUSE_SPMV, OPT_GENERIC_GRAM, OPT_GRAPHS, OPT_ORTHOG, OPT_ELL_GRAM, OPT_MGS_CHAIN, OPT_OVERLAP_GEMV = 1, 2, 3, 4, 5, 6, 7
 OPT_SPMV_PIPE = 8
 OPT_EARLY_CON = 9
+OPT_NT_BASIS = 10
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

@@ -104,7 +104,9 @@ inline bool mgs_chain_fits(int64_t n, bool aggregator = false) {
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
-                            unsigned long long* flag, const unsigned long long* seq, bool aggregator = false);
+                            unsigned long long* flag, const unsigned long long* seq, bool aggregator = false,
+                            bool nt = false);
+// (nt: the chain's basis loads are nontemporal — the matrix stays Infinity-Cache resident)
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
 

@@ -67,6 +67,17 @@ static void launch_k(F kernel, dim3 g, dim3 b, uint32_t shm, hipStream_t s, cons
     hipLaunchKernelGGL(kernel, g, b, shm, s, args...);
 }
 
+// basis-vector loads of the MGS chain: optionally nontemporal, so that re-streaming the basis at
+// every Arnoldi step does not evict the matrix from the 256 MB Infinity Cache between two SpMVs
+__device__ __forceinline__ double2 ld_basis(const double2* p, bool nt) {
+  if (nt) {
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    const v2d v = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+    return make_double2(v.x, v.y);
+  }
+  return *p;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1: CSR SpMV, row blocks of <= kItemCap merge items (rows + nnz), products staged in LDS.
 //
@@ -813,7 +824,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
-    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, int agg_wg) {
+    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, int agg_wg, bool nt) {
 #pragma clang fp contract(off)
   __shared__ double s_wave[4];
   __shared__ double s_h;
@@ -835,7 +846,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     const double2* v2 = reinterpret_cast<const double2*>(v);
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * kBlock < npair) r[k] = v2[p0 + k * kBlock];
+      if (data && p0 + k * kBlock < npair) r[k] = ld_basis(v2 + p0 + k * kBlock, nt);
   };
   const unsigned base = *epoch;
   load(y, w);
@@ -986,7 +997,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
-                            unsigned long long* flag, const unsigned long long* seq, bool aggregator) {
+                            unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt) {
   const int64_t npair = n >> 1;
   if (npair > kChainMaxPairs || !aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
   const int64_t wmax = kChainMaxWG - (aggregator ? 1 : 0);  // one workgroup per CU in all
@@ -998,7 +1009,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
   const int agg_wg = aggregator ? GD : -1;
 #define SPIS_CHAIN(PER_)                                                                                   \
   launch_k(mgs_chain_kernel<PER_>, dim3(G), dim3(kChainThreads), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, hcol, \
-           gran, epoch, err, xpart, n_x, x_out, flag, seq, agg_wg)
+           gran, epoch, err, xpart, n_x, x_out, flag, seq, agg_wg, nt)
   switch (per) {
     case 2: SPIS_CHAIN(2); break;
     case 4: SPIS_CHAIN(4); break;

@@ -125,6 +125,7 @@ struct spis_context {
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   int ell_gram = 1;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy (SPIS_OPT_ELL_GRAM)
   int mgs_chain = 2;                // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 on, 2 with a dedicated gathering workgroup
+  int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
   // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
   // waits for it through 1 a stream write / wait on a device word, 2 the GEMV launch's own
   // completion event (hipStreamWaitEvent: no blit kernels)
@@ -589,6 +590,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_OVERLAP_GEMV:
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "overlap gemv %lld: 0, 1 or 2", (long long)value);
         c->overlap_gemv = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_NT_BASIS:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "nt basis %lld: 0, 1 or 2", (long long)value);
+        c->nt_basis = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_EARLY_CON:
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "early con %lld: 0, 1 or 2", (long long)value);
@@ -1700,10 +1705,15 @@ struct Solver {
     const LaunchEv e_first = pm.first();
     const LaunchEv e_last = pm.last();
     const bool agg = c->mgs_chain == 2;
+    // nontemporal basis loads when the matrix and the basis overflow the 256 MB Infinity Cache:
+    // the chain then leaves the matrix resident for the next SpMV (C3: dual SpMV 49 -> 42 us,
+    // chain +1-2 us, +2.9%; C4, whose working set fits, measured 1% slower with them)
+    const double ws_bytes = 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * (k + 1) * static_cast<double>(n);
+    const bool nt_chain = c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
     if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
-                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg));
+                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain));
       return SPIS_OK;
     }
     double* src = c->partA;

@@ -55,6 +55,7 @@ _OPTIONS = {
     "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2}),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 2, "gather0": 1, "aggregator": 2}),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
+    "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}),
 }
@@ -76,6 +77,8 @@ def set_option(name, value, ctx=None):
       launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
       ("gather0"); False = one launch per MGS step;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
+    * ``nt_basis`` ("auto"): the MGS chain's basis loads are nontemporal when the matrix and the
+      basis exceed the 256 MB Infinity Cache (True: always; False: never), results identical;
     * ``early_con`` (False): CGMRES's final forced constrained step reduces its constraints on a
       third stream once the last Arnoldi step is queued (True / "a_k-1") or the one before it
       ("a_k-2"); results identical, measured no faster at C3;

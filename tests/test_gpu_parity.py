@@ -319,6 +319,30 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
         set_option("ell_gram", "ell")
 
 
+def test_nontemporal_chain_loads_bit_identical(spis):
+    """SPIS_OPT_NT_BASIS changes the cache policy of the MGS chain's basis loads only: the same
+    bits with and without it."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+    A, b = dic["A"], dic["b"]
+    runs = []
+    try:
+        for mode in (False, True, "auto"):
+            set_option("nt_basis", mode)
+            x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
+            runs.append((x, np.asarray(d["res"]), d["x"].basis(25)))
+    finally:
+        set_option("nt_basis", "auto")
+    for r in runs[1:]:
+        for a, bb in zip(runs[0], r):
+            assert np.array_equal(a, bb)
+
+
 def test_early_constraint_reduction_bit_identical(spis):
     """SPIS_OPT_EARLY_CON: the final step's constraint reduction launched early on a third stream
     (after A_{k-2} or A_{k-1} is queued) gives the same bits as reducing when the step is reached,
