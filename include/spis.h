@@ -140,10 +140,11 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
  *   The dual SpMV waits for it through a stream write / wait on a device word (1) or through the
  *   GEMV launch's own completion event (2; measured equal end to end); 0 = main stream.
- * SPIS_OPT_SPMV_PIPE (default 2): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
+ * SPIS_OPT_SPMV_PIPE (default 5): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
  *   software-pipelined row-block kernels; 2 = each XCD's workgroups walk a contiguous eighth of
  *   the row blocks (its share of the gathered vectors stays in its own L2), 1 = grid-stride walk,
- *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight.  Rows are bit-identical in every mode; the reduction partials
+ *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight;
+ *   5 = 2 while the matrix's val/col fit the 256 MB Infinity Cache, else 1.  Rows are bit-identical in every mode; the reduction partials
  *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.
  * SPIS_OPT_EARLY_CON (default 0): the constraint reduction of CGMRES's forced final constrained
  *   step (j = k-1) is launched on a third stream once A_{k-1} (2; measured equal to 0 at C3) or

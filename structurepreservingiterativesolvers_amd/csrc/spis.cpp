@@ -131,7 +131,7 @@ struct spis_context {
   // completion event (hipStreamWaitEvent: no blit kernels)
   int overlap_gemv = 1;
   hipEvent_t ev_gemv = nullptr;
-  int spmv_pipe = 2;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep
+  int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1)
   hipStream_t stream2 = nullptr;
   // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
   // on stream3 as soon as its basis exists, beside the last Arnoldi step and update
@@ -256,10 +256,14 @@ static bool fixed_grid(const spis_context* c) { return c->comm != nullptr; }
 // the solver's SpMV table: kDualCap row blocks, run by the pipelined kernels unless disabled
 CsrView spis_matrix::dual_view() const {
   CsrView v{n_rows, indptr, indices, vals, blk_row_d, n_blk_d, false};
-  if (ctx->spmv_pipe > 0) {
+  int mode = ctx->spmv_pipe;
+  // auto: the XCD-local walk while val/col fit the 256 MB Infinity Cache (C3 dual SpMV 42-43 vs
+  // 44-45 us grid-stride), the grid-stride walk beyond (C5, 1.5 GB: 502 vs 574 us)
+  if (mode == 5) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
+  if (mode > 0) {
     v.blk_meta = blk_meta_d;
-    v.walk = (ctx->spmv_pipe & 1) == 0 ? 1 : 0;
-    v.depth = ctx->spmv_pipe >= 3 ? 2 : 1;
+    v.walk = (mode & 1) == 0 ? 1 : 0;
+    v.depth = mode >= 3 ? 2 : 1;
   }
   return v;
 }
@@ -600,7 +604,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->early_con = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
-        if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 4", (long long)value);
+        if (value < 0 || value > 5) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 5", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_ORTHOG:

@@ -57,7 +57,7 @@ _OPTIONS = {
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
-    "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4}),
+    "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5}),
 }
 
 
@@ -82,9 +82,10 @@ def set_option(name, value, ctx=None):
     * ``early_con`` (False): CGMRES's final forced constrained step reduces its constraints on a
       third stream once the last Arnoldi step is queued (True / "a_k-1") or the one before it
       ("a_k-2"); results identical, measured no faster at C3;
-    * ``spmv_pipe`` ("xcd"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of
-      the row blocks, "stride" pipelined grid-stride, "off" unpipelined (rows bit-identical in
-      every mode; reduction partials grouped per workgroup);
+    * ``spmv_pipe`` ("auto"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of
+      the row blocks, "stride" pipelined grid-stride, "off" unpipelined, "auto" = "xcd" while
+      the matrix fits the 256 MB Infinity Cache, else "stride" (rows bit-identical in every
+      mode; reduction partials grouped per workgroup);
     * ``device_ilu`` ("auto"): how a SuperLU ``pre`` (``spilu``/``splu``) is applied — True on
       the device (K8), False by its host ``pre.solve`` through the callback (as the reference
       does), "auto" on the device when the plan's cost model predicts it is faster

@@ -69,7 +69,7 @@ def _matrices():
     return out
 
 
-@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd2", "stride2", "off"])
+@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd2", "stride2", "off", "auto"])
 def test_spmv_bit_exact_vs_scipy(spis, pipe):
     """Every SpMV kernel (SPIS_OPT_SPMV_PIPE: pipelined XCD-local / grid-stride walk, unpipelined)
     is bit-exact vs SciPy on rows that fit a row block (<= 1024 nnz: the solver's table); longer
@@ -93,7 +93,7 @@ def test_spmv_bit_exact_vs_scipy(spis, pipe):
             r = P.residual_norm(A, x, yref + 1e-3)
             np.testing.assert_allclose(r, np.linalg.norm(A @ x - (yref + 1e-3)), rtol=1e-12)
     finally:
-        set_option("spmv_pipe", "xcd")
+        set_option("spmv_pipe", "auto")
 
 
 def test_spmv_pipe_modes_solver_agree(spis):
@@ -114,7 +114,7 @@ def test_spmv_pipe_modes_solver_agree(spis):
             x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
             runs[pipe] = (x, np.asarray(d["res"]), d["steps"], d["x"].trace)
     finally:
-        set_option("spmv_pipe", "xcd")
+        set_option("spmv_pipe", "auto")
     x0, r0, s0, t0 = runs["off"]
     for pipe in ("stride", "xcd", "stride2", "xcd2"):
         x, r, st, tr = runs[pipe]
