@@ -97,9 +97,11 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // previous step's exchange; w is not written back (q_{j+1} = w / h is).  Single GPU, N <= 2^20.
 constexpr int kChainMaxWG = 256;                       // <= 256 partials per exchange
 constexpr int64_t kChainMaxPairs = int64_t(kChainMaxWG) * kBlock * 8;  // PER <= 8 double2 (N <= 2^20)
-// with a dedicated gathering workgroup, 255 workgroups hold the slices
+// K2b (with a dedicated gathering workgroup only): w alone in registers, 255 workgroups of 512
+// threads x <= 40 pairs (N <= 10.4 M)
+constexpr int64_t kChainBigMaxPairs = int64_t(kChainMaxWG - 1) * 512 * 40;
 inline bool mgs_chain_fits(int64_t n, bool aggregator = false) {
-  return (n >> 1) <= (aggregator ? kChainMaxPairs - int64_t(kBlock) * 8 : kChainMaxPairs);
+  return (n >> 1) <= (aggregator ? kChainBigMaxPairs : kChainMaxPairs);
 }
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,

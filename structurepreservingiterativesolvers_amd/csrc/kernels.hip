@@ -994,12 +994,254 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
   if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
 }
 
+// The exchange of one chain step (K2p's protocol): the gathering workgroup's wave sweeps every
+// data workgroup's {tag, half} granules, sums the partials in a fixed order and publishes h as two
+// granules at hs; every other workgroup's wave polls those two.  Bounded spins (0.5 s).
+__device__ __forceinline__ void chain_exchange(int lane, bool gatherer, int GD, unsigned tag,
+                                               unsigned long long* slots, unsigned long long* hs, unsigned* err,
+                                               double* s_h, int* s_fail) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool all_ok = false;
+  double acc = 0.0;
+  if (gatherer) {
+    unsigned long long g[8];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = lane + 64 * k;
+        g[k] = idx < 2 * GD ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
+        ok &= static_cast<unsigned>(g[k] >> 32) == tag;
+      }
+      if (__all(ok)) {
+        all_ok = true;
+        break;
+      }
+      if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // lane pairs (2m, 2m+1) of round k hold partial (64 k + 2 m) / 2
+      const unsigned lo = static_cast<unsigned>(g[k]);
+      const unsigned hi = static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
+      const double v = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+      if ((lane & 1) == 0 && lane + 64 * k < 2 * GD) acc += v;
+    }
+    acc = wave_sum_dpp(acc);
+    if (lane == 0) {
+      const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(acc));
+      chain_store(hs, tag, static_cast<unsigned>(bits));
+      chain_store(hs + 1, tag, static_cast<unsigned>(bits >> 32));
+    }
+  } else {
+    unsigned long long g = 0;
+    for (unsigned spins = 0;; ++spins) {
+      g = lane < 2 ? chain_load(hs + lane) : (static_cast<unsigned long long>(tag) << 32);
+      if (__all(static_cast<unsigned>(g >> 32) == tag)) {
+        all_ok = true;
+        break;
+      }
+      if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+    }
+    const unsigned lo = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 0, 64));
+    const unsigned hi = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 1, 64));
+    acc = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+  }
+  if (lane == 0) {
+    *s_h = acc;
+    if (!all_ok) {
+      *s_fail = 1;
+      atomicOr(err, 1u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2b: the persistent MGS chain for large N (K2p's limit < N <= 10.4 M; K2 launches beyond).
+// Only w lives in registers (PER double2 per thread, 8 waves per workgroup, 255 data workgroups +
+// the gathering one, one workgroup per CU).  Each step streams q_i (mostly still in the Infinity
+// Cache from the previous step's dot) and q_{i+1} in chunks of 2 pairs, two chunks in flight:
+// 16 N bytes per step instead of K2's 32 N (w is neither re-read nor written back) and no kernel
+// boundary.  Wave 0 runs the exchange after the data phase (no loads in flight then).  Tags,
+// exchange and arithmetic as K2p (contraction off; partials grouped per workgroup).
+// ---------------------------------------------------------------------------------------------
+constexpr int kBigThreads = 512;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// buffer-descriptor loads / stores: one 32-bit lane offset shared by every element of a thread,
+// the element's distance in the scalar offset (no per-element address registers).  The hardware
+// range check does not cover the scalar offset: callers predicate every access themselves.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_double2(__hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)),
+                      __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)));
+}
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 d) {
+  u32x4_t v;
+  v.x = static_cast<unsigned>(__double2loint(d.x));
+  v.y = static_cast<unsigned>(__double2hiint(d.x));
+  v.z = static_cast<unsigned>(__double2loint(d.y));
+  v.w = static_cast<unsigned>(__double2hiint(d.y));
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+
+template <int PER>
+__global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
+    int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
+    const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
+    unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
+    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq) {
+#pragma clang fp contract(off)
+  constexpr int NW = kBigThreads / 64;
+  constexpr int CH = 2;  // pairs per streamed chunk
+  constexpr int NC = PER / CH;
+  static_assert(NC % 2 == 0, "chunks are consumed in pairs");
+  __shared__ double s_wave[NW];
+  __shared__ double s_h;
+  __shared__ int s_fail;
+  const int GD = static_cast<int>(gridDim.x) - 1;  // the last workgroup gathers
+  const int tid = threadIdx.x;
+  const bool data = static_cast<int>(blockIdx.x) != GD;
+  const int64_t npair = n >> 1;
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBigThreads * PER + tid;
+  const int voff = static_cast<int>(p0 * 16);      // this thread's first pair, bytes
+  constexpr int kStep = kBigThreads * 16;           // bytes between a thread's consecutive pairs
+  const int64_t vbytes = npair * 16;
+  // pairs k < kv of this thread exist (every access is predicated on it)
+  const int kv = (data && p0 < npair) ? static_cast<int>(min<int64_t>(PER, (npair - p0 + kBigThreads - 1) / kBigThreads)) : 0;
+  double2 y[PER];
+  {
+    const __amdgpu_buffer_rsrc_t rw = vec_rsrc(w, vbytes);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) y[k] = k < kv ? buf_ld2(rw, voff, k * kStep) : make_double2(0.0, 0.0);
+  }
+  const unsigned base = *epoch;
+  const bool tail = (n & 1) && blockIdx.x == 0 && tid == 0;  // odd element: workgroup 0, lane 0
+  double yt = tail ? w[n - 1] : 0.0;
+  if (tid == 0) s_fail = 0;
+  double h = chain_sum_partials(part_in, n_in, s_wave);
+  if (blockIdx.x == 0 && tid == 0) hcol[0] = h;
+  if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
+    const double t = chain_sum_partials(xpart, n_x, s_wave);
+    if (tid == 0) publish(x_out, t, flag, seq);
+  }
+  for (int i = 0; i <= j; ++i) {
+    const bool last = i == j;
+    double part = 0.0;
+    if (data) {
+      // q_i and q_{i+1} (none at the last step: a zero-length range reads zeros)
+      const __amdgpu_buffer_rsrc_t ru = vec_rsrc(Q + static_cast<int64_t>(i) * pitch, vbytes);
+      const __amdgpu_buffer_rsrc_t rd = vec_rsrc(Q + static_cast<int64_t>(i + 1) * pitch, vbytes);
+      double2 ua[CH], da[CH], ub[CH], db[CH];
+      auto fetch = [&](double2 (&uu)[CH], double2 (&dd)[CH], int c) {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const bool ok = c * CH + q < kv;
+          uu[q] = ok ? buf_ld2(ru, voff, (c * CH + q) * kStep) : make_double2(0.0, 0.0);
+          dd[q] = (ok && !last) ? buf_ld2(rd, voff, (c * CH + q) * kStep) : make_double2(0.0, 0.0);
+        }
+      };
+      auto consume = [&](const double2 (&uu)[CH], const double2 (&dd)[CH], int c) {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const int k = c * CH + q;
+          if (k < kv) {
+            const double a0 = h * uu[q].x, a1 = h * uu[q].y;
+            y[k].x = y[k].x - a0;
+            y[k].y = y[k].y - a1;
+            if (!last) {
+              part += dd[q].x * y[k].x;
+              part += dd[q].y * y[k].y;
+            } else {
+              part += y[k].x * y[k].x;
+              part += y[k].y * y[k].y;
+            }
+          }
+        }
+      };
+      fetch(ua, da, 0);
+#pragma unroll
+      for (int c = 0; c < NC; c += 2) {
+        fetch(ub, db, c + 1);
+        consume(ua, da, c);
+        if (c + 2 < NC) fetch(ua, da, c + 2);
+        consume(ub, db, c + 1);
+      }
+    }
+    if (tail) {
+      const double a = h * Q[static_cast<int64_t>(i) * pitch + n - 1];
+      yt = yt - a;
+      part += last ? yt * yt : Q[static_cast<int64_t>(i + 1) * pitch + n - 1] * yt;
+    }
+    {  // workgroup partial: DPP wave sums, fixed combine
+      const double wv = wave_sum_dpp(part);
+      if (data && (tid & 63) == 0) s_wave[tid >> 6] = wv;
+    }
+    __syncthreads();
+    const unsigned tag = base + static_cast<unsigned>(i) + 1u;
+    unsigned long long* slots = gran + static_cast<size_t>(i & 1) * 2 * kChainMaxWG;
+    if (tid < 64) {
+      if (tid == 0 && data) {
+        double tot = s_wave[0];
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) tot += s_wave[ww];
+        const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(tot));
+        chain_store(slots + 2 * blockIdx.x, tag, static_cast<unsigned>(bits));
+        chain_store(slots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bits >> 32));
+      }
+      chain_exchange(tid, !data, GD, tag, slots, gran + 4 * kChainMaxWG + 2 * (i & 1), err, &s_h, &s_fail);
+    }
+    __syncthreads();
+    const double hn = s_h;
+    if (s_fail) break;  // uniform: a workgroup never arrived; the host reports it
+    if (!last) {
+      h = hn;
+      if (blockIdx.x == 0 && tid == 0) hcol[i + 1] = hn;
+    } else {  // K3: h_{j+1,j} = ||y||, q_{j+1} = y / h (zeros on breakdown)
+      const double hh = sqrt(hn);
+      if (blockIdx.x == 0 && tid == 0) hcol[j + 1] = hh;
+      const __amdgpu_buffer_rsrc_t rq = vec_rsrc(Q + static_cast<int64_t>(j + 1) * pitch, vbytes);
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (k < kv)
+          buf_st2(rq, voff, k * kStep, hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh));
+      if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
+}
+
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt) {
   const int64_t npair = n >> 1;
-  if (npair > kChainMaxPairs || !aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
+  if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
+  if (aggregator && npair > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b
+    if (npair > kChainBigMaxPairs) return hipErrorInvalidValue;
+    const int64_t wd = kChainMaxWG - 1;
+    const int per = npair <= wd * kBigThreads * 8    ? 8
+                    : npair <= wd * kBigThreads * 16 ? 16
+                    : npair <= wd * kBigThreads * 24 ? 24
+                    : npair <= wd * kBigThreads * 32 ? 32
+                                                     : 40;
+    const int64_t span = int64_t(kBigThreads) * per;
+    const int GD = static_cast<int>((npair + span - 1) / span);
+#define SPIS_BIG(PER_)                                                                                             \
+  launch_k(mgs_chain_big_kernel<PER_>, dim3(GD + 1), dim3(kBigThreads), 0, s, ev, n, w, Q, pitch, j, part_in, n_in, \
+           hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq)
+    switch (per) {
+      case 8: SPIS_BIG(8); break;
+      case 16: SPIS_BIG(16); break;
+      case 24: SPIS_BIG(24); break;
+      case 32: SPIS_BIG(32); break;
+      default: SPIS_BIG(40); break;
+    }
+#undef SPIS_BIG
+    return hipGetLastError();
+  }
+  if (npair > kChainMaxPairs) return hipErrorInvalidValue;
   const int64_t wmax = kChainMaxWG - (aggregator ? 1 : 0);  // one workgroup per CU in all
   const int per = npair <= wmax * kBlock * 2 ? 2 : npair <= wmax * kBlock * 4 ? 4 : 8;
   const int64_t span = int64_t(kBlock) * per;

@@ -787,12 +787,14 @@ def test_distributed_code_path_self_halo(spis):
     ctx.close()
 
 
-@pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_048_575, 2_000_001])
+@pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_048_575, 2_000_001, 3_500_000, 5_000_001, 7_500_001, 10_000_001])
 def test_mgs_chain_matches_per_step_launches(spis, n):
-    """K2p (SPIS_OPT_MGS_CHAIN): the persistent MGS chain against one launch per MGS step, on
-    sizes that select each register tiling (PER = 2, 4, 8 double2 per thread), the largest N the
-    chain takes (odd: a tail element) and one beyond it (per-step launches either way).  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
-    agree to 1e-11 relative; the chain is bitwise reproducible run to run; orthogonality as MGS's."""
+    """K2p / K2b (SPIS_OPT_MGS_CHAIN): the persistent MGS chains against one launch per MGS step,
+    on sizes that select each register tiling (K2p: PER = 2, 4, 8 double2 per thread; K2b, the
+    dedicated-gatherer mode beyond 2^20: PER = 8, 16, 24, 32, 40), the largest N K2p takes (odd: a
+    tail element).  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
+    agree to 1e-11 relative; the chains are bitwise reproducible run to run; orthogonality as
+    MGS's."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
     from structurepreservingiterativesolvers_amd.device import get_context
 
@@ -804,18 +806,20 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
     k = 12
     runs = []
     # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 0: per-step launches
-    for chain in (1, 1, 2, 2, 0):
+    modes = (1, 1, 2, 2, 0) if n <= 2_000_001 else (2, 2, 0)
+    for chain in modes:
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
         try:
             x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
         finally:
             _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 2), "spis_set_option")
         runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
-    (x1, r1, Q1), (x2, r2, Q2), (x3, r3, Q3), (x4, r4, Q4), (x0, r0, Q0) = runs
-    assert np.array_equal(x1, x2) and np.array_equal(r1, r2) and np.array_equal(Q1, Q2)
-    assert np.array_equal(x3, x4) and np.array_equal(r3, r4) and np.array_equal(Q3, Q4)
+    x0, r0, Q0 = runs[-1]
+    pairs = [(runs[i], runs[i + 1]) for i in range(0, len(runs) - 1, 2)]
+    for (xa, ra, Qa), (xb, rb, Qb) in pairs:
+        assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
     loss0 = np.abs(Q0 @ Q0.T - np.eye(k)).max()
-    for x, r, Q in ((x1, r1, Q1), (x3, r3, Q3)):
+    for x, r, Q in (p[0] for p in pairs):
         assert np.linalg.norm(x - x0) <= 1e-11 * np.linalg.norm(x0)
         np.testing.assert_allclose(r, r0, rtol=1e-10, atol=0)
         np.testing.assert_allclose(Q, Q0, rtol=0, atol=1e-11)
