@@ -13,7 +13,8 @@ constexpr int kNnzCap = 2048;    // nnz staged in LDS per row block (16 KiB fp64
 constexpr int kItemCap = 2048;   // merge items (rows + nnz) per row block
 constexpr int kDualCap = 1024;   // nnz / items per row block of the fused dual SpMV (2 x 8 KiB LDS)
 constexpr int kSpmvGrid = 2048;  // max SpMV workgroups (= max epilogue partials)
-constexpr int kPipeGridFixed = 1280;  // pipelined SpMV workgroups on several ranks (MI355X: 256 CUs x 5 resident)
+constexpr int kPipeCap = 2048;   // nnz per row block of the pipelined SpMVs (K1p / K1dp: kNnzCap / kItemCap table)
+constexpr int kPipeGridFixed = 768;  // pipelined SpMV workgroups on several ranks (MI355X: 256 CUs x 3 resident)
 constexpr int kRedGrid = 1024;   // max BLAS-1 workgroups (= max reduction partials)
 constexpr int kMaxK = 1024;      // max Krylov dimension handled by the GEMV's LDS copy of y
 constexpr int kGramChunk = 32;   // vector elements staged per Gram chunk
@@ -76,7 +77,7 @@ hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, co
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev = nullptr);
-// K1p / K1dp (A.blk_meta on a kDualCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
+// K1p / K1dp (A.blk_meta on a kPipeCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
 // part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi)
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,

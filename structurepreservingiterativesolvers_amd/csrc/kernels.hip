@@ -554,10 +554,10 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   dim3 g(grid), b(kBlock);
 #define SPIS_PIPE(M)                                                                                            \
   if (A.depth == 2)                                                                                             \
-    launch_k(spmv_pipe2_kernel<kDualCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
+    launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
   else                                                                                                          \
-    launch_k(spmv_pipe_kernel<kDualCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
+    launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
@@ -595,8 +595,8 @@ static int resident_grid(F kernel) {
 }
 
 static int pipe_grid_max(int depth) {
-  static const int g1 = resident_grid(spmv_pipe_kernel<kDualCap, 4>);
-  static const int g2 = resident_grid(spmv_pipe2_kernel<kDualCap, 4>);
+  static const int g1 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
+  static const int g2 = resident_grid(spmv_pipe2_kernel<kPipeCap, 4>);
   return depth == 2 ? g2 : g1;
 }
 

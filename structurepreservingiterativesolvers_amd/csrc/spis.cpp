@@ -174,7 +174,7 @@ struct spis_matrix {
   int32_t n_blk = 0, n_long = 0;
   int32_t* blk_row_d = nullptr;  // row blocks of <= kDualCap nnz / items for the fused dual SpMV
   int32_t n_blk_d = 0;
-  int2* blk_meta_d = nullptr;    // the same blocks as (row start, nz start): the pipelined kernels' table
+  int2* blk_meta_d = nullptr;    // blk_row's blocks (<= kPipeCap nnz) as (row start, nz start): the pipelined kernels' table
   // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
@@ -262,6 +262,7 @@ CsrView spis_matrix::dual_view() const {
   if (mode == 5) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   if (mode > 0) {
     v.blk_meta = blk_meta_d;
+    v.n_blk = n_blk;
     v.walk = (mode & 1) == 0 ? 1 : 0;
     v.depth = mode >= 3 ? 2 : 1;
   }
@@ -769,16 +770,20 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       HIP_TRY(hipMemcpy(M->vals, data, sizeof(double) * nnz, hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMemcpy(M->blk_row, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+    {  // the pipelined kernels walk blk_row's blocks (kNnzCap = kPipeCap): in kbench at C3, 2048-nnz
+       // blocks at 3 workgroups per CU vs 1024 at 5: dual SpMV 52.6 vs 56.4 us cold, 41.2 vs 41.1 warm
+      static_assert(kNnzCap == kPipeCap && kItemCap == kPipeCap, "pipelined table = blk_row");
+      std::vector<int2> meta(blk.size());
+      for (size_t i = 0; i < blk.size(); ++i) meta[i] = make_int2(blk[i], indptr[blk[i]]);
+      HIP_TRY(hipMalloc(&M->blk_meta_d, sizeof(int2) * meta.size()));
+      HIP_TRY(hipMemcpy(M->blk_meta_d, meta.data(), sizeof(int2) * meta.size(), hipMemcpyHostToDevice));
+    }
     {  // the fused residual + Arnoldi SpMV stages two product arrays: half-size blocks keep its LDS
       int32_t n_long_d = 0;  // at 16 KiB per workgroup (kbench: 52 vs 62 us at C3)
       build_row_blocks(n_rows, indptr, blk, n_long_d, kDualCap, kDualCap);
       M->n_blk_d = static_cast<int32_t>(blk.size()) - 1;
       HIP_TRY(hipMalloc(&M->blk_row_d, sizeof(int32_t) * blk.size()));
       HIP_TRY(hipMemcpy(M->blk_row_d, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
-      std::vector<int2> meta(blk.size());
-      for (size_t i = 0; i < blk.size(); ++i) meta[i] = make_int2(blk[i], indptr[blk[i]]);
-      HIP_TRY(hipMalloc(&M->blk_meta_d, sizeof(int2) * meta.size()));
-      HIP_TRY(hipMemcpy(M->blk_meta_d, meta.data(), sizeof(int2) * meta.size(), hipMemcpyHostToDevice));
     }
     if (halo && halo->n_neighbors > 0) {
       M->n_ghost = n_ghost;

@@ -587,6 +587,90 @@ int main(int argc, char** argv) {
     printf("%-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
            100.0 * bytes / (us * 1e-6) / 8e12);
   };
+  if (argc > 2 && std::string(argv[2]) == "cap") {
+    // K1dp / K1p block capacity: 512 / 1024 / 2048 nnz per row block (<= 256 rows), warm (back to
+    // back: the matrix Infinity-Cache resident, as in the solver) and cold; rows checked bit-equal
+    double *dx2, *dw, *dw2, *db, *pa, *pb;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&dw2, 8 * pitch));
+    CK(hipMalloc(&db, 8 * pitch));
+    CK(hipMalloc(&pa, 8 * 16384));
+    CK(hipMalloc(&pb, 8 * 16384));
+    std::vector<double> h2(pitch);
+    for (int64_t i = 0; i < pitch; ++i) h2[i] = i < n ? 1e-3 * ((i * 104729) % 997) - 0.4 : 0.0;
+    CK(hipMemcpy(dx2, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    auto table = [&](int cap, int& nb) {
+      std::vector<int32_t> blk;
+      blocks(n, rp.data(), cap, 256, cap, blk);
+      nb = static_cast<int>(blk.size()) - 1;
+      std::vector<int2> meta(nb + 1);
+      for (int i = 0; i <= nb; ++i) meta[i] = make_int2(blk[i], rp[blk[i]]);
+      int2* d;
+      CK(hipMalloc(&d, 8 * meta.size()));
+      CK(hipMemcpy(d, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice));
+      return d;
+    };
+    int nb5, nb1, nb2;
+    int2* m5 = table(512, nb5);
+    int2* m1 = table(1024, nb1);
+    int2* m2 = table(2048, nb2);
+    printf("blocks: cap512 %d cap1024 %d cap2048 %d\n", nb5, nb1, nb2);
+    const int64_t big = int64_t(1) << 26;
+    double* bx;
+    CK(hipMalloc(&bx, 8 * big));
+    CK(hipMemset(bx, 0, 8 * big));
+    auto run = [&](const char* name, double bytes, auto&& launch) {
+      for (int cold = 0; cold < 2; ++cold) {
+        double tot = 0;
+        const int reps = 30;
+        for (int r = 0; r < reps + 3; ++r) {
+          if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                                       reinterpret_cast<const double2*>(bx), pb + 8192);
+          launch();
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (r >= 3) tot += ms;
+        }
+        const double us = 1e3 * tot / reps;
+        printf("%s %-40s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", cold ? "COLD" : "WARM", name, us,
+               bytes / (us * 1e-6) / 1e9, 100.0 * bytes / (us * 1e-6) / 8e12);
+      }
+    };
+    char nm[128];
+#define CAPRUN(CAPV, MT, NB, G)                                                                                \
+  snprintf(nm, sizeof nm, "dual cap%d grid=%d", CAPV, G);                                                      \
+  run(nm, SD, [&] {                                                                                            \
+    hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
+                          dva, MT, NB, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);                      \
+  });                                                                                                          \
+  snprintf(nm, sizeof nm, "K1 dot cap%d grid=%d", CAPV, G);                                                    \
+  run(nm, S, [&] {                                                                                             \
+    hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 1, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
+                          dva, MT, NB, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);                                     \
+  })
+    for (int g : {1280, 2048}) { CAPRUN(512, m5, nb5, g); }
+    for (int g : {1024, 1280}) { CAPRUN(1024, m1, nb1, g); }
+    for (int g : {512, 768, 1024, 1280}) { CAPRUN(2048, m2, nb2, g); }
+#undef CAPRUN
+    {  // rows bit-equal across capacities (each row sum is left to right in every table)
+      hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, m1,
+                         nb1, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+      hipLaunchKernelGGL((spmv_pipe_kernel<2048, 4, false, 1>), dim3(768), dim3(kBlock), 0, s, drp, dci, dva, m2,
+                         nb2, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb);
+      CK(hipStreamSynchronize(s));
+      std::vector<double> w1(n), w2(n);
+      CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(w2.data(), dw2, 8 * n, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+      printf("cap2048 vs cap1024 dual rows: %lld differ\n", (long long)bad);
+    }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "pipe") {
     // pipelined K1p / K1dp vs the current kernels: bit-identity check, then timings
     std::vector<int32_t> blk;
