@@ -306,6 +306,16 @@ int spis_solve(spis_context* ctx, spis_matrix* A, const double* b_dev, const dou
 int spis_workspace_iterate(spis_workspace* ws, int32_t i, double* x_dev_out);
 /* Z[:, :p] to host, row-major (p, n) */
 int spis_workspace_basis(spis_workspace* ws, int32_t p, double* Z_host);
+/* H[:p+1, :p] of the run (solvers.py:181,193-196) to host, row-major (p+1, p);
+ * p <= the number of LS steps taken.  With res_host[0] = beta it is the exact
+ * small least-squares problem every step j < p solved (diagnostics, parity). */
+int spis_workspace_hessenberg(spis_workspace* ws, int32_t p, double* H_host);
+/* The reduced class-form constraint ci (solvers.py:33-36) of the run's last
+ * constrained step, as the host KKT solve received it: *p_out = that step's p;
+ * term1 capacity k, term2 capacity k*k (row-major p x p).  SPIS_ERR_ARG if the
+ * run had no such step (dict-form constraints go through the callback). */
+int spis_workspace_constraint_terms(spis_workspace* ws, int32_t ci, int32_t* p_out, double* term0,
+                                    double* term1, double* term2);
 int spis_workspace_release(spis_workspace* ws);
 
 #ifdef __cplusplus

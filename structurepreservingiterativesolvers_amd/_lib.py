@@ -141,6 +141,8 @@ SIGNATURES = [
     ("spis_solve", C.c_int, [_VP, _VP, _VP, _VP, C.POINTER(SolveOpts), C.POINTER(SolveOut), C.POINTER(_VP)]),
     ("spis_workspace_iterate", C.c_int, [_VP, _I32, _VP]),
     ("spis_workspace_basis", C.c_int, [_VP, _I32, _PD]),
+    ("spis_workspace_hessenberg", C.c_int, [_VP, _I32, _PD]),
+    ("spis_workspace_constraint_terms", C.c_int, [_VP, _I32, C.POINTER(C.c_int32), _PD, _PD, _PD]),
     ("spis_workspace_release", C.c_int, [_VP]),
 ]
 

@@ -141,6 +141,250 @@ double norm2(const double* v, int n) {
 
 }  // namespace
 
+namespace {
+
+// Outcome of one Newton run on the KKT system.
+enum class Stop { kFloor, kSmallStep, kStall, kIterLimit, kSingular, kNonFinite };
+
+struct Run {
+  Stop stop = Stop::kIterLimit;
+  int iterations = 0;
+  double fn = 0.0;  // ||F|| at the returned point
+};
+
+// ||grad_y L|| and the magnitude of its terms at (y, lam); J must hold the Jacobian at y
+void grad_scale(const KKTState& st, const double* y, const double* lam, const double* F,
+                const std::vector<double>& J, double* gn, double* gs) {
+  const int p = st.p, m = st.m;
+  *gn = 0.0;
+  *gs = 0.0;
+  for (int a = 0; a < p; ++a) {
+    double t = std::fabs(st.b0[a]);
+    for (int b = 0; b < p; ++b) t += std::fabs(st.B[static_cast<size_t>(a) * p + b] * y[b]);
+    for (int i = 0; i < m; ++i) t += std::fabs(J[static_cast<size_t>(i) * p + a] * lam[i]);
+    *gs = std::max(*gs, t);
+    *gn = std::max(*gn, std::fabs(F[a]));
+  }
+}
+
+// Newton with a merit line search on ||F|| from (y, lam); both updated in place
+Run newton_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& lam, int max_iter) {
+  const int p = st.p, m = st.m, n = p + m;
+  std::vector<double> J(static_cast<size_t>(m) * p), F(n), Fn(n), K, rhs(n), yn(p), ln(m);
+  Run run;
+  int it = 0;
+  for (; it < max_iter; ++it) {
+    // offsets: a few ulps of each constraint's rounding scale, so that the COMPUTED value
+    // lands <= 0 (the reference's checker is a signed max against ctol, solvers.py:14-18,267)
+    for (int i = 0; i < m; ++i) st.tau[i] = 8.0 * DBL_EPSILON * con_scale(cons[i], p, y);
+    st.residual(cons, y, lam.data(), F.data(), J);
+    const double fn = norm2(F.data(), n);
+    run.fn = fn;
+    if (!std::isfinite(fn)) { run.stop = Stop::kNonFinite; break; }
+    {  // converged at the rounding floor: the gradient part of F within 64 ulps of its terms'
+       // scale and every constraint at its target (c_i in [-2 tau_i, 0]).  Newton steps from
+       // here are noise; the line search would backtrack ~30 times per step (~60 us at p = 30)
+      double gn, gs;
+      grad_scale(st, y, lam.data(), F.data(), J, &gn, &gs);
+      bool cons_ok = true;
+      for (int i = 0; i < m; ++i) cons_ok = cons_ok && std::fabs(F[p + i]) <= st.tau[i];
+      if (cons_ok && gn <= 64.0 * DBL_EPSILON * gs) { run.stop = Stop::kFloor; break; }
+    }
+    K.assign(static_cast<size_t>(n) * n, 0.0);
+    for (int a = 0; a < p; ++a)
+      for (int b = 0; b < p; ++b) {
+        double w = st.B[static_cast<size_t>(a) * p + b];
+        for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
+        K[static_cast<size_t>(a) * n + b] = w;
+      }
+    for (int i = 0; i < m; ++i)
+      for (int a = 0; a < p; ++a) {
+        K[static_cast<size_t>(a) * n + p + i] = J[static_cast<size_t>(i) * p + a];
+        K[static_cast<size_t>(p + i) * n + a] = J[static_cast<size_t>(i) * p + a];
+      }
+    for (int r = 0; r < n; ++r) rhs[r] = -F[r];
+    if (!lu_solve(n, K, rhs.data())) { run.stop = Stop::kSingular; break; }
+    {  // a Newton step below the stopping size: take it unless it raises ||F||, and stop (no
+       // backtracking: at roundoff level the sufficient-decrease test cannot pass and would cost
+       // 40 residual evaluations)
+      double step = 0.0, ymax = 0.0;
+      for (int a = 0; a < p; ++a) {
+        step = std::max(step, std::fabs(rhs[a]));
+        ymax = std::max(ymax, std::fabs(y[a] + rhs[a]));
+      }
+      if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax)) {
+        for (int a = 0; a < p; ++a) yn[a] = y[a] + rhs[a];
+        for (int i = 0; i < m; ++i) ln[i] = lam[i] + rhs[p + i];
+        st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
+        const double fnew = norm2(Fn.data(), n);
+        if (std::isfinite(fnew) && fnew <= fn) {
+          for (int a = 0; a < p; ++a) y[a] = yn[a];
+          for (int i = 0; i < m; ++i) lam[i] = ln[i];
+          run.fn = fnew;
+        }
+        run.stop = Stop::kSmallStep;
+        ++it;
+        break;
+      }
+    }
+    double alpha = 1.0;
+    double fnew = 0.0;
+    // up to 40 halvings (alpha >= 2^-39): far from the solution the merit function can need
+    // short steps; near it the rounding-floor test above ends the run before any halving
+    for (int ls = 0; ls < 40; ++ls) {
+      for (int a = 0; a < p; ++a) yn[a] = y[a] + alpha * rhs[a];
+      for (int i = 0; i < m; ++i) ln[i] = lam[i] + alpha * rhs[p + i];
+      st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
+      fnew = norm2(Fn.data(), n);
+      if (std::isfinite(fnew) && fnew <= (1.0 - 1e-4 * alpha) * fn) break;
+      alpha *= 0.5;
+    }
+    double step = 0.0, ymax = 0.0;
+    for (int a = 0; a < p; ++a) {
+      step = std::max(step, std::fabs(yn[a] - y[a]));
+      ymax = std::max(ymax, std::fabs(yn[a]));
+    }
+    if (std::isfinite(fnew) && fnew <= fn) {
+      for (int a = 0; a < p; ++a) y[a] = yn[a];
+      for (int i = 0; i < m; ++i) lam[i] = ln[i];
+      run.fn = fnew;
+    }
+    if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax)) { run.stop = Stop::kSmallStep; ++it; break; }
+    if (!(fnew < fn)) { run.stop = Stop::kStall; ++it; break; }
+  }
+  run.iterations = it;
+  return run;
+}
+
+// First-order test at the returned point, looser than the rounding floor (a run that stops on
+// a small step or a stalled line search has not necessarily converged): gradient of the
+// Lagrangian within 1e-8 of its terms' scale and every constraint within 1e-10 of its own
+// rounding scale.  The multipliers are refit by least squares first (the run's lam may lag).
+bool first_order_ok(KKTState& st, const QuadCon* cons, const double* y, std::vector<double>& lam) {
+  const int p = st.p, m = st.m;
+  std::vector<double> J(static_cast<size_t>(m) * p), F(p + m), zero(m, 0.0);
+  st.residual(cons, y, zero.data(), F.data(), J);
+  if (m > 0) {
+    std::vector<double> JJ(static_cast<size_t>(m) * m), r(m);
+    for (int i = 0; i < m; ++i) {
+      for (int k = 0; k < m; ++k) {
+        double t = 0.0;
+        for (int a = 0; a < p; ++a) t += J[static_cast<size_t>(i) * p + a] * J[static_cast<size_t>(k) * p + a];
+        JJ[static_cast<size_t>(i) * m + k] = t;
+      }
+      double t = 0.0;
+      for (int a = 0; a < p; ++a) t += J[static_cast<size_t>(i) * p + a] * F[a];
+      r[i] = -t;
+    }
+    // a rank-deficient J (a constraint whose gradient is roundoff, e.g. a conserved quantity the
+    // Krylov space cannot change) keeps the run's multipliers
+    if (lu_solve(m, JJ, r.data())) {
+      std::vector<double> lam_fit(r.begin(), r.end());
+      std::vector<double> Ft(p + m);
+      st.residual(cons, y, lam_fit.data(), Ft.data(), J);
+      std::vector<double> Fr(p + m);
+      st.residual(cons, y, lam.data(), Fr.data(), J);
+      if (norm2(Ft.data(), p) < norm2(Fr.data(), p)) lam = lam_fit;
+    }
+  }
+  st.residual(cons, y, lam.data(), F.data(), J);
+  double gn, gs;
+  grad_scale(st, y, lam.data(), F.data(), J, &gn, &gs);
+  if (!(gn <= 1e-8 * gs)) return false;
+  for (int i = 0; i < m; ++i) {
+    const double sc = con_scale(cons[i], p, y);
+    if (!(std::fabs(F[p + i]) <= 1e-10 * sc + 1e-300)) return false;
+  }
+  return true;
+}
+
+// Second-order test: the Hessian of the Lagrangian, B + sum lam_i S_i, positive definite on the
+// null space of J (a constrained minimum, not a saddle of the indefinite energy constraint).
+// Null space from a Householder QR of J'; Cholesky of the reduced matrix with a shift of
+// 1e-10 of its largest diagonal entry, so a semidefinite direction at roundoff passes.
+bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, const std::vector<double>& lam) {
+  const int p = st.p, m = st.m;
+  if (m >= p) return true;
+  std::vector<double> W(static_cast<size_t>(p) * p);
+  for (int a = 0; a < p; ++a)
+    for (int b = 0; b < p; ++b) {
+      double w = st.B[static_cast<size_t>(a) * p + b];
+      for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
+      W[static_cast<size_t>(a) * p + b] = w;
+    }
+  // Q (p x p, column-major basis vectors as rows of Qt) from Householder reflections of J'
+  std::vector<double> Jt(static_cast<size_t>(p) * m);  // column i = grad c_i
+  for (int i = 0; i < m; ++i)
+    for (int a = 0; a < p; ++a) {
+      double t = cons[i].term1[a];
+      for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y[b];
+      Jt[static_cast<size_t>(i) * p + a] = t;
+    }
+  std::vector<double> Qt(static_cast<size_t>(p) * p, 0.0);  // rows = orthonormal basis
+  for (int a = 0; a < p; ++a) Qt[static_cast<size_t>(a) * p + a] = 1.0;
+  std::vector<double> v(p);
+  for (int i = 0; i < m; ++i) {
+    double* col = Jt.data() + static_cast<size_t>(i) * p;
+    double nrm = 0.0;
+    for (int a = i; a < p; ++a) nrm += col[a] * col[a];
+    nrm = std::sqrt(nrm);
+    if (nrm == 0.0) continue;
+    const double alpha = col[i] > 0 ? -nrm : nrm;
+    std::fill(v.begin(), v.end(), 0.0);
+    for (int a = i; a < p; ++a) v[a] = col[a];
+    v[i] -= alpha;
+    double vv = 0.0;
+    for (int a = i; a < p; ++a) vv += v[a] * v[a];
+    if (vv == 0.0) continue;
+    auto reflect = [&](double* x) {  // x -= 2 v (v.x) / (v.v)
+      double t = 0.0;
+      for (int a = i; a < p; ++a) t += v[a] * x[a];
+      t = 2.0 * t / vv;
+      for (int a = i; a < p; ++a) x[a] -= t * v[a];
+    };
+    for (int k = i; k < m; ++k) reflect(Jt.data() + static_cast<size_t>(k) * p);
+    // accumulate H_i ... applied to e_r: Q = H_0 H_1 ... ; rows of Qt are Q' rows => reflect rows
+    for (int r = 0; r < p; ++r) reflect(Qt.data() + static_cast<size_t>(r) * p);
+  }
+  // Qt row r holds (Q' e_r)' ... with reflections applied to rows, Qt = I H_0 H_1 ... = Q, so
+  // the null space of J is spanned by columns m..p-1 of Q
+  const int nz = p - m;
+  std::vector<double> N(static_cast<size_t>(p) * nz);
+  for (int a = 0; a < p; ++a)
+    for (int c = 0; c < nz; ++c) N[static_cast<size_t>(a) * nz + c] = Qt[static_cast<size_t>(a) * p + m + c];
+  std::vector<double> WN(static_cast<size_t>(p) * nz, 0.0), Rm(static_cast<size_t>(nz) * nz, 0.0);
+  for (int a = 0; a < p; ++a)
+    for (int c = 0; c < nz; ++c) {
+      double t = 0.0;
+      for (int b = 0; b < p; ++b) t += W[static_cast<size_t>(a) * p + b] * N[static_cast<size_t>(b) * nz + c];
+      WN[static_cast<size_t>(a) * nz + c] = t;
+    }
+  double dmax = 0.0;
+  for (int c = 0; c < nz; ++c)
+    for (int d = 0; d < nz; ++d) {
+      double t = 0.0;
+      for (int a = 0; a < p; ++a) t += N[static_cast<size_t>(a) * nz + c] * WN[static_cast<size_t>(a) * nz + d];
+      Rm[static_cast<size_t>(c) * nz + d] = t;
+      if (c == d) dmax = std::max(dmax, std::fabs(t));
+    }
+  const double shift = 1e-10 * dmax;
+  for (int c = 0; c < nz; ++c) {  // in-place Cholesky
+    double d = Rm[static_cast<size_t>(c) * nz + c] + shift;
+    for (int k = 0; k < c; ++k) d -= Rm[static_cast<size_t>(c) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    Rm[static_cast<size_t>(c) * nz + c] = d;
+    for (int r = c + 1; r < nz; ++r) {
+      double t = Rm[static_cast<size_t>(r) * nz + c];
+      for (int k = 0; k < c; ++k) t -= Rm[static_cast<size_t>(r) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
+      Rm[static_cast<size_t>(r) * nz + c] = t / d;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
 KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, const QuadCon* cons,
                      const double* y0, double* y, int max_iter) {
   KKTResult res;
@@ -175,14 +419,12 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   }
   st.tau.assign(m, 0.0);
 
-  const int n = p + m;
-  std::vector<double> lam(m, 0.0), J(static_cast<size_t>(m) * p), F(n), Fn(n), K, rhs(n), yn(p),
-      ln(m);
-  // least-squares multipliers at y0: (J J') lam = -J grad f
-  st.residual(cons, y, lam.data(), F.data(), J);
-  if (m > 0) {
-    std::vector<double> JJ(static_cast<size_t>(m) * m);
-    std::vector<double> r(m);
+  // least-squares multipliers at a start point: (J J') lam = -J grad f
+  auto init_lam = [&](const double* ys, std::vector<double>& lam) {
+    lam.assign(m, 0.0);
+    if (m == 0) return;
+    std::vector<double> J(static_cast<size_t>(m) * p), F(p + m), JJ(static_cast<size_t>(m) * m), r(m);
+    st.residual(cons, ys, lam.data(), F.data(), J);
     for (int i = 0; i < m; ++i) {
       for (int k = 0; k < m; ++k) {
         double t = 0.0;
@@ -195,100 +437,52 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
     }
     if (lu_solve(m, JJ, r.data()))
       for (int i = 0; i < m; ++i) lam[i] = r[i];
-  }
-  bool converged = false;
-  int it = 0;
-  for (; it < max_iter; ++it) {
-    // offsets: a few ulps of each constraint's rounding scale, so that the COMPUTED value
-    // lands <= 0 (the reference's checker is a signed max against ctol, solvers.py:14-18,267)
-    for (int i = 0; i < m; ++i) st.tau[i] = 8.0 * DBL_EPSILON * con_scale(cons[i], p, y);
-    st.residual(cons, y, lam.data(), F.data(), J);
-    const double fn = norm2(F.data(), n);
-    if (!std::isfinite(fn)) { res.finite = false; break; }
-    {  // converged at the rounding floor: the gradient part of F within 64 ulps of its terms'
-       // scale and every constraint at its target (c_i in [-2 tau_i, 0]).  Newton steps from
-       // here are noise; the line search would backtrack ~30 times per step (~60 us at p = 30)
-      double gs = 0.0, gn = 0.0;
-      for (int a = 0; a < p; ++a) {
-        double t = std::fabs(st.b0[a]);
-        for (int b = 0; b < p; ++b) t += std::fabs(st.B[static_cast<size_t>(a) * p + b] * y[b]);
-        for (int i = 0; i < m; ++i) t += std::fabs(J[static_cast<size_t>(i) * p + a] * lam[i]);
-        gs = std::max(gs, t);
-        gn = std::max(gn, std::fabs(F[a]));
-      }
-      bool cons_ok = true;
-      for (int i = 0; i < m; ++i) cons_ok = cons_ok && std::fabs(F[p + i]) <= st.tau[i];
-      if (cons_ok && gn <= 64.0 * DBL_EPSILON * gs) {
-        converged = true;
-        break;
-      }
-    }
-    K.assign(static_cast<size_t>(n) * n, 0.0);
+  };
+  // accepted: a run that reached the rounding floor, or stopped otherwise at a point that passes
+  // the first-order test; and in either case a constrained minimum (second-order test)
+  auto accept = [&](const Run& run, const double* yr, std::vector<double>& lam) {
+    if (run.stop == Stop::kSingular || run.stop == Stop::kNonFinite || run.stop == Stop::kIterLimit) return false;
     for (int a = 0; a < p; ++a)
-      for (int b = 0; b < p; ++b) {
-        double w = st.B[static_cast<size_t>(a) * p + b];
-        for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
-        K[static_cast<size_t>(a) * n + b] = w;
-      }
-    for (int i = 0; i < m; ++i)
-      for (int a = 0; a < p; ++a) {
-        K[static_cast<size_t>(a) * n + p + i] = J[static_cast<size_t>(i) * p + a];
-        K[static_cast<size_t>(p + i) * n + a] = J[static_cast<size_t>(i) * p + a];
-      }
-    for (int r = 0; r < n; ++r) rhs[r] = -F[r];
-    if (!lu_solve(n, K, rhs.data())) { res.message = SPIS_MSG_SINGULAR_C; break; }
-    {  // a Newton step below the stopping size: take it unless it raises ||F||, and stop (no
-       // backtracking: at roundoff level the sufficient-decrease test cannot pass and would cost
-       // 40 residual evaluations)
-      double step = 0.0, ymax = 0.0;
-      for (int a = 0; a < p; ++a) {
-        step = std::max(step, std::fabs(rhs[a]));
-        ymax = std::max(ymax, std::fabs(y[a] + rhs[a]));
-      }
-      if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax)) {
-        for (int a = 0; a < p; ++a) yn[a] = y[a] + rhs[a];
-        for (int i = 0; i < m; ++i) ln[i] = lam[i] + rhs[p + i];
-        st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
-        const double fnew = norm2(Fn.data(), n);
-        if (std::isfinite(fnew) && fnew <= fn)
-          for (int a = 0; a < p; ++a) y[a] = yn[a];
-        converged = true;
-        ++it;
-        break;
-      }
-    }
-    double alpha = 1.0;
-    double fnew = 0.0;
-    // <= 10 halvings: once the Newton residual sits at its rounding floor (||grad f|| ~ eps ||B|| ||y||)
-    // the direction is noise, and a step of alpha < 1e-3 only moves y by roundoff (40 halvings cost
-    // ~60 us per constrained step at p = 30)
-    for (int ls = 0; ls < 40; ++ls) {
-      for (int a = 0; a < p; ++a) yn[a] = y[a] + alpha * rhs[a];
-      for (int i = 0; i < m; ++i) ln[i] = lam[i] + alpha * rhs[p + i];
-      st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
-      fnew = norm2(Fn.data(), n);
-      if (std::isfinite(fnew) && fnew <= (1.0 - 1e-4 * alpha) * fn) break;
-      alpha *= 0.5;
-    }
-    double step = 0.0, ymax = 0.0;
-    for (int a = 0; a < p; ++a) {
-      step = std::max(step, std::fabs(yn[a] - y[a]));
-      ymax = std::max(ymax, std::fabs(yn[a]));
-    }
-    if (std::isfinite(fnew) && fnew <= fn) {
-      for (int a = 0; a < p; ++a) y[a] = yn[a];
-      for (int i = 0; i < m; ++i) lam[i] = ln[i];
-    }
-    if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax) || !(fnew < fn)) {
-      converged = true;
-      ++it;
-      break;
-    }
+      if (!std::isfinite(yr[a])) return false;
+    if (run.stop != Stop::kFloor && !first_order_ok(st, cons, yr, lam)) return false;
+    return second_order_ok(st, cons, yr, lam);
+  };
+
+  // 1) warm start at the reference's y0 (solvers.py:225-227), as SLSQP
+  std::vector<double> lam;
+  init_lam(y, lam);
+  Run r1 = newton_run(st, cons, y, lam, max_iter);
+  res.iterations = r1.iterations;
+  if (accept(r1, y, lam)) return res;
+
+  // 2) restart from the unconstrained minimiser (R y = g), the point SLSQP's first QP step
+  //    heads for
+  std::vector<double> y2(p), lam2;
+  for (int i = p - 1; i >= 0; --i) {
+    double t = g[i];
+    for (int k = i + 1; k < p; ++k) t -= R[static_cast<size_t>(k) * ld + i] * y2[k];
+    const double d = R[static_cast<size_t>(i) * ld + i];
+    y2[i] = d != 0.0 ? t / d : 0.0;
   }
-  res.iterations = it;
-  for (int a = 0; a < p; ++a)
-    if (!std::isfinite(y[a])) res.finite = false;
-  if (res.message == 0 && !converged) res.message = SPIS_MSG_ITER_LIMIT;
+  init_lam(y2.data(), lam2);
+  Run r2 = newton_run(st, cons, y2.data(), lam2, max_iter);
+  res.iterations += r2.iterations;
+  if (accept(r2, y2.data(), lam2)) {
+    for (int a = 0; a < p; ++a) y[a] = y2[a];
+    return res;
+  }
+  // neither start reached a verified constrained minimum: report it (the caller warns, as the
+  // reference does for a non-success SLSQP exit, :280-284) and keep the finite point with the
+  // smaller KKT residual
+  bool f1 = r1.stop != Stop::kNonFinite, f2 = r2.stop != Stop::kNonFinite;
+  for (int a = 0; a < p; ++a) {
+    f1 = f1 && std::isfinite(y[a]);
+    f2 = f2 && std::isfinite(y2[a]);
+  }
+  if (f2 && (!f1 || r2.fn < r1.fn))
+    for (int a = 0; a < p; ++a) y[a] = y2[a];
+  if (!f1 && !f2) res.finite = false;
+  res.message = (r1.stop == Stop::kSingular && r2.stop == Stop::kSingular) ? SPIS_MSG_SINGULAR_C : SPIS_MSG_ITER_LIMIT;
   return res;
 }
 

@@ -222,6 +222,8 @@ struct spis_workspace {
   std::vector<ConCache> con;
   std::vector<double> y_all;  // k*k host copy of every iteration's y
   std::vector<double> H;      // (k+1) x k column-major Hessenberg (host)
+  std::vector<QuadCon> last_con;  // reduced class-form constraints of the last constrained step
+  int last_con_p = 0;             // its p (0: none)
   int steps = 0;
   int n_iter_y = 0;           // iterations with a stored y
   bool broke_at_start = false;
@@ -1635,6 +1637,34 @@ extern "C" int spis_workspace_basis(spis_workspace* ws, int32_t p, double* Z_hos
   })
 }
 
+extern "C" int spis_workspace_hessenberg(spis_workspace* ws, int32_t p, double* H_host) {
+  ABI_GUARD({
+    if (!ws || !H_host || p < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    if (p > ws->n_iter_y) return fail(SPIS_ERR_ARG, "H has %d columns (asked %d)", ws->n_iter_y, p);
+    const int k = ws->k;
+    for (int r = 0; r <= p; ++r)
+      for (int cc = 0; cc < p; ++cc)
+        H_host[static_cast<size_t>(r) * p + cc] = r <= cc + 1 ? ws->H[static_cast<size_t>(cc) * (k + 1) + r] : 0.0;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_workspace_constraint_terms(spis_workspace* ws, int32_t ci, int32_t* p_out, double* term0,
+                                               double* term1, double* term2) {
+  ABI_GUARD({
+    if (!ws || !p_out || !term0 || !term1 || !term2) return fail(SPIS_ERR_ARG, "null argument");
+    if (ws->last_con_p == 0 || ci < 0 || ci >= static_cast<int32_t>(ws->last_con.size()))
+      return fail(SPIS_ERR_ARG, "no reduced constraint %d (the run had %zu at its last constrained step)", ci,
+                  ws->last_con.size());
+    const QuadCon& q = ws->last_con[ci];
+    *p_out = ws->last_con_p;
+    *term0 = q.term0;
+    std::copy(q.term1.begin(), q.term1.end(), term1);
+    std::copy(q.term2.begin(), q.term2.end(), term2);
+    return SPIS_OK;
+  })
+}
+
 // ------------------------------------------------------------------------------------------------
 // the solver
 // ------------------------------------------------------------------------------------------------
@@ -1979,6 +2009,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ws->broke_at_start = false;
     ws->y_all.assign(static_cast<size_t>(k) * k, 0.0);
     ws->H.assign(static_cast<size_t>(k + 1) * k, 0.0);
+    ws->last_con.clear();
+    ws->last_con_p = 0;
     const bool use_cb = o->conls_fn != nullptr;
     if (!use_cb && o->n_constraints > 0) ST_TRY(ensure_con_cache(ws, o->n_constraints, o->constraints));
 
@@ -2033,8 +2065,14 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // constraints on the fused single-GPU path, no separate preconditioned basis
     int nlin = 0;
     for (int i = 0; i < (use_cb ? 0 : o->n_constraints); ++i) nlin += o->constraints[i].v_dev ? 1 : 0;
+    // never beside a persistent MGS chain (K2p / K2b): the chain needs all of its workgroups
+    // resident at once, and a concurrent Gram could hold the CU slots its last workgroups wait
+    // for (the chain would then time out and fail the solve with SPIS_ERR_STATE)
+    const bool chain_runs = !fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, c->mgs_chain == 2) &&
+                            !(c->cgs2 && k <= kCgsMax);
     const bool early = c->early_con && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && !c->comm &&
-                       k + 1 <= 64 && nlin <= 4 && !c->force_generic_gram && ws->Zb == ws->Q && k >= 4;
+                       k + 1 <= 64 && nlin <= 4 && !c->force_generic_gram && ws->Zb == ws->Q && k >= 4 &&
+                       !chain_runs;
     bool pre_launched = false;
     auto launch_early = [&]() -> int {
       ST_TRY(ensure_host_buf(&c->pre_pinned, &c->pre_pinned_len, con_result_len(o->n_constraints, k)));
@@ -2128,6 +2166,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         } else {
           KKTResult kr = kkt_newton(p, qr.R(), qr.ld(), qr.g(), m_active, cons.data(), y0.data(), ycon.data());
           msg = kr.message;
+          ws->last_con.assign(cons.begin(), cons.begin() + m_active);
+          ws->last_con_p = p;
         }
         bool has_nan = false;
         for (int a = 0; a < p; ++a) has_nan = has_nan || std::isnan(ycon[a]);

@@ -241,24 +241,47 @@ def _matrix_key(A):
     return (id(A), A.shape, int(A.nnz), A.data.ctypes.data, A.indices.ctypes.data, A.indptr.ctypes.data)
 
 
+_FP_SAMPLES = 4096
+
+
+def fingerprint(A):
+    """Cheap content sample of a sparse matrix: up to 4096 evenly strided entries of ``data``
+    and ``indices`` plus ``indptr``'s ends (~10 us at any size).  Cache entries carry it, so an
+    in-place change of ``A.data`` / ``A.indices`` at a sampled position is seen and re-uploaded;
+    a change confined to unsampled entries is not: call :func:`invalidate` after modifying a
+    matrix in place (INTEGRATION.md)."""
+    nnz = int(A.nnz)
+    s = max(1, nnz // _FP_SAMPLES)
+    return hash((A.data[::s].tobytes(), A.indices[::s].tobytes(), int(A.indptr[0]), int(A.indptr[-1])))
+
+
+def _cached(cache, key, A, fp, make):
+    """Per-object cache entry ``key -> (fingerprint, value)``, evicted when ``A`` is collected
+    (so a later object that reuses ``id(A)`` can never hit it) and rebuilt on a changed
+    fingerprint."""
+    hit = cache.get(key)
+    if hit is not None and hit[0] == fp:
+        return hit[1]
+    val = make()
+    if hit is None:
+        try:
+            weakref.finalize(A, cache.pop, key, None)
+        except TypeError:  # not weak-referenceable: keep until invalidate()
+            pass
+    cache[key] = (fp, val)
+    return val
+
+
 def device_matrix(A, ctx=None) -> DeviceMatrix:
-    """HBM copy of SciPy CSR ``A`` (cached for the lifetime of ``A``)."""
+    """HBM copy of SciPy CSR ``A``, cached for the lifetime of ``A`` (keyed on identity, buffer
+    addresses and a content :func:`fingerprint`; after an in-place change call :func:`invalidate`)."""
     if isinstance(A, DeviceMatrix):
         return A
     ctx = ctx or get_context()
     if not sps.issparse(A):
         return DeviceMatrix(ctx, A)
     key = _matrix_key(A) + (ctx.device,)
-    hit = _MATRIX_CACHE.get(key)
-    if hit is not None:
-        return hit
-    dm = DeviceMatrix(ctx, A)
-    _MATRIX_CACHE[key] = dm
-    try:
-        weakref.finalize(A, _MATRIX_CACHE.pop, key, None)
-    except TypeError:  # not weak-referenceable: keep until invalidate()
-        pass
-    return dm
+    return _cached(_MATRIX_CACHE, key, A, fingerprint(A), lambda: DeviceMatrix(ctx, A))
 
 
 class DeviceILU:
@@ -358,13 +381,28 @@ def device_ilu(pre, ctx=None) -> DeviceILU:
     return d
 
 
+_ZERO_CACHE: dict = {}
+
+
+def is_zero_matrix(M):
+    """Whether a sparse matrix has no nonzero value (the reference wrappers' mass ``0*A`` keeps
+    A's pattern with all-zero values).  O(nnz) once per matrix, then cached like
+    :func:`device_matrix`: evicted with the object, rebuilt on a changed :func:`fingerprint`."""
+    if M.nnz == 0:
+        return True
+    return _cached(_ZERO_CACHE, _matrix_key(M), M, fingerprint(M), lambda: not np.any(M.data))
+
+
 def invalidate(A=None):
-    """Forget cached uploads (of ``A``, or all)."""
-    if A is None:
-        _MATRIX_CACHE.clear()
-        return
-    for key in [k for k in _MATRIX_CACHE if k[0] == id(A)]:
-        _MATRIX_CACHE.pop(key, None)
+    """Forget cached uploads and zero tests (of ``A``, or all).  Needed after changing a matrix's
+    values or pattern in place: the caches key on identity, buffer addresses and a sampled
+    :func:`fingerprint`, not on the full contents."""
+    for cache in (_MATRIX_CACHE, _ZERO_CACHE):
+        if A is None:
+            cache.clear()
+            continue
+        for key in [k for k in cache if k[0] == id(A)]:
+            cache.pop(key, None)
 
 
 def device_vector(v, ctx=None, capacity=None) -> DeviceVector:

@@ -40,7 +40,8 @@ import scipy.optimize as spo
 import scipy.sparse as sps
 
 from . import _lib
-from .device import DeviceMatrix, DeviceVector, choose_ilu, device_matrix, device_vector, get_context, is_superlu
+from .device import (DeviceMatrix, DeviceVector, choose_ilu, device_matrix, device_vector, get_context, is_superlu,
+                     is_zero_matrix)
 
 log = logging.getLogger("structurepreservingiterativesolvers_amd")
 
@@ -114,24 +115,15 @@ def _reduce_on_device(const, x0, Z):
 # ------------------------------------------------------------------------------------------------
 # device-side constraint descriptors
 # ------------------------------------------------------------------------------------------------
-_ZERO_CACHE: dict = {}
-
-
 def _is_zero_matrix(M):
-    """O(1) for an empty sparse matrix or a device matrix; O(nnz) (cached per object) otherwise."""
+    """O(1) for an empty sparse matrix or a device matrix; O(nnz) once per sparse object
+    (:func:`~.device.is_zero_matrix`) otherwise."""
     if M is None:
         return True
     if isinstance(M, DeviceMatrix):
         return M.all_zero or M.nnz == 0
     if sps.issparse(M):
-        if M.nnz == 0:
-            return True
-        key = (id(M), M.nnz)
-        hit = _ZERO_CACHE.get(key)
-        if hit is None:
-            hit = not np.any(M.data)
-            _ZERO_CACHE[key] = hit
-        return hit
+        return is_zero_matrix(M)
     return not np.any(M)
 
 
@@ -229,6 +221,28 @@ class IterateList(collections.abc.Sequence):
         _lib.check(self._ctx.L.spis_workspace_basis(self._ws, p, out.ctypes.data_as(C.POINTER(C.c_double))),
                    "spis_workspace_basis")
         return out
+
+    def hessenberg(self, p):
+        """``H[:p+1, :p]`` of the run (``solvers.py:181``), as the host least squares saw it."""
+        out = np.empty((p + 1, p))
+        _lib.check(self._ctx.L.spis_workspace_hessenberg(self._ws, p, out.ctypes.data_as(C.POINTER(C.c_double))),
+                   "spis_workspace_hessenberg")
+        return out
+
+    def constraint_terms(self, ci):
+        """``(p, term0, term1, term2)`` of class-form constraint ``ci`` at the run's last
+        constrained step (``solvers.py:33-36``), as the host KKT solve received them."""
+        k = self._k
+        p = C.c_int32()
+        t0 = C.c_double()
+        t1 = np.zeros(k)
+        t2 = np.zeros(k * k)
+        PD = C.POINTER(C.c_double)
+        _lib.check(self._ctx.L.spis_workspace_constraint_terms(self._ws, ci, C.byref(p), C.byref(t0),
+                                                               t1.ctypes.data_as(PD), t2.ctypes.data_as(PD)),
+                   "spis_workspace_constraint_terms")
+        q = p.value
+        return q, t0.value, t1[:q].copy(), t2[: q * q].reshape(q, q).copy()
 
     def release(self):
         """Free the device basis now (materialised entries stay available)."""
@@ -421,6 +435,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     final = xf if device_io else xf.numpy()
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
     xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)
+    xs.beta = float(res[0])  # ||r0||: with hessenberg(p), the exact LS problem of every step
     xs.stamps = stamps  # host clock: per-iteration / constraint-step stamps, [4k] call start, [4k+1] end
     return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
                 stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)

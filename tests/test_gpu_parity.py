@@ -347,7 +347,9 @@ def test_early_constraint_reduction_bit_identical(spis):
     """SPIS_OPT_EARLY_CON: the final step's constraint reduction launched early on a third stream
     (after A_{k-2} or A_{k-1} is queued) gives the same bits as reducing when the step is reached,
     also when constrained steps start earlier (they wait for it) and when the solve stops before
-    the final step (the early reduction goes unused)."""
+    the final step (the early reduction goes unused).  The early reduction never runs beside a
+    persistent MGS chain (a concurrent kernel could hold CU slots the chain's workgroups wait
+    for), so the per-step MGS launches are selected here; with the chain on the option is inert."""
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.device import set_option
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
@@ -360,6 +362,7 @@ def test_early_constraint_reduction_bit_identical(spis):
     _, d = solvers.cgmres(A, b, np.zeros_like(b), k, tol=1e-19, conlist=cons)
     tols = (1e-19, d["res"][20] / 10)  # all k steps / constrained steps from j ~ 21 on, early stop
     try:
+        set_option("mgs_chain", False)
         for tol in tols:
             runs = []
             for mode in (0, 1, 2, 1):
@@ -369,8 +372,14 @@ def test_early_constraint_reduction_bit_identical(spis):
             for r in runs[1:]:
                 assert np.array_equal(r[0], runs[0][0]) and np.array_equal(r[1], runs[0][1]), tol
                 assert r[2:] == runs[0][2:], tol
+        # chain on: early_con is ignored (same bits as the chain run without it)
+        set_option("mgs_chain", True)
+        ref = solvers.cgmres(A, b, np.zeros_like(b), k, tol=1e-19, conlist=cons)[0]
+        set_option("early_con", "a_k-2")
+        assert np.array_equal(solvers.cgmres(A, b, np.zeros_like(b), k, tol=1e-19, conlist=cons)[0], ref)
     finally:
         set_option("early_con", False)
+        set_option("mgs_chain", True)
 
 
 def test_fused_dual_spmv_bit_identical(spis):
@@ -610,22 +619,64 @@ def test_restarted_cgmres_vs_oracle_loop(spis):
 
 
 def test_lkdvrk_gl3_vs_oracle_medium(spis):
-    """Config C4 shape (GL(3) block-stage, 3 lifted invariants) at M=400 vs the oracle."""
-    import oracle
+    """Config C4 shape (GL(3) block-stage, 3 lifted invariants) at M=400 vs the oracle.
+
+    Steps 1..29 (unconstrained) match the oracle within 10x the reference's own roundoff
+    envelope.  The final, constrained step is degenerate in the reference itself: the mass
+    constraint's term0 is exactly 0 and its term1 is pure roundoff (the Krylov vectors carry no
+    mass), so SLSQP enforces a hyperplane whose normal is noise, and the reference's x_30 moves
+    by 7.3e-4 ... 3.8e-3 under 1e-16 perturbations of b (8 seeds, CPU).  That step is therefore
+    checked on identical inputs: the device's own H, beta, y0 and reduced constraint terms,
+    solved by the reference's SLSQP (oracle), must give the device's y_30 to 1e-8; the iterate
+    must preserve the three invariants to 1e-12; and it must stay within 10x the reference's
+    8-seed envelope of the oracle's x_30."""
+    from oracle.cgmres_port import _slsqp
     from structurepreservingiterativesolvers_amd.lkdvRK import LinearSolver as rk_ls
     from structurepreservingiterativesolvers_amd.lkdvRK import assembly as ra
 
     dic, prob = ra.linforms(M=400, tstages=3)
     x0 = np.zeros_like(dic["b"])
-    x, d = rk_ls.cgmresWrapper(dic, x0, 30, prob=prob, tol=1e-19)
+    k = 30
+    x, d = rk_ls.cgmresWrapper(dic, x0, k, prob=prob, tol=1e-19)
     cons = rk_ls.constraints(dic, prob)
-    xr, dr, trace, bad = _oracle_run(dic["A"], dic["b"], x0, 30, tol=1e-19, conlist=cons)
-    # lkdvRK is roundoff-sensitive (the golden fixtures' envelope reaches 3.5e-3): the bound is
-    # the reference's own envelope at this size, as in test_golden
-    env = _envelope(dic["A"], dic["b"], x0, 30, 1e-19, cons)
-    if _oracle_prefix_match(d["x"].trace, trace, np.asarray(d["x"]), np.asarray(dr["x"]), env, bad=bad):
-        tol_f = max(1e-8, 10 * env[-1])
-        np.testing.assert_allclose(x, xr, atol=tol_f * np.linalg.norm(xr))
+    xr, dr, trace, bad = _oracle_run(dic["A"], dic["b"], x0, k, tol=1e-19, conlist=cons)
+    env = _envelope(dic["A"], dic["b"], x0, k, 1e-19, cons, seeds=tuple(range(8)))
+    xs, xrs = np.asarray(d["x"]), np.asarray(dr["x"])
+    assert d["steps"] == dr["steps"] == k and not bad
+    assert d["x"].trace[: k - 1] == trace[: k - 1] and d["x"].trace[-1] == (k - 1, "con") == trace[-1]
+    for i in range(1, k):
+        tol_i = max(1e-8, 10 * env[i])
+        assert np.linalg.norm(xs[i] - xrs[i]) <= tol_i * np.linalg.norm(xrs[i]), (i, tol_i)
+    # the final step on identical inputs
+    H = d["x"].hessenberg(k)
+    beta = d["x"].beta
+    rhs = np.zeros(k + 1)
+    rhs[0] = beta
+
+    def func(z):
+        F = rhs - H @ z
+        return np.inner(F, F)
+
+    def jac(z):
+        F = rhs - H @ z
+        return -2 * np.transpose(H) @ F
+
+    ys = d["x"].y
+    y0 = np.zeros(k)
+    y0[:-1] = ys[k - 2]
+    eq = []
+    for ci in range(len(cons)):
+        p, t0, t1, t2 = d["x"].constraint_terms(ci)
+        assert p == k
+        eq.append({"type": "eq", "fun": lambda z, t0=t0, t1=t1, t2=t2: t0 + t1 @ z + z @ t2 @ z,
+                   "jac": lambda z, t1=t1, t2=t2: t1 + 2 * z @ t2})
+    # SLSQP may end on "Iteration limit reached" here (ftol = 1e-24 on a degenerate constraint
+    # set; on the CPU it does so even when started at its own solution) with x converged to ~1e-10
+    sol = _slsqp(func, y0, jac, eq, 1e-24)
+    assert np.linalg.norm(ys[-1] - sol.x) <= 1e-8 * np.linalg.norm(sol.x)
+    assert func(ys[-1]) <= func(sol.x) * (1 + 1e-9)
+    _assert_invariants(cons, x)
+    assert np.linalg.norm(x - xr) <= max(1e-8, 10 * env[-1]) * np.linalg.norm(xr)
 
 
 def _assert_invariants(cons, x, rel=1e-12):

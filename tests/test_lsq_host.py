@@ -119,3 +119,62 @@ def test_kkt_overconstrained_returns_initial_guess(lsq):
     terms = [(1.0, np.array([1.0]), np.array([[0.0]]))] * 2
     y, msg, _ = kkt(lsq, H, 1.0, terms, np.array([0.25]))
     assert msg == 2 and y[0] == 0.25
+
+
+def test_kkt_rejects_constrained_maximum(lsq):
+    """Newton on the KKT system converges to any stationary point.  Warm-started next to the
+    constrained MAXIMUM of ||(2, 0) - y||^2 on the unit circle (y = (-1, 0), multiplier -3,
+    reduced Hessian negative), kkt_newton must reject it by its second-order test and return
+    the minimum (1, 0) that SLSQP finds, with a success message."""
+    import scipy.optimize as spo
+
+    H = np.array([[1.0, 0.0], [0.0, 1.0], [0.0, 0.0]])
+    terms = [(-1.0, np.zeros(2), np.eye(2))]
+    y0 = np.array([-1.0, 0.01])
+    y, msg, _ = kkt(lsq, H, 2.0, terms, y0)
+    assert msg == 0
+    np.testing.assert_allclose(y, [1.0, 0.0], atol=1e-12)
+    rhs = np.array([2.0, 0.0, 0.0])
+    sol = spo.minimize(lambda z: np.sum((rhs - H @ z) ** 2), y0, jac=lambda z: -2 * H.T @ (rhs - H @ z),
+                       constraints=[{"type": "eq", "fun": lambda z: z @ z - 1.0, "jac": lambda z: 2 * z}],
+                       method="SLSQP", options={"ftol": 1e-24, "maxiter": 1000})
+    np.testing.assert_allclose(y, sol.x, atol=1e-8)
+
+
+def test_kkt_lkdvrk_gl3_final_step_matches_slsqp(lsq):
+    """The constrained step of config C4's shape (lkdvRK GL(3), 3 lifted invariants) at M=400:
+    the oracle (the reference's arithmetic) builds H and the constraint terms of step j = 29,
+    and the Newton-KKT solution matches the reference's SLSQP on those identical inputs.  This
+    step is degenerate: the mass constraint's term0 is exactly 0 and its term1 is roundoff
+    (|term1| ~ 4e-15, the Krylov vectors carry no mass), so its Jacobian row is noise and the
+    solution's dependence on roundoff is the reference's own; on identical
+    inputs the two solvers still agree to ~1e-10."""
+    from oracle.cgmres_port import _slsqp
+    from structurepreservingiterativesolvers_amd.lkdvRK import LinearSolver as rk_ls
+    from structurepreservingiterativesolvers_amd.lkdvRK import assembly as ra
+
+    dic, prob = ra.linforms(M=400, tstages=3)
+    x0 = np.zeros_like(dic["b"])
+    cons = rk_ls.constraints(dic, prob)
+    k = 30
+    st = _Arnoldi(dic["A"], dic["b"], x0, k, None)
+    yk = None
+    for j in range(k):
+        st.extend(j)
+        _, func, jac = st.ls_objective(j)
+        y0 = np.zeros(j + 1)
+        if j:
+            y0[:-1] = yk
+        if j < k - 1:  # the reference's unconstrained steps (its warm starts, :225-235)
+            yk = _slsqp(func, y0, jac, [], 1e-24).x
+    Z = st.basis(k - 1)
+    terms = [ConstraintTerms(c, x0, Z) for c in cons]
+    sol = _slsqp(func, y0, jac, [t.as_slsqp() for t in terms], 1e-24)
+    assert sol.message == "Optimization terminated successfully"
+    y, msg, _ = kkt(lsq, st.H[: k + 1, :k], st.beta, [(t.term0, t.term1, t.term2) for t in terms], y0)
+    assert msg == 0
+    assert np.linalg.norm(y - sol.x) <= 1e-9 * np.linalg.norm(sol.x)
+    for t in terms:  # the signed checker passes (solvers.py:267)
+        assert lsq.lsq_con_value(k, t.term0, _p(t.term1), _p(t.term2), _p(y)) <= 1e-12
+    assert func(y) <= func(sol.x) * (1 + 1e-9)
+    assert abs(terms[0].term0) == 0.0 and np.linalg.norm(terms[0].term1) < 1e-12  # the degeneracy
