@@ -156,9 +156,9 @@ def main():
     ap.add_argument("--gemv-sync", type=int, default=1, choices=[1, 2],
                     help="how the dual SpMV waits for the side-stream GEMV (SPIS_OPT_OVERLAP_GEMV): "
                          "1 stream write/wait on a device word, 2 the GEMV launch's completion event")
-    ap.add_argument("--chain", type=int, default=2, choices=[0, 1, 2],
+    ap.add_argument("--chain", type=int, default=3, choices=[0, 1, 2, 3],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
-                         "workgroup 0, 2 with a dedicated gathering workgroup")
+                         "workgroup 0, 2 with a dedicated gathering workgroup, 3 pipelined (dots one step early)")
     ap.add_argument("--nt-basis", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
     ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],

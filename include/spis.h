@@ -131,11 +131,14 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   boundaries), 2 = row chunks with their distinct columns (the basis rows of those columns
  *   staged in LDS once per chunk; a matrix with a row of > 64 entries or > 176 distinct columns
  *   falls back to 1; measured 12% slower than 1 at C3), 0 = the CSR itself.
- * SPIS_OPT_MGS_CHAIN (default 2): each Arnoldi step's MGS chain + normalise runs as one persistent
+ * SPIS_OPT_MGS_CHAIN (default 3): each Arnoldi step's MGS chain + normalise runs as one persistent
  *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 2 = the
  *   partials are gathered by a dedicated workgroup that holds no slice (N <= 2^20 - 4096), 1 = by
  *   workgroup 0; 0 = one launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
- *   so results differ from the per-step launches at roundoff level.
+ *   so results differ from the per-step launches at roundoff level.  3 = the pipelined chain:
+ *   MGS's projections and updates, each dot product evaluated one step early by the distributive
+ *   law (h_{i+1} = q_{i+1}.w^{(i)} - h_i q_{i+1}.q_i), so two exchanges overlap; roundoff differs
+ *   from MGS's (N <= 2^20 - 4096; mode 2's K2b beyond).
  * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
  *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
  *   The dual SpMV waits for it through a stream write / wait on a device word (1) or through the

@@ -994,6 +994,303 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
   if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
 }
 
+// ---------------------------------------------------------------------------------------------
+// K2q: pipelined MGS chain (SPIS_OPT_MGS_CHAIN = 3).  MGS's projections, with each dot product
+// evaluated one step early by the distributive law:
+//     h_{i+1} = q_{i+1} . w^{(i+1)} = q_{i+1} . w^{(i)} - h_i (q_{i+1} . q_i),
+// w^{(i+1)} = w^{(i)} - h_i q_i (the update itself is MGS's, in registers, contraction off).  The
+// partial of q_{i+1} . w^{(i)} needs only h_{i-1}, so the exchange that produces h_{i+1} starts
+// while the one producing h_i is still in flight: two exchanges overlap and each Arnoldi step
+// waits for about half a round trip per MGS step instead of a whole one.  The sub-diagonal Gram
+// entries g_m = q_m . q_{m-1} do not change once both vectors exist: chain j computes the new one,
+// g_j (partials published beside those of h_j), and keeps it in gsub[j] for the chains after it.
+// The dedicated gathering workgroup (the last) sums each step's partials in a fixed order, forms
+// h_m = A_m - h_{m-1} g_m (every workgroup gets the same bits) and publishes it; it also writes
+// H[:, j] to the host.  Exact arithmetic: the identity above, no orthogonality assumed.  Rounding:
+// the error of h_{i+1} is eps |w^{(i)}| instead of MGS's eps |w^{(i+1)}|.
+// Basis slices rotate through NS register slots (5; 4 at PER 8, where 5 spill) without moves: the step body is instantiated
+// for each ring position (vector q_m lives in slot m % NS; q_{i+NS-1} is loaded into q_{i-1}'s
+// slot right after the update that consumed it, NS - 2 steps before it is needed).
+// Slots: E_m (the exchange producing h_m, m = 1..j; E_{j+1} = ||w||^2) uses tag base + m, partial
+// ring m % 4, h ring m % 4; g_j's partials have their own granules.  Ring safety: a workgroup
+// publishes E_m after it has read h_{m-2}, which the gatherer published after reading E_{m-4}'s
+// partials; the gatherer publishes h_m after reading E_m, which every workgroup publishes after
+// it read h_{m-4} (and earlier h's).
+// ---------------------------------------------------------------------------------------------
+template <int PER, int NS>
+__global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
+    int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
+    const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
+    unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
+    unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
+    bool nt) {
+#pragma clang fp contract(off)
+  __shared__ double s_wave[8];
+  __shared__ double s_h;
+  __shared__ int s_fail;
+  const int G = gridDim.x;
+  const int GD = G - 1;  // data workgroups; the last one gathers
+  const int tid = threadIdx.x;
+  const bool agg = static_cast<int>(blockIdx.x) == GD;
+  const bool data = tid < kBlock && !agg;
+  const int64_t npair = n >> 1;
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBlock * PER + tid;
+  const bool tail = (n & 1) && blockIdx.x == 0 && tid == 0;  // odd element: workgroup 0, lane 0
+  unsigned long long* aslots = gran;                             // 4 x 2 kChainMaxWG
+  unsigned long long* gslots = gran + 8 * kChainMaxWG;           // 2 kChainMaxWG (g_j)
+  unsigned long long* hslots = gran + 10 * kChainMaxWG;          // 4 x 2
+  const unsigned base = *epoch;
+  double2 y[PER];
+  double2 S[NS][PER];
+  double yt = 0.0, st[NS];
+#pragma unroll
+  for (int r = 0; r < NS; ++r) st[r] = 0.0;
+  auto load = [&](double2 (&r)[PER], const double* v) {
+    const double2* v2 = reinterpret_cast<const double2*>(v);
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (data && p0 + k * kBlock < npair) r[k] = ld_basis(v2 + p0 + k * kBlock, nt);
+  };
+  if (!agg) {
+    load(y, w);
+    if (tail) yt = w[n - 1];
+#pragma unroll
+    for (int m = 0; m < NS - 1; ++m)
+      if (m <= j) {
+        load(S[m], Q + static_cast<int64_t>(m) * pitch);
+        if (tail) st[m] = Q[static_cast<int64_t>(m) * pitch + n - 1];
+      }
+  }
+  if (tid == 0) s_fail = 0;
+  const double h0 = chain_sum_partials(part_in, n_in, s_wave);
+  if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
+    const double t = chain_sum_partials(xpart, n_x, s_wave);
+    if (tid == 0) publish(x_out, t, flag, seq);
+  }
+
+  if (agg) {  // ---- the gatherer: one wave sums, forms h_m and publishes it
+    if (tid >= 64) return;
+    const int lane = tid;
+    // the whole column H[:, j] is written by this lane; H[j+1, j] last, behind a system-scope
+    // release, so a host that sees it (the solver's speculative update, spis.cpp) sees the column
+    if (lane == 0) hcol[0] = h0;
+    double hprev = h0;
+    for (int m = 1; m <= j + 1; ++m) {
+      const unsigned tag = base + static_cast<unsigned>(m);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      auto sweep = [&](const unsigned long long* slots, double* out) -> bool {
+        unsigned long long g[8];
+        bool all_ok = false;
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int idx = lane + 64 * k;
+            g[k] = idx < 2 * GD ? chain_load(slots + idx) : (static_cast<unsigned long long>(tag) << 32);
+            ok &= static_cast<unsigned>(g[k] >> 32) == tag;
+          }
+          if (__all(ok)) {
+            all_ok = true;
+            break;
+          }
+          if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // lane pairs (2m, 2m+1) of round k hold partial (64 k + 2 m) / 2
+          const unsigned lo = static_cast<unsigned>(g[k]);
+          const unsigned hi =
+              static_cast<unsigned>(__shfl_xor(static_cast<int>(static_cast<unsigned>(g[k])), 1, 64));
+          const double v =
+              __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+          if ((lane & 1) == 0 && lane + 64 * k < 2 * GD) acc += v;
+        }
+        *out = wave_sum_dpp(acc);
+        return all_ok;
+      };
+      double A = 0.0;
+      bool ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &A);
+      double hm;
+      if (m <= j) {
+        double g = 0.0;
+        if (m == j) {
+          ok = ok && sweep(gslots, &g);
+          if (lane == 0) gsub[j] = g;
+        } else {
+          g = gsub[m];
+        }
+        const double t = hprev * g;
+        hm = A - t;
+      } else {
+        hm = A;  // E_{j+1}: ||w^{(j+1)}||^2, square-rooted by every workgroup
+      }
+      if (!ok) {
+        if (lane == 0) atomicOr(err, 1u);
+        hm = 0.0;  // the data workgroups time out as well and report the failure
+      }
+      if (lane == 0) {
+        const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(hm));
+        unsigned long long* hs = hslots + 2 * (m & 3);
+        chain_store(hs, tag, static_cast<unsigned>(bits));
+        chain_store(hs + 1, tag, static_cast<unsigned>(bits >> 32));
+        if (m <= j) {
+          hcol[m] = hm;
+        } else {
+          __threadfence_system();
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(hcol + m),
+                             static_cast<unsigned long long>(__double_as_longlong(sqrt(hm))), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if (!ok) return;
+      hprev = hm;
+    }
+    if (lane == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
+    return;
+  }
+
+  // ---- data workgroups
+  // h_m from the gatherer (exchange wave polls, every wave joins the barrier); false on timeout
+  auto wait_h = [&](int m, double* out) -> bool {
+    const unsigned tag = base + static_cast<unsigned>(m);
+    if (tid >= kBlock) {
+      const int lane = tid - kBlock;
+      const unsigned long long* hs = hslots + 2 * (m & 3);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned long long g = 0;
+      bool ok = false;
+      for (unsigned spins = 0;; ++spins) {
+        g = lane < 2 ? chain_load(hs + lane) : (static_cast<unsigned long long>(tag) << 32);
+        if (__all(static_cast<unsigned>(g >> 32) == tag)) {
+          ok = true;
+          break;
+        }
+        if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) break;
+      }
+      const unsigned lo = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 0, 64));
+      const unsigned hi = static_cast<unsigned>(__shfl(static_cast<int>(static_cast<unsigned>(g)), 1, 64));
+      if (lane == 0) {
+        s_h = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+        if (!ok) {
+          s_fail = 1;
+          atomicOr(err, 1u);
+        }
+      }
+    }
+    __syncthreads();
+    *out = s_h;
+    const bool failed = s_fail != 0;
+    __syncthreads();  // s_h is rewritten by the next wait
+    return !failed;
+  };
+  // workgroup partial(s) -> granules {tag, half} (sc1 stores from a data wave)
+  auto publish2 = [&](double pa, double pb, bool with_b, int m) {
+    const double wa = wave_sum_dpp(pa);
+    const double wb = with_b ? wave_sum_dpp(pb) : 0.0;
+    if (data && (tid & 63) == 0) {
+      s_wave[tid >> 6] = wa;
+      s_wave[4 + (tid >> 6)] = wb;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned tag = base + static_cast<unsigned>(m);
+      const double ta = ((s_wave[0] + s_wave[1]) + s_wave[2]) + s_wave[3];
+      const unsigned long long ba = static_cast<unsigned long long>(__double_as_longlong(ta));
+      unsigned long long* sl = aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG + 2 * blockIdx.x;
+      chain_store(sl, tag, static_cast<unsigned>(ba));
+      chain_store(sl + 1, tag, static_cast<unsigned>(ba >> 32));
+      if (with_b) {
+        const double tb = ((s_wave[4] + s_wave[5]) + s_wave[6]) + s_wave[7];
+        const unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(tb));
+        chain_store(gslots + 2 * blockIdx.x, tag, static_cast<unsigned>(bb));
+        chain_store(gslots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bb >> 32));
+      }
+    }
+  };
+  // y -= h q (MGS's update, contraction off)
+  auto update = [&](double h, const double2 (&q)[PER], double qt) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (data && p0 + k * kBlock < npair) {
+        const double a0 = h * q[k].x, a1 = h * q[k].y;
+        y[k].x = y[k].x - a0;
+        y[k].y = y[k].y - a1;
+      }
+    if (tail) {
+      const double a = h * qt;
+      yt = yt - a;
+    }
+  };
+  // one MGS step at ring position R = i % NS; false once the chain is finished (or failed)
+  auto step = [&](auto RC, int i) -> bool {
+    constexpr int R = decltype(RC)::value;
+    constexpr int RM = (R + NS - 1) % NS;  // q_{i-1}, then q_{i+NS-1}
+    constexpr int RD = (R + 1) % NS;       // q_{i+1}
+    if (i >= 1) {
+      double hu = h0;
+      if (i - 1 >= 1 && !wait_h(i - 1, &hu)) return false;
+      update(hu, S[RM], st[RM]);
+    }
+    if (i == j) {  // last: subtract h_j q_j, ||w||^2 through the gatherer, normalise
+      double hj = h0;
+      if (j >= 1 && !wait_h(j, &hj)) return false;
+      update(hj, S[R], st[R]);
+      double part = 0.0;
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (data && p0 + k * kBlock < npair) {
+          part += y[k].x * y[k].x;
+          part += y[k].y * y[k].y;
+        }
+      if (tail) part += yt * yt;
+      publish2(part, 0.0, false, j + 1);
+      double nn = 0.0;
+      if (!wait_h(j + 1, &nn)) return false;
+      const double hh = sqrt(nn);
+      double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (data && p0 + k * kBlock < npair)
+          q2[p0 + k * kBlock] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+      if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
+      return false;
+    }
+    // q_{i+NS-1} into the slot q_{i-1} just left (NS - 2 steps of lead)
+    if (i + NS - 1 <= j) {
+      load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
+      if (tail) st[RM] = Q[static_cast<int64_t>(i + NS - 1) * pitch + n - 1];
+    }
+    // partial of h_{i+1}'s dot q_{i+1} . w^{(i)}; at i + 1 == j also g_j = q_j . q_{j-1}
+    const bool with_b = i + 1 == j;
+    double pa = 0.0, pb = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (data && p0 + k * kBlock < npair) {
+        pa += S[RD][k].x * y[k].x;
+        pa += S[RD][k].y * y[k].y;
+        if (with_b) {
+          pb += S[RD][k].x * S[R][k].x;
+          pb += S[RD][k].y * S[R][k].y;
+        }
+      }
+    if (tail) {
+      pa += st[RD] * yt;
+      if (with_b) pb += st[RD] * st[R];
+    }
+    publish2(pa, pb, with_b, i + 1);
+    return true;
+  };
+  for (int i = 0;; i += NS) {
+    if (!step(std::integral_constant<int, 0>{}, i)) break;
+    if (!step(std::integral_constant<int, 1>{}, i + 1)) break;
+    if (!step(std::integral_constant<int, 2>{}, i + 2)) break;
+    if (!step(std::integral_constant<int, 3>{}, i + 3)) break;
+    if constexpr (NS > 4) {
+      if (!step(std::integral_constant<int, 4>{}, i + 4)) break;
+    }
+  }
+}
+
 // The exchange of one chain step (K2p's protocol): the gathering workgroup's wave sweeps every
 // data workgroup's {tag, half} granules, sums the partials in a fixed order and publishes h as two
 // granules at hs; every other workgroup's wave polls those two.  Bounded spins (0.5 s).
@@ -1215,10 +1512,11 @@ __global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
-                            unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt) {
+                            unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt,
+                            double* gsub) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
-  if (aggregator && npair > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b
+  if (aggregator && npair > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b (K2q falls back to it)
     if (npair > kChainBigMaxPairs) return hipErrorInvalidValue;
     const int64_t wd = kChainMaxWG - 1;
     const int per = npair <= wd * kBigThreads * 8    ? 8
@@ -1242,6 +1540,23 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     return hipGetLastError();
   }
   if (npair > kChainMaxPairs) return hipErrorInvalidValue;
+  if (gsub != nullptr) {  // K2q: always with the dedicated gatherer
+    const int64_t wd = kChainMaxWG - 1;
+    const int per = npair <= wd * kBlock * 2 ? 2 : npair <= wd * kBlock * 4 ? 4 : 8;
+    const int64_t span = int64_t(kBlock) * per;
+    const int GD = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
+    if (GD > wd) return hipErrorInvalidValue;
+#define SPIS_LAG(PER_)                                                                                     \
+  launch_k(mgs_chain_lag_kernel<PER_, (PER_ >= 8 ? 4 : 5)>, dim3(GD + 1), dim3(kChainThreads), 0, s, ev, n, w, Q, pitch, j, \
+           part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, nt)
+    switch (per) {
+      case 2: SPIS_LAG(2); break;
+      case 4: SPIS_LAG(4); break;
+      default: SPIS_LAG(8); break;
+    }
+#undef SPIS_LAG
+    return hipGetLastError();
+  }
   const int64_t wmax = kChainMaxWG - (aggregator ? 1 : 0);  // one workgroup per CU in all
   const int per = npair <= wmax * kBlock * 2 ? 2 : npair <= wmax * kBlock * 4 ? 4 : 8;
   const int64_t span = int64_t(kBlock) * per;

@@ -124,7 +124,7 @@ struct spis_context {
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
   int ell_gram = 1;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy (SPIS_OPT_ELL_GRAM)
-  int mgs_chain = 2;                // K2p persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 on, 2 with a dedicated gathering workgroup
+  int mgs_chain = 3;                // persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 K2p gathered by workgroup 0, 2 by a dedicated workgroup, 3 K2q pipelined
   int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
   // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
   // waits for it through 1 a stream write / wait on a device word, 2 the GEMV launch's own
@@ -144,7 +144,8 @@ struct spis_context {
   size_t con_pinned_len = 0;
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
   uint64_t gemv_seq = 0;
-  unsigned long long* chain_gran = nullptr;  // 2 parities x kChainMaxWG x 2 granules
+  unsigned long long* chain_gran = nullptr;  // exchange granules (kChainGranLag: K2p / K2b / K2q layouts)
+  double* chain_gsub = nullptr;              // K2q: gsub[m] = q_m . q_{m-1} of the current basis
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
   unsigned* chain_err_dev = nullptr;
@@ -211,7 +212,8 @@ struct spis_workspace {
   double* Q = nullptr;
   double* Zb = nullptr;  // == Q when not preconditioned
   double* w = nullptr;   // Arnoldi vector
-  double* xj = nullptr;  // iterate (with ghost space)
+  double* xj = nullptr;   // iterate x_j of even j (with ghost space)
+  double* xj2 = nullptr;  // x_j of odd j: an update may be enqueued while the previous x is still read
   double* r0 = nullptr;
   double* x0 = nullptr;  // copy of x0 (n)
   double* ext = nullptr;  // scratch SpMV input with ghost space (constraint / preconditioner halos)
@@ -468,8 +470,10 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
-    HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * (4 * kChainMaxWG + 8)));
-    HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * (4 * kChainMaxWG + 8)));
+    HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * kChainGranLag));
+    HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * kChainGranLag));
+    HIP_TRY(hipMalloc(&c->chain_gsub, sizeof(double) * (kMaxK + 8)));
+    HIP_TRY(hipMemset(c->chain_gsub, 0, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->chain_epoch, 16));
     HIP_TRY(hipMemset(c->chain_epoch, 0, 16));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->chain_err), 16, hipHostMallocMapped));
@@ -507,6 +511,7 @@ static void free_workspace(spis_workspace* ws) {
   if (ws->sep_z) (void)hipFree(ws->Zb);
   (void)hipFree(ws->w);
   (void)hipFree(ws->xj);
+  (void)hipFree(ws->xj2);
   (void)hipFree(ws->r0);
   (void)hipFree(ws->x0);
   (void)hipFree(ws->ydev);
@@ -536,6 +541,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
     (void)hipFree(c->chain_gran);
+    (void)hipFree(c->chain_gsub);
     (void)hipFree(c->gemv_flag);
     (void)hipFree(c->chain_epoch);
     if (c->chain_err) (void)hipHostFree(c->chain_err);
@@ -591,7 +597,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->ell_gram = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0, 1 or 2", (long long)value);
+        if (value < 0 || value > 3) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0, 1, 2 or 3", (long long)value);
         c->mgs_chain = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_OVERLAP_GEMV:
@@ -1580,7 +1586,7 @@ static int get_workspace(spis_context* c, int64_t n, int64_t n_ext, int k, bool 
   } else {
     ws->Zb = ws->Q;
   }
-  for (double** p : {&ws->w, &ws->xj, &ws->r0, &ws->x0}) {
+  for (double** p : {&ws->w, &ws->xj, &ws->xj2, &ws->r0, &ws->x0}) {
     HIP_TRY(hipMalloc(p, sizeof(double) * pitch));
     HIP_TRY(hipMemsetAsync(*p, 0, sizeof(double) * pitch, c->stream));
   }
@@ -1711,6 +1717,51 @@ struct Solver {
     *reinterpret_cast<volatile unsigned long long*>(c->pinned + seq_off(j)) = upd_seq[j & 1];
   }
 
+  double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
+
+  // Speculative update (single GPU, K2q chains): K2q's gatherer writes H[:, j] with H[j+1, j]
+  // last, behind a system-scope release, so the host can read the column as soon as A_j's chain
+  // ends, instead of waiting for U_{j-1}'s residual (published at the start of A_{j+1}'s chain,
+  // one dual SpMV later).  Where the branch of LS_j cannot depend on that residual except through
+  // an unconstrained -> constrained switch, the unconstrained y_j is solved then and U_j's GEMV
+  // enqueued at once on the side stream: it then runs beside the dual SpMV and A_{j+1}'s chain
+  // instead of delaying the dual SpMV that reads x_j.  A constrained LS_j re-enqueues the GEMV
+  // with its own y (stream order on the side stream); a stop at j-1 leaves x_j unused (x_j and
+  // x_{j-1} live in separate buffers).  Results are identical to the unspeculated path.
+  bool lag_chain() const {
+    return c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && (n >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8;
+  }
+  static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
+  void arm_hcol(int j) {  // before A_j's chain is enqueued
+    *reinterpret_cast<volatile uint64_t*>(c->pinned + hoff(j) + j + 1) = kHSentinel;
+  }
+  // true once H[:, j] is complete; false if the stream drained without it (a failed chain)
+  int wait_hcol(int j, bool* ok) const {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + j + 1);
+    const double t0 = now_s();
+    for (unsigned spin = 0;; ++spin) {
+      if (__atomic_load_n(w, __ATOMIC_ACQUIRE) != kHSentinel) {
+        *ok = true;
+        return SPIS_OK;
+      }
+      if ((spin & 4095) == 4095 && now_s() - t0 > 0.02) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e != hipSuccess && e != hipErrorNotReady) return fail(SPIS_ERR_HIP, "stream: %s", hipGetErrorString(e));
+        if (e == hipSuccess && __atomic_load_n(w, __ATOMIC_ACQUIRE) == kHSentinel) {
+          *ok = false;
+          return SPIS_OK;
+        }
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  int spec_gemv(int j, int p, const double* y) {  // U_j's GEMV on the side stream + its count
+    ST_TRY(update_gemv(j, p, y, c->stream2));
+    ++c->gemv_seq;
+    HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
+    return SPIS_OK;
+  }
+
   // A_j = arnoldi_pre (preconditioner + halo) -> Arnoldi SpMV -> arnoldi_post (MGS + normalise)
   int arnoldi_pre(int j) {  // solvers.py:190
     hipStream_t s = c->stream;
@@ -1743,7 +1794,9 @@ struct Solver {
     ProfEv pm(c, SPIS_PROF_MGS);  // start on the first MGS step, stop on the normalise
     const LaunchEv e_first = pm.first();
     const LaunchEv e_last = pm.last();
-    const bool agg = c->mgs_chain == 2;
+    const bool agg = c->mgs_chain >= 2;
+    // K2q (mode 3): the pipelined chain, while it fits K2p's register slices (K2b beyond)
+    double* gsub = c->mgs_chain == 3 ? c->chain_gsub : nullptr;
     // nontemporal basis loads when the matrix and the basis overflow the 256 MB Infinity Cache:
     // the chain then leaves the matrix resident for the next SpMV (C3: dual SpMV 49 -> 42 us,
     // chain +1-2 us, +2.9%; C4, whose working set fits, measured 1% slower with them)
@@ -1751,8 +1804,9 @@ struct Solver {
     const bool nt_chain = c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
     if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
+      if (lag_chain()) arm_hcol(j);
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
-                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain));
+                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub));
       return SPIS_OK;
     }
     double* src = c->partA;
@@ -1825,15 +1879,15 @@ struct Solver {
         *done = le.stop;
       }
       if (p <= kYArg) {
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, ws->xj, s, &le));
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le));
       } else {
         double* yh = c->pinned + yoff();
         for (int a = 0; a < p; ++a) yh[a] = y[a];
         HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, ws->xj, s, &le));
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, xbuf(j), s, &le));
       }
     }
-    return exchange(c, A, ws->xj);
+    return exchange(c, A, xbuf(j));
   }
 
   // U_j's true-residual partials go to device memory (partR).  Single GPU: one workgroup reduces
@@ -1854,7 +1908,7 @@ struct Solver {
     {
       ProfEv ps(c, SPIS_PROF_SPMV_RES);
       const LaunchEv le = ps.both();
-      HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, ws->xj, nullptr, b, c->partR, gs, c->stream, &le));
+      HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, xbuf(j), nullptr, b, c->partR, gs, c->stream, &le));
     }
     if (c->comm) return update_comm_finish(j);
     next_seq(j);
@@ -1868,7 +1922,7 @@ struct Solver {
     {
       ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
       const LaunchEv le = pd.both();
-      HIP_TRY(launch_spmv_dual(A->dual_view(), ws->xj, ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
+      HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
                                c->stream, &le));
     }
     if (c->comm) {
@@ -1910,8 +1964,10 @@ struct Solver {
   }
 
   // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
-  int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
-    if (c->overlap_gemv && !c->comm && p <= kYArg) {
+  int enqueue_update_arnoldi(int j, int p, const double* y, int ja, bool gemv_done = false) {
+    if (gemv_done) {  // U_j's GEMV was enqueued speculatively (spec_gemv) with this y
+      HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
+    } else if (c->overlap_gemv && !c->comm && p <= kYArg) {
       // U_j's GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM
       // traffic) still running on the main stream; the dual SpMV waits for it.  Safe: every
       // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
@@ -2068,7 +2124,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // never beside a persistent MGS chain (K2p / K2b): the chain needs all of its workgroups
     // resident at once, and a concurrent Gram could hold the CU slots its last workgroups wait
     // for (the chain would then time out and fail the solve with SPIS_ERR_STATE)
-    const bool chain_runs = !fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, c->mgs_chain == 2) &&
+    const bool chain_runs = !fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, c->mgs_chain >= 2) &&
                             !(c->cgs2 && k <= kCgsMax);
     const bool early = c->early_con && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && !c->comm &&
                        k + 1 <= 64 && nlin <= 4 && !c->force_generic_gram && ws->Zb == ws->Q && k >= 4 &&
@@ -2089,7 +2145,30 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
       ws->broke_at_start = true;
     }
+    std::vector<double> yspec(k);
+    bool spec_any = false;  // a speculative GEMV was enqueued on the side stream
+    int last_x = -1;        // iteration whose x_j is x[-1]
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
+      // speculative U_j (Solver::lag_chain): LS_j's branch cannot depend on res_{j-1} except
+      // through the unconstrained -> constrained switch (GMRES: never; CGMRES: while safety is
+      // None and j < k - 1), so the unconstrained y_j goes out as soon as H[:, j] is complete
+      bool spec = false, col_added = false;
+      const bool spec_ok = j >= 1 && j + 2 < k && c->fuse_spmv && c->overlap_gemv == 1 && !c->comm && j + 1 <= kYArg &&
+                           S.lag_chain() && !S.graphable() &&
+                           (o->method == SPIS_GMRES || (o->method == SPIS_CGMRES && safety == kSafetyNone));
+      if (spec_ok) {
+        bool ok = false;
+        ST_TRY(S.wait_hcol(j, &ok));
+        const double* hp = c->pinned + S.hoff(j);
+        if (ok && hp[j + 1] != 0.0) {  // (a breakdown ends the run below)
+          for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
+          qr.add_column(j, hcol.data());
+          col_added = true;
+          qr.solve(j + 1, yspec.data());
+          ST_TRY(S.spec_gemv(j, j + 1, yspec.data()));
+          spec = spec_any = true;
+        }
+      }
       ST_TRY(j == 0 ? wait_event(c->ev_arn) : S.wait_update(j - 1));
       prof_drain(c);
       if (pending >= 0) {  // finish iteration j-1: true residual + stop test (solvers.py:290-297)
@@ -2110,7 +2189,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         out->events_host[j] |= SPIS_EV_BREAKDOWN;
         break;
       }
-      qr.add_column(j, hcol.data());
+      if (!col_added) qr.add_column(j, hcol.data());
       const int p = j + 1;
       std::fill(y0.begin(), y0.end(), 0.0);
       for (int a = 0; a < j; ++a) y0[a] = yk[a];  // warm start (:225-227)
@@ -2128,7 +2207,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
 
       if (!constrained) {
-        qr.solve(p, y.data());
+        if (spec) std::copy(yspec.begin(), yspec.begin() + p, y.begin());  // the same solve
+        else qr.solve(p, y.data());
       } else if (use_cb && m_active > 0) {
         // dict-form constraints: the host callback runs the constrained LS (and its fallback)
         std::vector<double> Hc(static_cast<size_t>(p + 1) * p);
@@ -2213,7 +2293,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       ws->n_iter_y = j + 1;
       if (j + 2 < k && c->fuse_spmv) {
         if (stamps) stamps[j + 2] = now_s();
-        ST_TRY(S.enqueue_update_arnoldi(j, p, y.data(), j + 2));
+        // a speculative GEMV with the y taken stands; otherwise (constrained) it is redone
+        ST_TRY(S.enqueue_update_arnoldi(j, p, y.data(), j + 2, spec && !constrained));
       } else {
         ST_TRY(S.enqueue_update(j, p, y.data()));
         if (j + 2 < k) {
@@ -2223,13 +2304,16 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
       if (early && !pre_launched && j + 2 == k - 3 + c->early_con) ST_TRY(launch_early());  // A_{k-2} / A_{k-1} queued
       have_x = true;
+      last_x = j;
       pending = j;
     }
     // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
     // Arnoldi step, which never touches xj / r0), then one synchronisation
+    // (an unconsumed speculative GEMV writes the other x buffer; the stream waits for it below)
+    if (spec_any) HIP_TRY(hipStreamWaitValue64(s, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
     if (out->x_final_dev) {
       if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
-      else HIP_TRY(launch_copy(n, have_x ? ws->xj : ws->r0, out->x_final_dev, s));
+      else HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));
     }
     if (pending >= 0) {
       ST_TRY(S.wait_update(pending));

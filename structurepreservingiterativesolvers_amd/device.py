@@ -53,7 +53,7 @@ _OPTIONS = {
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
     "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2}),
-    "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 2, "gather0": 1, "aggregator": 2}),
+    "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 3, "gather0": 1, "aggregator": 2, "pipelined": 3}),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
@@ -73,9 +73,11 @@ def set_option(name, value, ctx=None):
       (sliced ELL; True), "staged" (row chunks whose distinct columns' basis rows are staged in
       LDS; falls back to "ell" for a matrix with a row that does not fit a chunk) or "csr"
       (False);
-    * ``mgs_chain`` (True = "aggregator"): each Arnoldi step's MGS chain + normalise as one persistent
+    * ``mgs_chain`` (True = "pipelined"): each Arnoldi step's MGS chain + normalise as one persistent
       launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
-      ("gather0"); False = one launch per MGS step;
+      ("gather0"); "pipelined": each dot product one MGS step early by the distributive law
+      (h_{i+1} = q_{i+1}.w^(i) - h_i q_{i+1}.q_i), two exchanges in flight (not MGS's rounding);
+      False = one launch per MGS step;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
     * ``nt_basis`` ("auto"): the MGS chain's basis loads are nontemporal when the matrix and the
       basis exceed the 256 MB Infinity Cache (True: always; False: never), results identical;

@@ -197,8 +197,18 @@ def _run_package(spis, case):
     return solvers.cgmres(case.A, case.b, x0, m["k"], tol=m["tol"], conlist=case.conlist(), pre=pre, **kw)
 
 
+@pytest.fixture(params=["aggregator", "pipelined"])
+def chain_mode(request, spis):
+    """The pipelined MGS chain (the default, SPIS_OPT_MGS_CHAIN = 3) and the plain one (2)."""
+    from structurepreservingiterativesolvers_amd.device import set_option
+
+    set_option("mgs_chain", request.param)
+    yield request.param
+    set_option("mgs_chain", True)
+
+
 @pytest.mark.parametrize("name", names())
-def test_golden(spis, name, caplog):
+def test_golden(spis, chain_mode, name, caplog):
     case = Case(name)
     with warnings.catch_warnings(record=True) as caught, caplog.at_level(logging.WARNING):
         warnings.simplefilter("always")
@@ -840,7 +850,7 @@ def test_distributed_code_path_self_halo(spis):
 
 @pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_048_575, 2_000_001, 3_500_000, 5_000_001, 7_500_001, 10_000_001])
 def test_mgs_chain_matches_per_step_launches(spis, n):
-    """K2p / K2b (SPIS_OPT_MGS_CHAIN): the persistent MGS chains against one launch per MGS step,
+    """K2p / K2b / K2q (SPIS_OPT_MGS_CHAIN): the persistent MGS chains against one launch per MGS step,
     on sizes that select each register tiling (K2p: PER = 2, 4, 8 double2 per thread; K2b, the
     dedicated-gatherer mode beyond 2^20: PER = 8, 16, 24, 32, 40), the largest N K2p takes (odd: a
     tail element).  Same MGS arithmetic, partial dots grouped differently: iterates and residuals
@@ -856,14 +866,15 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
     b = rng.standard_normal(n)
     k = 12
     runs = []
-    # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 0: per-step launches
-    modes = (1, 1, 2, 2, 0) if n <= 2_000_001 else (2, 2, 0)
+    # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 3: pipelined (K2q; K2b
+    # beyond 2^20); 0: per-step launches
+    modes = (1, 1, 2, 2, 3, 3, 0) if n <= 2_000_001 else (2, 2, 3, 3, 0)
     for chain in modes:
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
         try:
             x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
         finally:
-            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 2), "spis_set_option")
+            _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 3), "spis_set_option")
         runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
     x0, r0, Q0 = runs[-1]
     pairs = [(runs[i], runs[i + 1]) for i in range(0, len(runs) - 1, 2)]
