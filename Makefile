@@ -43,3 +43,7 @@ clean:
 	rm -rf build $(LIB) $(PKG)/liblsq_host.so
 
 .PHONY: all clean
+
+# tuning tools (not built by default)
+tools/chainbench: tools/chainbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h
+	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<

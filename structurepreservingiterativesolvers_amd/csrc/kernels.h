@@ -108,12 +108,16 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator = false,
-                            bool nt = false, double* gsub = nullptr);
+                            bool nt = false, double* gsub = nullptr, const double* yx_host = nullptr, int px = 0,
+                            const double* x0 = nullptr, double* xo = nullptr);
 // (nt: the chain's basis loads are nontemporal — the matrix stays Infinity-Cache resident)
 // gsub != nullptr selects K2q, the pipelined chain (dot products one MGS step early by the
 // distributive law; gsub[m] = q_m . q_{m-1}, written by chain m, read by the later chains of the
 // same basis); gran then needs kChainGranLag granules.  Beyond K2p's size it falls back to K2b.
+// K2q only: px > 0 fuses the GEMV xo = Q[:, :px] yx + x0 (px <= j, p <= kYArg; K4's arithmetic).
 constexpr int kChainGranLag = 10 * kChainMaxWG + 16;
+constexpr int kLagDW = 8;  // K2q data waves per workgroup (+1 exchange wave): PER <= 4 pairs per thread
+constexpr int kLagNS = 4;  // K2q basis ring: q_{i-1} .. q_{i+2} in registers (2 steps of prefetch lead)
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
 

@@ -994,6 +994,27 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
   if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// buffer-descriptor loads / stores: one 32-bit lane offset shared by every element of a thread,
+// the element's distance in the scalar offset (no per-element address registers).  The hardware
+// range check does not cover the scalar offset: callers predicate every access themselves.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_double2(__hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)),
+                      __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)));
+}
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 d) {
+  u32x4_t v;
+  v.x = static_cast<unsigned>(__double2loint(d.x));
+  v.y = static_cast<unsigned>(__double2hiint(d.x));
+  v.z = static_cast<unsigned>(__double2loint(d.y));
+  v.w = static_cast<unsigned>(__double2hiint(d.y));
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K2q: pipelined MGS chain (SPIS_OPT_MGS_CHAIN = 3).  MGS's projections, with each dot product
 // evaluated one step early by the distributive law:
@@ -1017,24 +1038,30 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
 // partials; the gatherer publishes h_m after reading E_m, which every workgroup publishes after
 // it read h_{m-4} (and earlier h's).
 // ---------------------------------------------------------------------------------------------
-template <int PER, int NS>
-__global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
+// DW data waves hold the slices (DW * 64 threads x PER pairs each); wave DW runs the exchange.
+template <int DW, int PER, int NS, bool FX, bool NT>
+__global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    bool nt) {
+    bool nt, YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
 #pragma clang fp contract(off)
-  __shared__ double s_wave[8];
+  // FX: the update GEMV x = Q[:, :px] yx + x0 of the previous LS step rides along (K4's
+  // arithmetic: the sum in basis order, then + x0), accumulated in LDS as each q_i passes (the
+  // thread's own entries: no barrier); x = acc + x0 is stored after the chain's last exchange
+  constexpr int DT = DW * 64;  // data threads
+  __shared__ double2 s_acc[FX ? PER * DT : 1];  // (in registers it spilled)
+  __shared__ double s_wave[2 * DW];
   __shared__ double s_h;
   __shared__ int s_fail;
   const int G = gridDim.x;
   const int GD = G - 1;  // data workgroups; the last one gathers
   const int tid = threadIdx.x;
   const bool agg = static_cast<int>(blockIdx.x) == GD;
-  const bool data = tid < kBlock && !agg;
+  const bool data = tid < DT && !agg;
   const int64_t npair = n >> 1;
-  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * kBlock * PER + tid;
+  const int64_t p0 = static_cast<int64_t>(blockIdx.x) * DT * PER + tid;
   const bool tail = (n & 1) && blockIdx.x == 0 && tid == 0;  // odd element: workgroup 0, lane 0
   unsigned long long* aslots = gran;                             // 4 x 2 kChainMaxWG
   unsigned long long* gslots = gran + 8 * kChainMaxWG;           // 2 kChainMaxWG (g_j)
@@ -1042,16 +1069,21 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
   const unsigned base = *epoch;
   double2 y[PER];
   double2 S[NS][PER];
-  double yt = 0.0, st[NS];
+  double yt = 0.0, st[NS], acct = 0.0;
 #pragma unroll
   for (int r = 0; r < NS; ++r) st[r] = 0.0;
+  // (buffer-descriptor loads here, to save address registers, measured 1.0-1.4x slower)
   auto load = [&](double2 (&r)[PER], const double* v) {
     const double2* v2 = reinterpret_cast<const double2*>(v);
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * kBlock < npair) r[k] = ld_basis(v2 + p0 + k * kBlock, nt);
+      if (data && p0 + k * DT < npair) r[k] = ld_basis(v2 + p0 + k * DT, NT);
   };
   if (!agg) {
+    if (FX && data) {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) s_acc[k * DT + tid] = make_double2(0.0, 0.0);
+    }
     load(y, w);
     if (tail) yt = w[n - 1];
 #pragma unroll
@@ -1153,8 +1185,8 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
   // h_m from the gatherer (exchange wave polls, every wave joins the barrier); false on timeout
   auto wait_h = [&](int m, double* out) -> bool {
     const unsigned tag = base + static_cast<unsigned>(m);
-    if (tid >= kBlock) {
-      const int lane = tid - kBlock;
+    if (tid >= DT) {
+      const int lane = tid - DT;
       const unsigned long long* hs = hslots + 2 * (m & 3);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       unsigned long long g = 0;
@@ -1189,18 +1221,22 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
     const double wb = with_b ? wave_sum_dpp(pb) : 0.0;
     if (data && (tid & 63) == 0) {
       s_wave[tid >> 6] = wa;
-      s_wave[4 + (tid >> 6)] = wb;
+      s_wave[DW + (tid >> 6)] = wb;
     }
     __syncthreads();
     if (tid == 0) {
       const unsigned tag = base + static_cast<unsigned>(m);
-      const double ta = ((s_wave[0] + s_wave[1]) + s_wave[2]) + s_wave[3];
+      double ta = s_wave[0];
+#pragma unroll
+      for (int v = 1; v < DW; ++v) ta += s_wave[v];
       const unsigned long long ba = static_cast<unsigned long long>(__double_as_longlong(ta));
       unsigned long long* sl = aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG + 2 * blockIdx.x;
       chain_store(sl, tag, static_cast<unsigned>(ba));
       chain_store(sl + 1, tag, static_cast<unsigned>(ba >> 32));
       if (with_b) {
-        const double tb = ((s_wave[4] + s_wave[5]) + s_wave[6]) + s_wave[7];
+        double tb = s_wave[DW];
+#pragma unroll
+        for (int v = 1; v < DW; ++v) tb += s_wave[DW + v];
         const unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(tb));
         chain_store(gslots + 2 * blockIdx.x, tag, static_cast<unsigned>(bb));
         chain_store(gslots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bb >> 32));
@@ -1211,7 +1247,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
   auto update = [&](double h, const double2 (&q)[PER], double qt) {
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * kBlock < npair) {
+      if (data && p0 + k * DT < npair) {
         const double a0 = h * q[k].x, a1 = h * q[k].y;
         y[k].x = y[k].x - a0;
         y[k].y = y[k].y - a1;
@@ -1238,7 +1274,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
       double part = 0.0;
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (data && p0 + k * kBlock < npair) {
+        if (data && p0 + k * DT < npair) {
           part += y[k].x * y[k].x;
           part += y[k].y * y[k].y;
         }
@@ -1250,10 +1286,38 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
       double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (data && p0 + k * kBlock < npair)
-          q2[p0 + k * kBlock] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+        if (data && p0 + k * DT < npair)
+          q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
       if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
+      if (FX) {
+        const double2* x02 = reinterpret_cast<const double2*>(x0);
+        double2* xo2 = reinterpret_cast<double2*>(xo);
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+          if (data && p0 + k * DT < npair) {
+            const double2 a = s_acc[k * DT + tid];
+            const double2 b = x02[p0 + k * DT];
+            xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
+          }
+        if (tail) xo[n - 1] = acct + x0[n - 1];
+      }
       return false;
+    }
+    if (FX && i < px) {  // x += yx_i q_i (K4's order; x0 is added after the last coefficient)
+      const double cf = yx.v[i];
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (data) {
+          double2 a = s_acc[k * DT + tid];
+          const double m0 = S[R][k].x * cf, m1 = S[R][k].y * cf;
+          a.x = a.x + m0;
+          a.y = a.y + m1;
+          s_acc[k * DT + tid] = a;
+        }
+      if (tail) {
+        const double m = st[R] * cf;
+        acct = acct + m;
+      }
     }
     // q_{i+NS-1} into the slot q_{i-1} just left (NS - 2 steps of lead)
     if (i + NS - 1 <= j) {
@@ -1265,7 +1329,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_lag_kernel(
     double pa = 0.0, pb = 0.0;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * kBlock < npair) {
+      if (data && p0 + k * DT < npair) {
         pa += S[RD][k].x * y[k].x;
         pa += S[RD][k].y * y[k].y;
         if (with_b) {
@@ -1362,27 +1426,6 @@ __device__ __forceinline__ void chain_exchange(int lane, bool gatherer, int GD, 
 // exchange and arithmetic as K2p (contraction off; partials grouped per workgroup).
 // ---------------------------------------------------------------------------------------------
 constexpr int kBigThreads = 512;
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-// buffer-descriptor loads / stores: one 32-bit lane offset shared by every element of a thread,
-// the element's distance in the scalar offset (no per-element address registers).  The hardware
-// range check does not cover the scalar offset: callers predicate every access themselves.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* p, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, static_cast<int>(bytes), 0x00020000);
-}
-__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  return make_double2(__hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)),
-                      __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)));
-}
-__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 d) {
-  u32x4_t v;
-  v.x = static_cast<unsigned>(__double2loint(d.x));
-  v.y = static_cast<unsigned>(__double2hiint(d.x));
-  v.z = static_cast<unsigned>(__double2loint(d.y));
-  v.w = static_cast<unsigned>(__double2hiint(d.y));
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
-}
-
 template <int PER>
 __global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
@@ -1513,10 +1556,11 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt,
-                            double* gsub) {
+                            double* gsub, const double* yx_host, int px, const double* x0, double* xo) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
   if (aggregator && npair > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b (K2q falls back to it)
+    if (px > 0) return hipErrorInvalidValue;  // the fused GEMV is K2q's only
     if (npair > kChainBigMaxPairs) return hipErrorInvalidValue;
     const int64_t wd = kChainMaxWG - 1;
     const int per = npair <= wd * kBigThreads * 8    ? 8
@@ -1540,20 +1584,31 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     return hipGetLastError();
   }
   if (npair > kChainMaxPairs) return hipErrorInvalidValue;
-  if (gsub != nullptr) {  // K2q: always with the dedicated gatherer
+  if (gsub != nullptr) {  // K2q: always with the dedicated gatherer; 8 data waves (kLagDW)
     const int64_t wd = kChainMaxWG - 1;
-    const int per = npair <= wd * kBlock * 2 ? 2 : npair <= wd * kBlock * 4 ? 4 : 8;
-    const int64_t span = int64_t(kBlock) * per;
+    constexpr int DT = kLagDW * 64;
+    const int per = npair <= wd * DT * 1 ? 1 : npair <= wd * DT * 2 ? 2 : 4;
+    const int64_t span = int64_t(DT) * per;
     const int GD = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
     if (GD > wd) return hipErrorInvalidValue;
-#define SPIS_LAG(PER_)                                                                                     \
-  launch_k(mgs_chain_lag_kernel<PER_, (PER_ >= 8 ? 4 : 5)>, dim3(GD + 1), dim3(kChainThreads), 0, s, ev, n, w, Q, pitch, j, \
-           part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, nt)
-    switch (per) {
-      case 2: SPIS_LAG(2); break;
-      case 4: SPIS_LAG(4); break;
-      default: SPIS_LAG(8); break;
-    }
+    if (px < 0 || px > j || px > kYArg || (px > 0 && (!yx_host || !x0 || !xo || !aligned16(x0) || !aligned16(xo))))
+      return hipErrorInvalidValue;
+    YArg ya;
+    for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
+#define SPIS_LAG(PER_, FX_, NT_)                                                                                 \
+  launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, pitch, j, \
+           part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, nt, ya, px, x0, xo)
+#define SPIS_LAG_PER(FX_, NT_)          \
+  switch (per) {                        \
+    case 1: SPIS_LAG(1, FX_, NT_); break; \
+    case 2: SPIS_LAG(2, FX_, NT_); break; \
+    default: SPIS_LAG(4, FX_, NT_); break; \
+  }
+    if (px > 0 && nt) SPIS_LAG_PER(true, true)
+    else if (px > 0) SPIS_LAG_PER(true, false)
+    else if (nt) SPIS_LAG_PER(false, true)
+    else SPIS_LAG_PER(false, false)
+#undef SPIS_LAG_PER
 #undef SPIS_LAG
     return hipGetLastError();
   }

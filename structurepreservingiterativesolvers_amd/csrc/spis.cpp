@@ -1755,12 +1755,6 @@ struct Solver {
       __builtin_ia32_pause();
     }
   }
-  int spec_gemv(int j, int p, const double* y) {  // U_j's GEMV on the side stream + its count
-    ST_TRY(update_gemv(j, p, y, c->stream2));
-    ++c->gemv_seq;
-    HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
-    return SPIS_OK;
-  }
 
   // A_j = arnoldi_pre (preconditioner + halo) -> Arnoldi SpMV -> arnoldi_post (MGS + normalise)
   int arnoldi_pre(int j) {  // solvers.py:190
@@ -1784,8 +1778,10 @@ struct Solver {
 
   // (xpart, x_out, done): the first MGS step also reduces the previous update's residual partials
   // into host memory and carries that update's completion event (single GPU, fused path)
+  // (yx, jx): K2q only — the chain also computes U_jx's GEMV x_jx = Z[:, :jx+1] yx + x0 (L mode)
   int arnoldi_post(int j, const double* xpart = nullptr, double* x_out = nullptr,
-                   unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr) {
+                   unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr,
+                   const double* yx = nullptr, int jx = -1) {
     if (c->cgs2 && j + 1 <= kCgsMax) return arnoldi_post_cgs2(j, xpart, x_out, flag, seq);
     hipStream_t s = c->stream;
     c->prof_iter = j;
@@ -1805,10 +1801,13 @@ struct Solver {
     if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
       if (lag_chain()) arm_hcol(j);
+      const int px = (gsub && yx) ? jx + 1 : 0;
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
-                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub));
+                               c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub, yx, px,
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr));
       return SPIS_OK;
     }
+    if (yx) return fail(SPIS_ERR_STATE, "fused update GEMV without the pipelined chain");
     double* src = c->partA;
     double* dst = c->partB;
     int n_in = gs;
@@ -1854,7 +1853,7 @@ struct Solver {
     return SPIS_OK;
   }
 
-  int enqueue_arnoldi(int j) {  // solvers.py:190-198
+  int enqueue_arnoldi(int j, bool with_chain = true) {  // solvers.py:190-198
     c->prof_iter = j;
     ST_TRY(arnoldi_pre(j));
     {
@@ -1862,7 +1861,53 @@ struct Solver {
       const LaunchEv le = ps.both();
       HIP_TRY(launch_spmv(A->dual_view(), kEpiDot, Zv(j), ws->w, Qv(0), c->partA, gs, c->stream, &le));
     }
-    return arnoldi_post(j);
+    return with_chain ? arnoldi_post(j) : SPIS_OK;
+  }
+
+  // ---- L mode (lag_chain, see the solver loop): A_ja's chain is enqueued one iteration after its
+  // SpMV, once H[:, ja-1] is on the host, so that it can carry U_{ja-1}'s GEMV
+  // U_j's residual SpMV fused with A_ja's Arnoldi SpMV (the chain follows later: enqueue_chain)
+  int enqueue_dual(int j, int ja) {
+    ST_TRY(arnoldi_pre(ja));
+    next_seq(j);
+    c->prof_iter = j;
+    ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
+    const LaunchEv le = pd.both();
+    HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
+                             c->stream, &le));
+    return SPIS_OK;
+  }
+  // A_ja's chain; jres >= 0: it also reduces U_jres's residual (the dual before it) and publishes
+  // it; yx != nullptr: it also computes x_{ja-1} = Z y_{ja-1} + x0
+  int enqueue_chain(int ja, int jres, const double* yx) {
+    if (jres >= 0) return arnoldi_post(ja, c->partR, c->pinned_dev + roff(jres), flag_dev(), seq_dev(jres), yx, ja - 1);
+    return arnoldi_post(ja, nullptr, nullptr, nullptr, nullptr, yx, ja - 1);
+  }
+  // U_j's GEMV: beside a running chain on the side stream (the main stream waits for it), or in
+  // stream order on the main stream
+  int enqueue_gemv(int j, int p, const double* y, bool overlap) {
+    if (!overlap || p > kYArg) return update_gemv(j, p, y);
+    ST_TRY(update_gemv(j, p, y, c->stream2));
+    ++c->gemv_seq;
+    HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
+    HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
+    return SPIS_OK;
+  }
+  // U_j's residual partials (from [U_j res | a_{j+2}]) reduced and published without a chain
+  int enqueue_finalize(int j) {
+    HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
+    return SPIS_OK;
+  }
+  // U_j's residual SpMV on its own (no A_{j+2} to pair with) and its host signal
+  int enqueue_residual(int j) {
+    {
+      ProfEv ps(c, SPIS_PROF_SPMV_RES);
+      const LaunchEv le = ps.both();
+      HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, xbuf(j), nullptr, b, c->partR, gs, c->stream, &le));
+    }
+    next_seq(j);
+    HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
+    return SPIS_OK;
   }
 
   // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
@@ -1964,10 +2009,8 @@ struct Solver {
   }
 
   // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
-  int enqueue_update_arnoldi(int j, int p, const double* y, int ja, bool gemv_done = false) {
-    if (gemv_done) {  // U_j's GEMV was enqueued speculatively (spec_gemv) with this y
-      HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
-    } else if (c->overlap_gemv && !c->comm && p <= kYArg) {
+  int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
+    if (c->overlap_gemv && !c->comm && p <= kYArg) {
       // U_j's GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM
       // traffic) still running on the main stream; the dual SpMV waits for it.  Safe: every
       // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
@@ -2096,12 +2139,14 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)
     // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
     // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
+    // L mode: the solver loop below (lag_chain: K2q chains publish H[:, j] to the host themselves)
+    const bool L = S.lag_chain() && c->fuse_spmv && !S.graphable();
     if (stamps) stamps[0] = now_s();
     ST_TRY(S.enqueue_arnoldi(0));
     HIP_TRY(hipEventRecord(c->ev_arn, s));
     if (k > 1) {
       if (stamps) stamps[1] = now_s();
-      ST_TRY(S.enqueue_arnoldi(1));
+      ST_TRY(S.enqueue_arnoldi(1, !L));  // L: A_1's chain is enqueued at iteration 0
     }
     ST_TRY(wait_event(c->ev_gram));
     const double beta = *beta_slot;
@@ -2145,31 +2190,46 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
       ws->broke_at_start = true;
     }
+    // L mode.  Stream order  A_0, a_1, [c_1 + U_0 gemv], [U_0 res | a_2], [c_2 + U_1 gemv],
+    // [U_1 res | a_3], ...  with a_j = A_j's preconditioner + Arnoldi SpMV, c_j = its MGS chain (K2q).
+    // At iteration j the host waits for H[:, j] (c_j's gatherer publishes it: one chain, not one
+    // chain plus a dual SpMV, after LS_{j-1}), then enqueues c_{j+1}; when LS_j's branch can
+    // depend on res_{j-1} only through the unconstrained -> constrained switch (GMRES: never;
+    // CGMRES while safety is None and j < k - 1) y_j is solved first and c_{j+1} computes U_j's
+    // GEMV as it streams q_0 .. q_j (no second pass over the basis).  Then it waits for res_{j-1}
+    // (reduced and published by c_{j+1}), decides LS_j as the reference does (a constrained LS_j
+    // recomputes x_j after c_{j+1}), and enqueues [U_j res | a_{j+2}] (res + finalize at the end).
     std::vector<double> yspec(k);
-    bool spec_any = false;  // a speculative GEMV was enqueued on the side stream
-    int last_x = -1;        // iteration whose x_j is x[-1]
+    int last_x = -1;  // iteration whose x_j is x[-1]
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
-      // speculative U_j (Solver::lag_chain): LS_j's branch cannot depend on res_{j-1} except
-      // through the unconstrained -> constrained switch (GMRES: never; CGMRES: while safety is
-      // None and j < k - 1), so the unconstrained y_j goes out as soon as H[:, j] is complete
-      bool spec = false, col_added = false;
-      const bool spec_ok = j >= 1 && j + 2 < k && c->fuse_spmv && c->overlap_gemv == 1 && !c->comm && j + 1 <= kYArg &&
-                           S.lag_chain() && !S.graphable() &&
-                           (o->method == SPIS_GMRES || (o->method == SPIS_CGMRES && safety == kSafetyNone));
-      if (spec_ok) {
+      bool fused = false, col_added = false;
+      if (L) {
         bool ok = false;
         ST_TRY(S.wait_hcol(j, &ok));
+        if (!ok) {  // the chain failed (c->chain_err): reported at the end of the solve
+          (void)hipStreamSynchronize(s);
+          break;
+        }
         const double* hp = c->pinned + S.hoff(j);
-        if (ok && hp[j + 1] != 0.0) {  // (a breakdown ends the run below)
-          for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
-          qr.add_column(j, hcol.data());
-          col_added = true;
-          qr.solve(j + 1, yspec.data());
-          ST_TRY(S.spec_gemv(j, j + 1, yspec.data()));
-          spec = spec_any = true;
+        const bool brk = hp[j + 1] == 0.0 && o->method != SPIS_CGMRES_P;  // the run ends below
+        if (!brk && j + 1 < k) {
+          const double prev = out->res_host[n_res - 1];  // beta at j = 0; res_{j-1} arrives later
+          const bool uncon = o->method == SPIS_GMRES ||
+                             (o->method == SPIS_CGMRES && safety == kSafetyNone && j < k - 1 &&
+                              (j >= 1 || prev > o->contol * o->tol));
+          if (uncon && j + 1 <= kYArg && ws->Zb == ws->Q) {
+            for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
+            qr.add_column(j, hcol.data());
+            col_added = true;
+            qr.solve(j + 1, yspec.data());
+            fused = true;
+          }
+          ST_TRY(S.enqueue_chain(j + 1, j >= 1 ? j - 1 : -1, fused ? yspec.data() : nullptr));
+        } else if (brk && j >= 1 && j + 1 < k) {  // no c_{j+1}: U_{j-1}'s residual on its own
+          ST_TRY(S.enqueue_finalize(j - 1));
         }
       }
-      ST_TRY(j == 0 ? wait_event(c->ev_arn) : S.wait_update(j - 1));
+      ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : S.wait_update(j - 1));
       prof_drain(c);
       if (pending >= 0) {  // finish iteration j-1: true residual + stop test (solvers.py:290-297)
         out->res_host[n_res++] = S.residual(pending);
@@ -2207,7 +2267,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
 
       if (!constrained) {
-        if (spec) std::copy(yspec.begin(), yspec.begin() + p, y.begin());  // the same solve
+        if (fused) std::copy(yspec.begin(), yspec.begin() + p, y.begin());  // the same solve
         else qr.solve(p, y.data());
       } else if (use_cb && m_active > 0) {
         // dict-form constraints: the host callback runs the constrained LS (and its fallback)
@@ -2291,10 +2351,19 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         out->y_host[static_cast<size_t>(j) * k + a] = y[a];
       }
       ws->n_iter_y = j + 1;
-      if (j + 2 < k && c->fuse_spmv) {
+      if (L) {
+        // x_j: from c_{j+1} (fused), else a GEMV beside c_{j+1} on the side stream, or after it
+        // on the main stream when c_{j+1} computed x_j from the speculative unconstrained y_j
+        if (!fused || constrained) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k && c->overlap_gemv));
+        if (j + 2 < k) {
+          if (stamps) stamps[j + 2] = now_s();
+          ST_TRY(S.enqueue_dual(j, j + 2));
+        } else {
+          ST_TRY(S.enqueue_residual(j));
+        }
+      } else if (j + 2 < k && c->fuse_spmv) {
         if (stamps) stamps[j + 2] = now_s();
-        // a speculative GEMV with the y taken stands; otherwise (constrained) it is redone
-        ST_TRY(S.enqueue_update_arnoldi(j, p, y.data(), j + 2, spec && !constrained));
+        ST_TRY(S.enqueue_update_arnoldi(j, p, y.data(), j + 2));
       } else {
         ST_TRY(S.enqueue_update(j, p, y.data()));
         if (j + 2 < k) {
@@ -2309,8 +2378,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
     // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
     // Arnoldi step, which never touches xj / r0), then one synchronisation
-    // (an unconsumed speculative GEMV writes the other x buffer; the stream waits for it below)
-    if (spec_any) HIP_TRY(hipStreamWaitValue64(s, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
     if (out->x_final_dev) {
       if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
       else HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));

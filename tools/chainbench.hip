@@ -1,0 +1,98 @@
+// chainbench.hip — MGS chain variants at solver size, timed with HIP events (tuning tool, not
+// part of libspis): K2p (dedicated gatherer), K2q (pipelined), K2q + fused update GEMV, and the
+// standalone GEMV, for Arnoldi steps j in {1, 5, 15, 29}.  Build: make tools/chainbench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
+
+using namespace spis;
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 1002252;
+  const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  const int kmax = 31;
+  const int64_t pitch = (n + 63) / 64 * 64;
+  std::vector<double> h(static_cast<size_t>(pitch) * (kmax + 1));
+  std::mt19937_64 rng(1);
+  std::normal_distribution<double> nd;
+  for (auto& v : h) v = nd(rng) * 1e-3;
+  double *Q, *w, *x0, *xo, *part, *gsub;
+  CK(hipMalloc(&Q, sizeof(double) * pitch * (kmax + 1)));
+  CK(hipMalloc(&w, sizeof(double) * pitch));
+  CK(hipMalloc(&x0, sizeof(double) * pitch));
+  CK(hipMalloc(&xo, sizeof(double) * pitch));
+  CK(hipMalloc(&part, sizeof(double) * 4096));
+  CK(hipMalloc(&gsub, sizeof(double) * 2048));
+  CK(hipMemcpy(Q, h.data(), sizeof(double) * pitch * (kmax + 1), hipMemcpyHostToDevice));
+  CK(hipMemcpy(w, h.data(), sizeof(double) * pitch, hipMemcpyHostToDevice));
+  CK(hipMemcpy(x0, h.data() + pitch, sizeof(double) * pitch, hipMemcpyHostToDevice));
+  CK(hipMemset(part, 0, sizeof(double) * 4096));
+  CK(hipMemset(gsub, 0, sizeof(double) * 2048));
+  unsigned long long* gran;
+  unsigned *ep, *err;
+  CK(hipMalloc(&gran, sizeof(unsigned long long) * kChainGranLag));
+  CK(hipMemset(gran, 0, sizeof(unsigned long long) * kChainGranLag));
+  CK(hipMalloc(&ep, 16));
+  CK(hipMemset(ep, 0, 16));
+  CK(hipMalloc(&err, 16));
+  CK(hipMemset(err, 0, 16));
+  double* hcol;
+  CK(hipHostMalloc(&hcol, sizeof(double) * 64, hipHostMallocMapped | hipHostMallocCoherent));
+  double* hcol_dev;
+  CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hcol_dev), hcol, 0));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<double> y(64, 0.01);
+  // the chain reads w and never writes it: repeated launches see the same inputs
+  const char* names[] = {"K2p agg", "K2q", "K2q+gemv", "gemv"};
+  for (int nt = 0; nt < 2; ++nt)
+    for (int j : {1, 5, 15, 29}) {
+      printf("n=%lld nt=%d j=%2d:", static_cast<long long>(n), nt, j);
+      for (int v = 0; v < 4; ++v) {
+        auto run = [&]() {
+          if (v == 0)
+            CK(launch_mgs_chain(n, w, Q, pitch, j, part, 1024, hcol_dev, gran, ep, err, s, nullptr, nullptr, 0,
+                                nullptr, nullptr, nullptr, true, nt));
+          else if (v == 1)
+            CK(launch_mgs_chain(n, w, Q, pitch, j, part, 1024, hcol_dev, gran, ep, err, s, nullptr, nullptr, 0,
+                                nullptr, nullptr, nullptr, true, nt, gsub));
+          else if (v == 2)
+            CK(launch_mgs_chain(n, w, Q, pitch, j, part, 1024, hcol_dev, gran, ep, err, s, nullptr, nullptr, 0,
+                                nullptr, nullptr, nullptr, true, nt, gsub, y.data(), j, x0, xo));
+          else
+            CK(launch_gemv(n, j, Q, pitch, y.data(), true, x0, xo, s));
+        };
+        run();
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) run();
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("  %s %7.1f us", names[v], 1e3 * ms / reps);
+      }
+      unsigned he = 0;
+      CK(hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost));
+      printf("%s\n", he ? "  CHAIN ERROR" : "");
+      if (he) return 1;
+    }
+  return 0;
+}

@@ -2,15 +2,20 @@
 sequence with start offsets, durations and the idle time on the main queue.  Usage:
   python tools/rocpd_timeline.py run_results.db [solve_index_from_end] [--iters]"""
 import collections
+import re
 import sqlite3
 import sys
 
-KEYS = ['mgs_chain_lag', 'mgs_chain_big', 'mgs_chain', 'spmv_pipe_kernel<1024, 4', 'spmv_pipe_kernel<1024, 3',
-        'spmv_pipe_kernel<1024, 1', 'spmv_pipe_kernel<1024, 2', 'constraint_gram', 'gemv', 'transpose',
+KEYS = ['mgs_chain_lag', 'mgs_chain_big', 'mgs_chain', 'constraint_gram', 'gemv', 'transpose',
         'gram_reduce', 'streamOpsWait', 'streamOpsWrite', 'copy_kernel', 'fillBuffer', 'copyBuffer', 'finalize']
+SPMV = re.compile(r'spmv_(pipe|rowblock|dual)\w*<(\d+), (\d+)')
+R0 = re.compile(r'spmv_(pipe_kernel<\d+, 3|rowblock_kernel<3>)')  # r0 = b - A x0 opens every solve
 
 
 def short(n):
+    m = SPMV.search(n)
+    if m:
+        return {'1': 'spmv x', '2': 'spmv res', '3': 'spmv r0', '4': 'spmv dual'}.get(m.group(3), 'spmv ' + m.group(3))
     for k in KEYS:
         if k in n:
             return k
@@ -22,7 +27,7 @@ def main():
     back = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith('-') else 2
     c = sqlite3.connect(db)
     rows = c.execute("select name, queue_id, start, end from kernels order by start").fetchall()
-    starts = [i for i, r in enumerate(rows) if 'spmv_pipe_kernel<1024, 3' in r[0] or 'spmv_rowblock_kernel<3>' in r[0]]
+    starts = [i for i, r in enumerate(rows) if R0.search(r[0])]
     s0, s1 = starts[-back], starts[-back + 1] if back > 1 else len(rows)
     seg = rows[s0:s1]
     t0 = seg[0][2]
