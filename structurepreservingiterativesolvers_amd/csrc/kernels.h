@@ -115,9 +115,12 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
 // distributive law; gsub[m] = q_m . q_{m-1}, written by chain m, read by the later chains of the
 // same basis); gran then needs kChainGranLag granules.  Beyond K2p's size it falls back to K2b.
 // K2q only: px > 0 fuses the GEMV xo = Q[:, :px] yx + x0 (px <= j, p <= kYArg; K4's arithmetic).
-constexpr int kChainGranLag = 10 * kChainMaxWG + 16;
+constexpr int kChainGranLag = 12 * kChainMaxWG + 16;
 constexpr int kLagDW = 8;  // K2q data waves per workgroup (+1 exchange wave): PER <= 4 pairs per thread
-constexpr int kLagNS = 4;  // K2q basis ring: q_{i-1} .. q_{i+2} in registers (2 steps of prefetch lead)
+constexpr int kLagDepth = 2;  // K2q: dot products this many MGS steps early (1 or 2)
+void set_chain_lag(int lag);  // tuning tools only (tools/chainbench): 1 or 2, process-wide
+constexpr int kLagNS = 5;     // K2q basis ring: q_{i-1} .. q_{i+3} in registers
+constexpr int kChainGsub = 2 * kMaxK + 8;  // K2q gsub: G(m, m-1) at [m], G(m, m-2) at [kMaxK + m]
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev = nullptr);
 

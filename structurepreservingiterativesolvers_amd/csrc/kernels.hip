@@ -1016,43 +1016,50 @@ __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// K2q: pipelined MGS chain (SPIS_OPT_MGS_CHAIN = 3).  MGS's projections, with each dot product
-// evaluated one step early by the distributive law:
-//     h_{i+1} = q_{i+1} . w^{(i+1)} = q_{i+1} . w^{(i)} - h_i (q_{i+1} . q_i),
-// w^{(i+1)} = w^{(i)} - h_i q_i (the update itself is MGS's, in registers, contraction off).  The
-// partial of q_{i+1} . w^{(i)} needs only h_{i-1}, so the exchange that produces h_{i+1} starts
-// while the one producing h_i is still in flight: two exchanges overlap and each Arnoldi step
-// waits for about half a round trip per MGS step instead of a whole one.  The sub-diagonal Gram
-// entries g_m = q_m . q_{m-1} do not change once both vectors exist: chain j computes the new one,
-// g_j (partials published beside those of h_j), and keeps it in gsub[j] for the chains after it.
-// The dedicated gathering workgroup (the last) sums each step's partials in a fixed order, forms
-// h_m = A_m - h_{m-1} g_m (every workgroup gets the same bits) and publishes it; it also writes
-// H[:, j] to the host.  Exact arithmetic: the identity above, no orthogonality assumed.  Rounding:
-// the error of h_{i+1} is eps |w^{(i)}| instead of MGS's eps |w^{(i+1)}|.
-// Basis slices rotate through NS register slots (5; 4 at PER 8, where 5 spill) without moves: the step body is instantiated
-// for each ring position (vector q_m lives in slot m % NS; q_{i+NS-1} is loaded into q_{i-1}'s
-// slot right after the update that consumed it, NS - 2 steps before it is needed).
+// K2q: pipelined MGS chain (SPIS_OPT_MGS_CHAIN = 3, the default).  MGS's projections and updates,
+// with each dot product evaluated LAG steps early by the distributive law:
+//     h_m = q_m . w^{(m)} = q_m . w^{(m-LAG)} - sum_{l = m-LAG}^{m-1} h_l (q_m . q_l),
+// w^{(i+1)} = w^{(i)} - h_i q_i (the update itself is MGS's, in registers, contraction off; for
+// m < LAG the dot is taken against w^{(0)} and every earlier h_l is subtracted).  The partial of
+// q_m . w^{(m-LAG)} needs h_{m-LAG-1} only, so LAG + 1 exchanges are in flight and an Arnoldi
+// step waits for about 1 / (LAG + 1) of a round trip per MGS step instead of a whole one.  The
+// Gram entries G(m, l) = q_m . q_l, l = m-LAG .. m-1, do not change once q_m exists: chain j
+// computes the new ones, G(j, j-LAG .. j-1) (partials published beside those of h_j), and keeps
+// them in gsub for the later chains of the same basis.  The dedicated gathering workgroup (the
+// last) sums each step's partials in a fixed order, forms h_m (the correction terms in l order;
+// every workgroup gets the same bits), publishes it and writes H[:, j] to the host.
+// Exact arithmetic: the identity above, no orthogonality assumed.  Rounding: the error of h_m is
+// eps |w^{(m-LAG)}| instead of MGS's eps |w^{(m)}|.
+// Basis slices rotate through NS register slots without moves (vector q_m in slot m % NS; the
+// step body is instantiated per ring position): q_{i+NS-1} is loaded into q_{i-1}'s slot right
+// after the update that consumed it, NS - LAG - 1 steps before it is dotted.
+// Vectors are handled as ceil(n / 2) pairs: an odd n's last pair reaches into the basis' zero
+// padding (pitch > n; the padding of Q, w and x0 is zeroed at allocation and never written
+// nonzero), so no thread has a scalar tail.
 // Slots: E_m (the exchange producing h_m, m = 1..j; E_{j+1} = ||w||^2) uses tag base + m, partial
-// ring m % 4, h ring m % 4; g_j's partials have their own granules.  Ring safety: a workgroup
-// publishes E_m after it has read h_{m-2}, which the gatherer published after reading E_{m-4}'s
-// partials; the gatherer publishes h_m after reading E_m, which every workgroup publishes after
-// it read h_{m-4} (and earlier h's).
+// ring m % 4, h ring m % 4; G(j, .)'s partials have their own granules.  Ring safety (LAG <= 2):
+// a workgroup publishes E_m once it has read h_{m-LAG-1}, which the gatherer published after
+// reading E_{m-4}'s partials; the gatherer publishes h_m after reading E_m, which every workgroup
+// publishes after it read h_{m-LAG-1} >= h_{m-3}, the last reader of h slot m % 4 before.
+// FX: the update GEMV x = Q[:, :px] yx + x0 of the previous LS step rides along (K4's
+// arithmetic: the sum in basis order, then + x0), accumulated in LDS as each q_i passes (each
+// thread its own entries: no barrier; in registers it spilled); x = acc + x0 is stored after the
+// chain's last exchange.
 // ---------------------------------------------------------------------------------------------
 // DW data waves hold the slices (DW * 64 threads x PER pairs each); wave DW runs the exchange.
-template <int DW, int PER, int NS, bool FX, bool NT>
+template <int DW, int PER, int NS, int LAG, bool FX, bool NT>
 __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     int64_t n, const double* __restrict__ w, double* __restrict__ Q, int64_t pitch, int j,
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    bool nt, YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
+    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
 #pragma clang fp contract(off)
-  // FX: the update GEMV x = Q[:, :px] yx + x0 of the previous LS step rides along (K4's
-  // arithmetic: the sum in basis order, then + x0), accumulated in LDS as each q_i passes (the
-  // thread's own entries: no barrier); x = acc + x0 is stored after the chain's last exchange
+  static_assert(LAG >= 1 && LAG <= 2 && NS >= LAG + 3, "ring: q_{i-1}, the dotted q_{i+LAG}, one loading");
   constexpr int DT = DW * 64;  // data threads
-  __shared__ double2 s_acc[FX ? PER * DT : 1];  // (in registers it spilled)
-  __shared__ double s_wave[2 * DW];
+  constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
+  __shared__ double2 s_acc[FX ? PER * DT : 1];
+  __shared__ double s_wave[NV * DW];
   __shared__ double s_h;
   __shared__ int s_fail;
   const int G = gridDim.x;
@@ -1060,19 +1067,16 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   const int tid = threadIdx.x;
   const bool agg = static_cast<int>(blockIdx.x) == GD;
   const bool data = tid < DT && !agg;
-  const int64_t npair = n >> 1;
+  const int64_t npair = (n + 1) >> 1;  // the last pair of an odd n reaches into the zero padding
   const int64_t p0 = static_cast<int64_t>(blockIdx.x) * DT * PER + tid;
-  const bool tail = (n & 1) && blockIdx.x == 0 && tid == 0;  // odd element: workgroup 0, lane 0
-  unsigned long long* aslots = gran;                             // 4 x 2 kChainMaxWG
-  unsigned long long* gslots = gran + 8 * kChainMaxWG;           // 2 kChainMaxWG (g_j)
-  unsigned long long* hslots = gran + 10 * kChainMaxWG;          // 4 x 2
+  unsigned long long* aslots = gran;                       // 4 x 2 kChainMaxWG
+  unsigned long long* gslots = gran + 8 * kChainMaxWG;     // LAG x 2 kChainMaxWG (G(j, .))
+  unsigned long long* hslots = gran + 12 * kChainMaxWG;    // 4 x 2
+  double* gs1 = gsub;          // G(m, m-1)
+  double* gs2 = gsub + kMaxK;  // G(m, m-2)
   const unsigned base = *epoch;
   double2 y[PER];
   double2 S[NS][PER];
-  double yt = 0.0, st[NS], acct = 0.0;
-#pragma unroll
-  for (int r = 0; r < NS; ++r) st[r] = 0.0;
-  // (buffer-descriptor loads here, to save address registers, measured 1.0-1.4x slower)
   auto load = [&](double2 (&r)[PER], const double* v) {
     const double2* v2 = reinterpret_cast<const double2*>(v);
 #pragma unroll
@@ -1085,13 +1089,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       for (int k = 0; k < PER; ++k) s_acc[k * DT + tid] = make_double2(0.0, 0.0);
     }
     load(y, w);
-    if (tail) yt = w[n - 1];
 #pragma unroll
     for (int m = 0; m < NS - 1; ++m)
-      if (m <= j) {
-        load(S[m], Q + static_cast<int64_t>(m) * pitch);
-        if (tail) st[m] = Q[static_cast<int64_t>(m) * pitch + n - 1];
-      }
+      if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch);
   }
   if (tid == 0) s_fail = 0;
   const double h0 = chain_sum_partials(part_in, n_in, s_wave);
@@ -1104,9 +1104,12 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     if (tid >= 64) return;
     const int lane = tid;
     // the whole column H[:, j] is written by this lane; H[j+1, j] last, behind a system-scope
-    // release, so a host that sees it (the solver's speculative update, spis.cpp) sees the column
+    // release, so a host that sees it (the solver's L mode, spis.cpp) sees the column
     if (lane == 0) hcol[0] = h0;
-    double hprev = h0;
+    double hl[LAG];  // h_{m-LAG} .. h_{m-1} (hl[LAG-1] = h_{m-1})
+#pragma unroll
+    for (int l = 0; l < LAG; ++l) hl[l] = 0.0;
+    hl[LAG - 1] = h0;
     for (int m = 1; m <= j + 1; ++m) {
       const unsigned tag = base + static_cast<unsigned>(m);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -1140,22 +1143,30 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         *out = wave_sum_dpp(acc);
         return all_ok;
       };
-      double A = 0.0;
-      bool ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &A);
-      double hm;
+      double hm = 0.0;
+      bool ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &hm);
       if (m <= j) {
-        double g = 0.0;
-        if (m == j) {
-          ok = ok && sweep(gslots, &g);
-          if (lane == 0) gsub[j] = g;
-        } else {
-          g = gsub[m];
+        // h_m = a_m - sum_{l = max(0, m-LAG)}^{m-1} h_l G(m, l), l ascending
+        double gv[LAG];
+#pragma unroll
+        for (int d = 0; d < LAG; ++d) {  // gv[d] = G(m, m - LAG + d)
+          gv[d] = 0.0;
+          const int l = m - LAG + d;
+          if (l < 0) continue;
+          if (m == j) {
+            ok = ok && sweep(gslots + static_cast<size_t>(LAG - 1 - d) * 2 * kChainMaxWG, &gv[d]);
+            if (lane == 0) (LAG - d == 1 ? gs1 : gs2)[j] = gv[d];
+          } else {
+            gv[d] = (LAG - d == 1 ? gs1 : gs2)[m];
+          }
         }
-        const double t = hprev * g;
-        hm = A - t;
-      } else {
-        hm = A;  // E_{j+1}: ||w^{(j+1)}||^2, square-rooted by every workgroup
-      }
+#pragma unroll
+        for (int d = 0; d < LAG; ++d) {
+          if (m - LAG + d < 0) continue;
+          const double t = hl[d] * gv[d];
+          hm = hm - t;
+        }
+      }  // else E_{j+1}: ||w^{(j+1)}||^2, square-rooted by every workgroup
       if (!ok) {
         if (lane == 0) atomicOr(err, 1u);
         hm = 0.0;  // the data workgroups time out as well and report the failure
@@ -1175,7 +1186,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         }
       }
       if (!ok) return;
-      hprev = hm;
+#pragma unroll
+      for (int l = 0; l + 1 < LAG; ++l) hl[l] = hl[l + 1];
+      hl[LAG - 1] = hm;
     }
     if (lane == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
     return;
@@ -1215,36 +1228,35 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     __syncthreads();  // s_h is rewritten by the next wait
     return !failed;
   };
-  // workgroup partial(s) -> granules {tag, half} (sc1 stores from a data wave)
-  auto publish2 = [&](double pa, double pb, bool with_b, int m) {
-    const double wa = wave_sum_dpp(pa);
-    const double wb = with_b ? wave_sum_dpp(pb) : 0.0;
+  // the workgroup's partials of E_m: v[0] = a_m, v[1 + d] = G(m, m - LAG + d) when ng > 0
+  // (granules {tag, half}, sc1 stores from a data wave)
+  auto publish_m = [&](const double (&v)[NV], bool with_g, int m) {
+    double wv[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) wv[c] = (c == 0 || with_g) ? wave_sum_dpp(v[c]) : 0.0;
     if (data && (tid & 63) == 0) {
-      s_wave[tid >> 6] = wa;
-      s_wave[DW + (tid >> 6)] = wb;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) s_wave[c * DW + (tid >> 6)] = wv[c];
     }
     __syncthreads();
     if (tid == 0) {
       const unsigned tag = base + static_cast<unsigned>(m);
-      double ta = s_wave[0];
 #pragma unroll
-      for (int v = 1; v < DW; ++v) ta += s_wave[v];
-      const unsigned long long ba = static_cast<unsigned long long>(__double_as_longlong(ta));
-      unsigned long long* sl = aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG + 2 * blockIdx.x;
-      chain_store(sl, tag, static_cast<unsigned>(ba));
-      chain_store(sl + 1, tag, static_cast<unsigned>(ba >> 32));
-      if (with_b) {
-        double tb = s_wave[DW];
+      for (int c = 0; c < NV; ++c) {
+        if (c > 0 && (!with_g || m - LAG + (c - 1) < 0)) continue;
+        double t = s_wave[c * DW];
 #pragma unroll
-        for (int v = 1; v < DW; ++v) tb += s_wave[DW + v];
-        const unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(tb));
-        chain_store(gslots + 2 * blockIdx.x, tag, static_cast<unsigned>(bb));
-        chain_store(gslots + 2 * blockIdx.x + 1, tag, static_cast<unsigned>(bb >> 32));
+        for (int q = 1; q < DW; ++q) t += s_wave[c * DW + q];
+        const unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(t));
+        unsigned long long* sl = c == 0 ? aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG + 2 * blockIdx.x
+                                        : gslots + static_cast<size_t>(LAG - c) * 2 * kChainMaxWG + 2 * blockIdx.x;
+        chain_store(sl, tag, static_cast<unsigned>(bb));
+        chain_store(sl + 1, tag, static_cast<unsigned>(bb >> 32));
       }
     }
   };
   // y -= h q (MGS's update, contraction off)
-  auto update = [&](double h, const double2 (&q)[PER], double qt) {
+  auto update = [&](double h, const double2 (&q)[PER]) {
 #pragma unroll
     for (int k = 0; k < PER; ++k)
       if (data && p0 + k * DT < npair) {
@@ -1252,34 +1264,54 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         y[k].x = y[k].x - a0;
         y[k].y = y[k].y - a1;
       }
-    if (tail) {
-      const double a = h * qt;
-      yt = yt - a;
-    }
+  };
+  // partials of E_m with q_m in slot RD: a_m = q_m . y (y = w^{(max(0, m-LAG))} when called),
+  // with G(m, l) for m == j (the slots of q_l: RD - LAG + d, ring order)
+  auto dots = [&](auto RDC, int m) {
+    constexpr int RD = decltype(RDC)::value;
+    const bool with_g = m == j;
+    double v[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) v[c] = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (data && p0 + k * DT < npair) {
+        v[0] += S[RD][k].x * y[k].x;
+        v[0] += S[RD][k].y * y[k].y;
+        if (with_g) {
+#pragma unroll
+          for (int d = 0; d < LAG; ++d) {
+            const int rl = (RD - LAG + d + 2 * NS) % NS;  // constant once unrolled
+            v[1 + d] += S[RD][k].x * S[rl][k].x;
+            v[1 + d] += S[RD][k].y * S[rl][k].y;
+          }
+        }
+      }
+    publish_m(v, with_g, m);
   };
   // one MGS step at ring position R = i % NS; false once the chain is finished (or failed)
   auto step = [&](auto RC, int i) -> bool {
     constexpr int R = decltype(RC)::value;
     constexpr int RM = (R + NS - 1) % NS;  // q_{i-1}, then q_{i+NS-1}
-    constexpr int RD = (R + 1) % NS;       // q_{i+1}
     if (i >= 1) {
       double hu = h0;
       if (i - 1 >= 1 && !wait_h(i - 1, &hu)) return false;
-      update(hu, S[RM], st[RM]);
+      update(hu, S[RM]);
     }
     if (i == j) {  // last: subtract h_j q_j, ||w||^2 through the gatherer, normalise
       double hj = h0;
       if (j >= 1 && !wait_h(j, &hj)) return false;
-      update(hj, S[R], st[R]);
-      double part = 0.0;
+      update(hj, S[R]);
+      double v[NV];
+#pragma unroll
+      for (int c = 0; c < NV; ++c) v[c] = 0.0;
 #pragma unroll
       for (int k = 0; k < PER; ++k)
         if (data && p0 + k * DT < npair) {
-          part += y[k].x * y[k].x;
-          part += y[k].y * y[k].y;
+          v[0] += y[k].x * y[k].x;
+          v[0] += y[k].y * y[k].y;
         }
-      if (tail) part += yt * yt;
-      publish2(part, 0.0, false, j + 1);
+      publish_m(v, false, j + 1);
       double nn = 0.0;
       if (!wait_h(j + 1, &nn)) return false;
       const double hh = sqrt(nn);
@@ -1288,7 +1320,6 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       for (int k = 0; k < PER; ++k)
         if (data && p0 + k * DT < npair)
           q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
-      if (tail) Q[static_cast<int64_t>(j + 1) * pitch + n - 1] = hh == 0.0 ? 0.0 : yt / hh;
       if (FX) {
         const double2* x02 = reinterpret_cast<const double2*>(x0);
         double2* xo2 = reinterpret_cast<double2*>(xo);
@@ -1299,7 +1330,6 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
             const double2 b = x02[p0 + k * DT];
             xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
           }
-        if (tail) xo[n - 1] = acct + x0[n - 1];
       }
       return false;
     }
@@ -1314,34 +1344,14 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
           a.y = a.y + m1;
           s_acc[k * DT + tid] = a;
         }
-      if (tail) {
-        const double m = st[R] * cf;
-        acct = acct + m;
-      }
     }
-    // q_{i+NS-1} into the slot q_{i-1} just left (NS - 2 steps of lead)
-    if (i + NS - 1 <= j) {
-      load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
-      if (tail) st[RM] = Q[static_cast<int64_t>(i + NS - 1) * pitch + n - 1];
+    // q_{i+NS-1} into the slot q_{i-1} just left
+    if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
+    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
+    if (i == 0) {
+      if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
     }
-    // partial of h_{i+1}'s dot q_{i+1} . w^{(i)}; at i + 1 == j also g_j = q_j . q_{j-1}
-    const bool with_b = i + 1 == j;
-    double pa = 0.0, pb = 0.0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * DT < npair) {
-        pa += S[RD][k].x * y[k].x;
-        pa += S[RD][k].y * y[k].y;
-        if (with_b) {
-          pb += S[RD][k].x * S[R][k].x;
-          pb += S[RD][k].y * S[R][k].y;
-        }
-      }
-    if (tail) {
-      pa += st[RD] * yt;
-      if (with_b) pb += st[RD] * st[R];
-    }
-    publish2(pa, pb, with_b, i + 1);
+    if (i + LAG <= j) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
     return true;
   };
   for (int i = 0;; i += NS) {
@@ -1351,6 +1361,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     if (!step(std::integral_constant<int, 3>{}, i + 3)) break;
     if constexpr (NS > 4) {
       if (!step(std::integral_constant<int, 4>{}, i + 4)) break;
+    }
+    if constexpr (NS > 5) {
+      if (!step(std::integral_constant<int, 5>{}, i + 5)) break;
     }
   }
 }
@@ -1552,6 +1565,9 @@ __global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
   if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
 }
 
+static int g_chain_lag = kLagDepth;
+void set_chain_lag(int lag) { g_chain_lag = lag == 1 ? 1 : 2; }
+
 hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch, int j, const double* part_in,
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
@@ -1587,27 +1603,36 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
   if (gsub != nullptr) {  // K2q: always with the dedicated gatherer; 8 data waves (kLagDW)
     const int64_t wd = kChainMaxWG - 1;
     constexpr int DT = kLagDW * 64;
-    const int per = npair <= wd * DT * 1 ? 1 : npair <= wd * DT * 2 ? 2 : 4;
+    const int64_t npr = (n + 1) >> 1;  // K2q pads an odd n's last pair with the zero padding
+    if (pitch < 2 * npr) return hipErrorInvalidValue;
+    const int per = npr <= wd * DT * 1 ? 1 : npr <= wd * DT * 2 ? 2 : 4;
     const int64_t span = int64_t(DT) * per;
-    const int GD = static_cast<int>(std::max<int64_t>(1, (npair + span - 1) / span));
+    const int GD = static_cast<int>(std::max<int64_t>(1, (npr + span - 1) / span));
     if (GD > wd) return hipErrorInvalidValue;
     if (px < 0 || px > j || px > kYArg || (px > 0 && (!yx_host || !x0 || !xo || !aligned16(x0) || !aligned16(xo))))
       return hipErrorInvalidValue;
     YArg ya;
     for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
-#define SPIS_LAG(PER_, FX_, NT_)                                                                                 \
-  launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, pitch, j, \
-           part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, nt, ya, px, x0, xo)
-#define SPIS_LAG_PER(FX_, NT_)          \
-  switch (per) {                        \
-    case 1: SPIS_LAG(1, FX_, NT_); break; \
-    case 2: SPIS_LAG(2, FX_, NT_); break; \
-    default: SPIS_LAG(4, FX_, NT_); break; \
+#define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
+  launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
+           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo)
+#define SPIS_LAG_PER(FX_, NT_, LAG_)          \
+  switch (per) {                              \
+    case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \
+    case 2: SPIS_LAG(2, FX_, NT_, LAG_); break; \
+    default: SPIS_LAG(4, FX_, NT_, LAG_); break; \
   }
-    if (px > 0 && nt) SPIS_LAG_PER(true, true)
-    else if (px > 0) SPIS_LAG_PER(true, false)
-    else if (nt) SPIS_LAG_PER(false, true)
-    else SPIS_LAG_PER(false, false)
+#define SPIS_LAG_D(LAG_)                                     \
+  if (px > 0 && nt) SPIS_LAG_PER(true, true, LAG_)           \
+  else if (px > 0) SPIS_LAG_PER(true, false, LAG_)           \
+  else if (nt) SPIS_LAG_PER(false, true, LAG_)               \
+  else SPIS_LAG_PER(false, false, LAG_)
+    if (g_chain_lag == 1) {
+      SPIS_LAG_D(1)
+    } else {
+      SPIS_LAG_D(2)
+    }
+#undef SPIS_LAG_D
 #undef SPIS_LAG_PER
 #undef SPIS_LAG
     return hipGetLastError();

@@ -145,7 +145,7 @@ struct spis_context {
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
   uint64_t gemv_seq = 0;
   unsigned long long* chain_gran = nullptr;  // exchange granules (kChainGranLag: K2p / K2b / K2q layouts)
-  double* chain_gsub = nullptr;              // K2q: gsub[m] = q_m . q_{m-1} of the current basis
+  double* chain_gsub = nullptr;              // K2q: Gram entries q_m . q_{m-1}, q_m . q_{m-2} (kChainGsub)
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
   unsigned* chain_err_dev = nullptr;
@@ -472,8 +472,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
     HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * kChainGranLag));
     HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * kChainGranLag));
-    HIP_TRY(hipMalloc(&c->chain_gsub, sizeof(double) * (kMaxK + 8)));
-    HIP_TRY(hipMemset(c->chain_gsub, 0, sizeof(double) * (kMaxK + 8)));
+    HIP_TRY(hipMalloc(&c->chain_gsub, sizeof(double) * kChainGsub));
+    HIP_TRY(hipMemset(c->chain_gsub, 0, sizeof(double) * kChainGsub));
     HIP_TRY(hipMalloc(&c->chain_epoch, 16));
     HIP_TRY(hipMemset(c->chain_epoch, 0, 16));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->chain_err), 16, hipHostMallocMapped));

@@ -36,12 +36,12 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&x0, sizeof(double) * pitch));
   CK(hipMalloc(&xo, sizeof(double) * pitch));
   CK(hipMalloc(&part, sizeof(double) * 4096));
-  CK(hipMalloc(&gsub, sizeof(double) * 2048));
+  CK(hipMalloc(&gsub, sizeof(double) * kChainGsub));
   CK(hipMemcpy(Q, h.data(), sizeof(double) * pitch * (kmax + 1), hipMemcpyHostToDevice));
   CK(hipMemcpy(w, h.data(), sizeof(double) * pitch, hipMemcpyHostToDevice));
   CK(hipMemcpy(x0, h.data() + pitch, sizeof(double) * pitch, hipMemcpyHostToDevice));
   CK(hipMemset(part, 0, sizeof(double) * 4096));
-  CK(hipMemset(gsub, 0, sizeof(double) * 2048));
+  CK(hipMemset(gsub, 0, sizeof(double) * kChainGsub));
   unsigned long long* gran;
   unsigned *ep, *err;
   CK(hipMalloc(&gran, sizeof(unsigned long long) * kChainGranLag));
@@ -62,9 +62,11 @@ int main(int argc, char** argv) {
   std::vector<double> y(64, 0.01);
   // the chain reads w and never writes it: repeated launches see the same inputs
   const char* names[] = {"K2p agg", "K2q", "K2q+gemv", "gemv"};
+  for (int lag = 1; lag <= 2; ++lag)
   for (int nt = 0; nt < 2; ++nt)
-    for (int j : {1, 5, 15, 29}) {
-      printf("n=%lld nt=%d j=%2d:", static_cast<long long>(n), nt, j);
+    for (int j : {1, 2, 5, 15, 29}) {
+      set_chain_lag(lag);
+      printf("n=%lld lag=%d nt=%d j=%2d:", static_cast<long long>(n), lag, nt, j);
       for (int v = 0; v < 4; ++v) {
         auto run = [&]() {
           if (v == 0)
