@@ -164,7 +164,7 @@ def main():
     ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],
                     help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
                          "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
-    ap.add_argument("--gram", default="ell", choices=["staged", "ell", "csr"],
+    ap.add_argument("--gram", default="mfma", choices=["staged", "ell", "csr", "mfma", "mfma_full"],
                     help="constraint-Gram matrix form (SPIS_OPT_ELL_GRAM)")
     ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "stride2", "xcd2", "auto"],
                     help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
@@ -204,7 +204,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, args.chain), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2}[args.gram]),
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5}[args.spmv_pipe]),
                "spis_set_option")

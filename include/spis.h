@@ -126,11 +126,14 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   1 = CGS2, classical Gram-Schmidt with one re-orthogonalisation pass (3 reductions per
  *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
  *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only.
- * SPIS_OPT_ELL_GRAM (default 1): how the fused constraint reduction (p + 1 <= 32) reads each
- *   constraint matrix, from a copy built once on first use: 1 = sliced ELL (static row
+ * SPIS_OPT_ELL_GRAM (default 3): how the fused constraint reduction (p + 1 <= 32) reads each
+ *   constraint matrix, from a copy built once on first use: 3 = on the f64 matrix cores, a
+ *   symmetric matrix from a slot table of its upper triangle (K7t: G = H + H^T, half the
+ *   gathers), any other from its CSR (K7m); 4 = K7m for every matrix; 1 = sliced ELL (static row
  *   boundaries), 2 = row chunks with their distinct columns (the basis rows of those columns
  *   staged in LDS once per chunk; a matrix with a row of > 64 entries or > 176 distinct columns
- *   falls back to 1; measured 12% slower than 1 at C3), 0 = the CSR itself.
+ *   falls back to 1; measured 12% slower than 1 at C3), 0 = the CSR itself.  C3 (swe energy
+ *   matrix, p = 30): K7t 122 us, K7m 232 us, ELL 326 us, staged 371 us.
  * SPIS_OPT_MGS_CHAIN (default 3): each Arnoldi step's MGS chain + normalise runs as one persistent
  *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 2 = the
  *   partials are gathered by a dedicated workgroup that holds no slice (N <= 2^20 - 4096), 1 = by

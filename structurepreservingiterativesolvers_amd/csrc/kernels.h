@@ -142,8 +142,9 @@ hipError_t launch_spmm(const CsrView& A, const double* X, int64_t ldx, int nvec,
                        int64_t ldy, hipStream_t s);
 size_t gram_lds_bytes(int nu, int nv);
 // Ut (n x (p+1), row-major) = [Z[:, :p], x0]^T
+// (perm: K7m's column order, position 2i = column i, 2i + 1 = column i + 16; p + 1 <= 32)
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
-                                  double* Ut, hipStream_t s);
+                                  double* Ut, hipStream_t s, bool perm = false);
 // G = [U^T M U | U^T v_0 .. U^T v_{nvv-1}] from Ut (M may be null: linear terms only);
 // partials: constraint_gram_partials() x (np1*np1 + nvv*np1) doubles
 int constraint_gram_partials();
@@ -183,6 +184,33 @@ hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, cons
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
                                   const double* const* v, double* partials, double* G, hipStream_t s,
                                   const EllView* ell = nullptr);
+// K7m: the same reduction on the f64 matrix cores from M's CSR (np1 <= 32, Ut in perm order).
+// split: the row bounds of the 8 XCD groups (balanced by nonzeros + rows; gram_split)
+struct GramSplit {
+  int32_t row[9];
+};
+void gram_split(int64_t n, const int32_t* indptr, GramSplit* out);
+// K7t (symmetric M): slot table of 4-row-group segments packed into blocks of ns = 16 slots:
+// block b's entries (row-in-group g, slot t) at b * 4 ns + g ns + t, mask[b] = segment-start
+// bits | (slots used << 32); G (np1 x np1) = H + H^T
+struct SymTabView {
+  const int32_t* col;
+  const double* val;
+  const unsigned long long* mask;
+  int32_t nblk;
+  int32_t ns;
+};
+hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
+                                      hipStream_t s);
+// Ut in the perm order plus the linear terms Gv[c][a] = sum_r U[r][a] v_c[r] (vpart: partials of
+// kTransposeGrid x nvv np1; Gv: nvv x np1); np1 <= 32, nvv <= 4
+constexpr int kTransposeGrid = 2048;
+hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                      double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
+                                      hipStream_t s);
+hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, const GramSplit* split,
+                                       const double* Ut, int nvv, const double* const* v, double* partials,
+                                       double* G, hipStream_t s);
 // partial dot / sum of squares
 hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_out, int grid,
                       hipStream_t s);

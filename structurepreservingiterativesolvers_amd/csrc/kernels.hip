@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -2223,6 +2224,26 @@ __global__ __launch_bounds__(kBlock) void gram_partial_kernel(int64_t n, int nu,
   }
 }
 
+// out[j] = sum over rows of part[row][j] (row-major rows x npairs), one workgroup per output:
+// strided per-thread sums then block_sum's fixed tree (deterministic); optional symmetrize:
+// out[a np1 + b] += (the same sum of part[.][b np1 + a]) for the np1 x np1 prefix (K7t's H + H^T)
+__global__ __launch_bounds__(kBlock) void reduce_cols_kernel(int npairs, int rows, const double* __restrict__ part,
+                                                             double* __restrict__ out, int sym_np1) {
+  __shared__ double s_wave[4];
+  const int j = blockIdx.x;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < rows; r += kBlock) s += part[static_cast<int64_t>(r) * npairs + j];
+  double tot = block_sum(s, s_wave);
+  if (sym_np1 > 0 && j < sym_np1 * sym_np1) {
+    const int a = j / sym_np1, b = j - (j / sym_np1) * sym_np1;
+    const int jt = b * sym_np1 + a;
+    double st = 0.0;
+    for (int r = threadIdx.x; r < rows; r += kBlock) st += part[static_cast<int64_t>(r) * npairs + jt];
+    tot = tot + block_sum(st, s_wave);
+  }
+  if (threadIdx.x == 0) out[j] = tot;
+}
+
 __global__ __launch_bounds__(kBlock) void gram_reduce_kernel(int npairs, int grid,
                                                              const double* __restrict__ partials,
                                                              double* __restrict__ G) {
@@ -2277,26 +2298,53 @@ hipError_t launch_gram(int64_t n, int nu, const double* const* U, int nv, const 
 // Ut row stride: 32 doubles (256 B, 16-B aligned rows) for np1 <= 32, else 64; zero padded
 __host__ __device__ __forceinline__ int ut_ld(int np1) { return np1 <= 32 ? 32 : 64; }
 
+// perm (ld 32 only, K7m / K7t): row position 2i holds column i and position 2i + 1 column
+// i + 16, so that one 16-B load of lane i gives the two MFMA tiles' column i.
+// nvv > 0 (K7t): the linear terms Gv[c][a] = sum_r U[r][a] v_c[r] ride along (the tile is in
+// LDS anyway): thread c * np1 + a sums its tiles' rows in order, one partial per block in
+// vpart[block][c * np1 + a] (grid-stride over the 64-row tiles, so a fixed grid).
 __global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int p,
                                                                  const double* __restrict__ Z,
                                                                  int64_t pitch,
                                                                  const double* __restrict__ x0,
-                                                                 double* __restrict__ Ut) {
-  extern __shared__ __attribute__((aligned(16))) double tile[];  // np1 x 65
+                                                                 double* __restrict__ Ut, bool perm, int nvv,
+                                                                 const double* __restrict__ v0,
+                                                                 const double* __restrict__ v1,
+                                                                 const double* __restrict__ v2,
+                                                                 const double* __restrict__ v3,
+                                                                 double* __restrict__ vpart) {
+  extern __shared__ __attribute__((aligned(16))) double tile[];  // np1 x 65, then 4 x 64 (v)
   const int np1 = p + 1;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int rows = static_cast<int>(n - r0 < 64 ? n - r0 : 64);
-  for (int idx = threadIdx.x; idx < np1 * 64; idx += kBlock) {
-    const int a = idx >> 6, r = idx & 63;
-    if (r < rows) tile[a * 65 + r] = a < p ? Z[a * pitch + r0 + r] : x0[r0 + r];
-  }
-  __syncthreads();
+  double* s_v = tile + np1 * 65;
+  const double* vv[4] = {v0, v1, v2, v3};
   const int ld = ut_ld(np1);
-  double* out = Ut + r0 * ld;
-  for (int idx = threadIdx.x; idx < rows * ld; idx += kBlock) {
-    const int r = idx / ld, a = idx - (idx / ld) * ld;
-    out[idx] = a < np1 ? tile[a * 65 + r] : 0.0;
+  const int nl = nvv * np1;
+  const int tc = threadIdx.x / np1, ta = threadIdx.x - tc * np1;  // this thread's linear term
+  double lin = 0.0;
+  const int64_t ntiles = (n + 63) / 64;
+  for (int64_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    const int64_t r0 = tb * 64;
+    const int rows = static_cast<int>(n - r0 < 64 ? n - r0 : 64);
+    for (int idx = threadIdx.x; idx < np1 * 64; idx += kBlock) {
+      const int a = idx >> 6, r = idx & 63;
+      if (r < rows) tile[a * 65 + r] = a < p ? Z[a * pitch + r0 + r] : x0[r0 + r];
+    }
+    if (nvv > 0) {
+      const int c = threadIdx.x >> 6, r = threadIdx.x & 63;
+      if (c < nvv) s_v[c * 64 + r] = r < rows ? vv[c][r0 + r] : 0.0;
+    }
+    __syncthreads();
+    double* out = Ut + r0 * ld;
+    for (int idx = threadIdx.x; idx < rows * ld; idx += kBlock) {
+      const int r = idx / ld, pos = idx - (idx / ld) * ld;
+      const int a = perm ? (pos >> 1) + ((pos & 1) << 4) : pos;
+      out[idx] = a < np1 ? tile[a * 65 + r] : 0.0;
+    }
+    if (threadIdx.x < nl)
+      for (int r = 0; r < rows; ++r) lin += tile[ta * 65 + r] * s_v[tc * 64 + r];
+    __syncthreads();
   }
+  if (vpart != nullptr && threadIdx.x < nl) vpart[static_cast<int64_t>(blockIdx.x) * nl + threadIdx.x] = lin;
 }
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -2823,17 +2871,275 @@ hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, cons
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int npairs = np1 * np1 + nvv * np1;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs, grid, partials, G);
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, grid, partials, G, 0);
   return hipGetLastError();
 }
 
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
-                                  double* Ut, hipStream_t s) {
+                                  double* Ut, hipStream_t s, bool perm) {
   const int np1 = p + 1;
-  if (np1 > 64) return hipErrorInvalidValue;
+  if (np1 > 64 || (perm && np1 > 32)) return hipErrorInvalidValue;
   const int64_t g = (n + 63) / 64;
   hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
-                     static_cast<size_t>(np1) * 65 * sizeof(double), s, n, p, Z, pitch, x0, Ut);
+                     static_cast<size_t>(np1) * 65 * sizeof(double) + 4 * 64 * sizeof(double), s, n, p, Z, pitch,
+                     x0, Ut, perm, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                      double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
+                                      hipStream_t s) {
+  const int np1 = p + 1;
+  if (np1 > 32 || nvv < 0 || nvv > 4 || nvv * np1 > kBlock) return hipErrorInvalidValue;
+  const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int c = 0; c < nvv; ++c) vv[c] = v[c];
+  const int64_t ntiles = (n + 63) / 64;
+  const int g = static_cast<int>(ntiles < kTransposeGrid ? (ntiles < 1 ? 1 : ntiles) : kTransposeGrid);
+  hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
+                     static_cast<size_t>(np1) * 65 * sizeof(double) + 4 * 64 * sizeof(double), s, n, p, Z, pitch,
+                     x0, Ut, true, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nvv == 0) return e;
+  const int npairs = nvv * np1;
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, g, vpart, Gv, 0);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K7m: constraint Gram on the f64 matrix cores (p + 1 <= 32; Ut in the transpose's perm order).
+//   G = U^T (M U) = sum over 4-row groups of U[rows]^T W[rows],  W = M U,
+// one v_mfma_f64_16x16x4_f64 per (16-column tile of U) x (16-column tile of W) and group: the K
+// index of the MFMA is the row within the group.  Lane (g, i) = (lane >> 4, lane & 15) owns row g
+// of the group and columns i, i + 16: exactly the MFMA's A / B operand lanes (A[i][k = g], B[k =
+// g][i]), so neither U nor W ever moves between lanes.
+//   W[r] = sum_t M[r, c_t] U[c_t] (t ascending, the row's CSR order): the 16 lanes of row g each
+// gather their 16 B of the 256-B Ut row of c_t (one wave instruction = 4 nonzeros' whole rows,
+// twice the bytes per instruction of K7's 8-B gathers), up to 16 nonzeros of a row in flight; the
+// (col, val) entries come in with one coalesced load per group and are broadcast by bpermute.
+// Pipeline per wave: group q+2's row bounds and group q+1's entries, own U row and linear-term
+// values are loaded while group q gathers.  Rows longer than 16 take further passes (direct
+// loads).  Schedule: XCD group (blockIdx % 8) owns an eighth of the rows, its waves take the
+// 4-row groups round-robin (compact L2 window); speed only, never correctness.  Fixed-order wave
+// combine and block partials as in K7 (gram_reduce_kernel sums them in block order).
+// Linear terms Gv[c][a] = sum_r U[r][a] v_c[r] from the same pass (VALU).
+// ---------------------------------------------------------------------------------------------
+typedef double v4d_t __attribute__((ext_vector_type(4)));
+
+// host: 8 row ranges of weight(row) = nnz + kGramRowW each.  A wave pays about one memory
+// round trip per 4-row group whatever its rows' lengths (the group's gathers are all in flight
+// at once), so rows, not nonzeros, set the time: measured at C3 (swe energy matrix, rows of 14,
+// 8 and 1 entries) 237 us with equal rows per XCD group vs 329 us with equal nonzeros + 2 rows
+constexpr double kGramRowW = 1e9;
+void gram_split(int64_t n, const int32_t* indptr, GramSplit* out) {
+  const double total = static_cast<double>(indptr[n]) + kGramRowW * static_cast<double>(n);
+  int64_t r = 0;
+  out->row[0] = 0;
+  for (int x = 1; x < 8; ++x) {
+    const double want = total * x / 8.0;
+    while (r < n && static_cast<double>(indptr[r]) + kGramRowW * static_cast<double>(r) < want) ++r;
+    out->row[x] = static_cast<int32_t>(r);
+  }
+  out->row[8] = static_cast<int32_t>(n);
+}
+
+__global__ __launch_bounds__(kBlock, 2) void constraint_gram_mfma_kernel(
+    int64_t n, int np1, GramSplit split, const int32_t* __restrict__ rp,
+    const int32_t* __restrict__ ci, const double* __restrict__ va, const double* __restrict__ Ut, int nvv,
+    const double* __restrict__ v0,
+    const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ v3,
+    double* __restrict__ partials) {
+  constexpr int NW = kBlock / 64;
+  constexpr int NA = 24;  // combine slots per lane: 16 G (4 tiles x 4 regs) + 2 x 4 Gv
+  __shared__ double s_acc[64 * NA];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int li = lane & 15;
+  const double2* __restrict__ U2 = reinterpret_cast<const double2*>(Ut);  // 16 double2 per row
+  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int grp = blockIdx.x % ngrp;
+  const int64_t wpg = static_cast<int64_t>(gridDim.x / ngrp) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x / ngrp) * NW + wid;
+  // XCD group grp's rows: the split balances nonzeros + rows (swe: edge rows 14 entries, rho 1)
+  const int64_t rb = ngrp == 8 ? split.row[grp] : 0;
+  const int64_t re_ = ngrp == 8 ? split.row[grp + 1] : n;
+  const int64_t ngroups = re_ > rb ? (re_ - rb + 3) / 4 : 0;
+  const bool has_m = rp != nullptr;
+  v4d_t acc00 = {0.0, 0.0, 0.0, 0.0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+  double gv0[4] = {0.0, 0.0, 0.0, 0.0}, gv1[4] = {0.0, 0.0, 0.0, 0.0};
+  const double* vv[4] = {v0, v1, v2, v3};
+
+  // stage A (group q + 2): this lane's row bounds
+  auto load_a = [&](int64_t q, int& s, int& e, int& ro) {
+    const int64_t r = rb + 4 * q + g;
+    s = e = 0;
+    ro = static_cast<int>(r);
+    if (has_m && q < ngroups && r < re_) {
+      s = rp[r];
+      e = rp[r + 1];
+    }
+  };
+  // stage B (group q + 1): the row's first 16 entries, its own U row and its v_c values
+  struct StB {
+    int s, e, col;
+    double val;
+    double2 u;
+    double vc[4];
+  };
+  auto load_b = [&](int64_t q, int s, int e, int ro, StB& B) {
+    const int64_t r = ro;
+    const bool ok = q < ngroups && rb + 4 * q + g < re_;
+    B.s = s;
+    B.e = e;
+    B.col = 0;
+    B.val = 0.0;
+    if (li < e - s) {
+      B.col = ci[s + li];
+      B.val = va[s + li];
+    }
+    B.u = ok ? U2[r * 16 + li] : make_double2(0.0, 0.0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) B.vc[c] = (ok && c < nvv) ? vv[c][r] : 0.0;
+  };
+
+  int64_t q = gw;
+  int sa = 0, ea = 0, oa = 0, sa2 = 0, ea2 = 0, oa2 = 0;
+  StB cur;
+  load_a(q, sa, ea, oa);
+  load_a(q + wpg, sa2, ea2, oa2);
+  if (q < ngroups) load_b(q, sa, ea, oa, cur);
+  for (; q < ngroups; q += wpg) {
+    StB nxt;
+    nxt.s = nxt.e = 0;
+    int sa3 = 0, ea3 = 0, oa3 = 0;
+    double w0 = 0.0, w1 = 0.0;
+    const int len = cur.e - cur.s;
+    const int l0 = __builtin_amdgcn_readlane(len, 0), l1 = __builtin_amdgcn_readlane(len, 16);
+    const int l2 = __builtin_amdgcn_readlane(len, 32), l3 = __builtin_amdgcn_readlane(len, 48);
+    const int maxlen = max(max(l0, l1), max(l2, l3));
+    int mcol = cur.col;
+    double mval = cur.val;
+    // pass b0 over entries [b0, b0 + 16) of each row; the first pass's gathers go out before the
+    // next groups' loads, so waiting for them never waits for those (vmcnt retires in order)
+    for (int b0 = 0; b0 == 0 || b0 < maxlen; b0 += 16) {
+      if (b0 > 0) {  // rows longer than 16 entries: the next 16, loaded directly
+        mcol = 0;
+        mval = 0.0;
+        if (b0 + li < len) {
+          mcol = ci[cur.s + b0 + li];
+          mval = va[cur.s + b0 + li];
+        }
+      }
+      double2 gt[16];
+      const int nt = maxlen - b0;  // wave-uniform: gathers past every row's end are not issued
+      if (has_m && maxlen > 0) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {  // col 0 (a valid row) past a row's end
+          const int c = __shfl(mcol, (g << 4) + t, 64);
+          gt[t] = t < nt ? U2[static_cast<int64_t>(c) * 16 + li] : make_double2(0.0, 0.0);
+        }
+      }
+      if (b0 == 0) {  // the next groups' loads: in flight through this group's gathers and MFMAs
+        if (q + wpg < ngroups) load_b(q + wpg, sa2, ea2, oa2, nxt);
+        load_a(q + 2 * wpg, sa3, ea3, oa3);
+      }
+      if (has_m && maxlen > 0) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          if (t < nt) {
+            const double v = __shfl(mval, (g << 4) + t, 64);
+            if (b0 + t < len) {
+              w0 += v * gt[t].x;
+              w1 += v * gt[t].y;
+            }
+          }
+        }
+      }
+    }
+    if (has_m) {
+      acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.u.x, w0, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.u.x, w1, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.u.y, w0, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.u.y, w1, acc11, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nvv) {
+        gv0[c] += cur.u.x * cur.vc[c];
+        gv1[c] += cur.u.y * cur.vc[c];
+      }
+    cur = nxt;
+    sa2 = sa3;
+    ea2 = ea3;
+    oa2 = oa3;
+  }
+  // combine the block's waves in wave order (deterministic), one partial per block
+  for (int w = 0; w < NW; ++w) {
+    if (wid == w) {
+      double v[NA];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc00[i];
+        v[4 + i] = acc01[i];
+        v[8 + i] = acc10[i];
+        v[12 + i] = acc11[i];
+        v[16 + i] = gv0[i];
+        v[20 + i] = gv1[i];
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) s_acc[lane * NA + j] = (w == 0 ? 0.0 : s_acc[lane * NA + j]) + v[j];
+    }
+    __syncthreads();
+  }
+  // G[16 ta + i][16 tb + j] = tile (ta, tb) register i >> 2 of lane ((i & 3) << 4) | j
+  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
+  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
+  for (int idx = threadIdx.x; idx < stride; idx += kBlock) {
+    if (idx < np1 * np1) {
+      const int a = idx / np1, b = idx - (idx / np1) * np1;
+      const int ta = a >> 4, ia = a & 15, tb = b >> 4, ib = b & 15;
+      const int ln = ((ia & 3) << 4) | ib;
+      out[idx] = has_m ? s_acc[ln * NA + (2 * ta + tb) * 4 + (ia >> 2)] : 0.0;
+    } else {
+      const int k2 = idx - np1 * np1;
+      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
+      const int slot = (a < 16 ? 16 : 20) + c;
+      const int ln = a & 15;
+      // the four row groups' sums in group order
+      out[idx] = ((s_acc[ln * NA + slot] + s_acc[(16 + ln) * NA + slot]) + s_acc[(32 + ln) * NA + slot]) +
+                 s_acc[(48 + ln) * NA + slot];
+    }
+  }
+}
+
+hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, const GramSplit* split,
+                                       const double* Ut, int nvv, const double* const* v, double* partials,
+                                       double* G, hipStream_t s) {
+  if (np1 > 32 || nvv > 4 || (M == nullptr && nvv == 0)) return hipErrorInvalidValue;
+  const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int c = 0; c < nvv; ++c) vv[c] = v[c];
+  static const int grid = [] {  // resident workgroups, a multiple of 8, <= the partial slots
+    int dev = 0, cus = 256, per = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, constraint_gram_mfma_kernel, kBlock, 0) != hipSuccess ||
+        per < 1)
+      per = 1;
+    int t = (cus * per) & ~7;
+    return t < 8 ? 8 : (t > kConGramGrid ? kConGramGrid : t);
+  }();
+  GramSplit sp;
+  if (M != nullptr && split != nullptr) {
+    sp = *split;
+  } else {  // rows only (no matrix): equal row ranges
+    for (int x = 0; x <= 8; ++x) sp.row[x] = static_cast<int32_t>(n * x / 8);
+  }
+  hipLaunchKernelGGL(constraint_gram_mfma_kernel, dim3(grid), dim3(kBlock), 0, s, n, np1, sp,
+                     M ? M->indptr : nullptr, M ? M->indices : nullptr, M ? M->vals : nullptr, Ut, nvv, vv[0],
+                     vv[1], vv[2], vv[3], partials);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int npairs = np1 * np1 + nvv * np1;
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, grid, partials, G, 0);
   return hipGetLastError();
 }
 
@@ -2865,6 +3171,167 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
   const int npairs = np1 * np1 + nvv * np1;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3((npairs + 63) / 64), dim3(kBlock), 0, s, npairs, grid,
                      partials, G);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K7t: constraint Gram of a SYMMETRIC constraint matrix on the f64 matrix cores, from a slot
+// table (p + 1 <= 32; Ut in the perm order; linear terms come from the transpose).
+//   G = H + H^T,   H = sum_r U_r What_r^T,   What_r = (1/2) M_rr U_r + sum_{c > r} M_rc U_c
+// (M = M^T: each off-diagonal pair is gathered once, the diagonal is the row's own U row), so a
+// row gathers about half of its nonzeros.  Rows go in 4-row groups (the MFMA's K = 4, lane
+// layout as K7m); a group's slots are its rows' own U rows (slot 0, value M_rr / 2) then their
+// upper entries, padded to the longest row; groups longer than NS slots are cut into segments,
+// each with its own own-row slot (H is linear in What).  Consecutive segments are packed into
+// blocks of <= NS slots (a host-built table: per block NS x 4 (col, val) entries and a mask of
+// segment starts), so short rows (swe: interior dofs ~2 slots, rho 1) share one round trip.
+// Per block: one coalesced table load (prefetched a block ahead), <= NS 16-B gathers in flight
+// per lane, then per segment What accumulated in slot order and 4 MFMAs.  Blocks: XCD group
+// (blockIdx % 8) owns a contiguous eighth, its waves take them round-robin.
+// ---------------------------------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabView T,
+                                                                        const double* __restrict__ Ut,
+                                                                        double* __restrict__ partials, int np1) {
+  constexpr int NW = kBlock / 64;
+  constexpr int NJ = NS / 16;  // table entries per lane and block
+  constexpr int NA = 16;
+  __shared__ double s_acc[64 * NA];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int li = lane & 15;
+  const double2* __restrict__ U2 = reinterpret_cast<const double2*>(Ut);
+  // waves take the blocks round-robin over the whole table: blocks differ widely in cost (an
+  // edge-row block of swe holds one segment, a rho-row block sixteen, with 4 MFMAs each), and
+  // giving each XCD a contiguous eighth (K7m's schedule) measured 251 vs 141 us at C3
+  const int64_t wpg = static_cast<int64_t>(gridDim.x) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * NW + wid;
+  const int64_t kb0 = 0;
+  const int64_t kb1 = T.nblk;
+  v4d_t acc00 = {0.0, 0.0, 0.0, 0.0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+  struct Ent {  // zero-initialised: a block past the range is never loaded, never undefined
+    unsigned long long mask = 0;
+    int col[NJ] = {};
+    double val[NJ] = {};
+  };
+  auto load = [&](int64_t kb, Ent& E) {
+    E.mask = T.mask[kb];
+    const int64_t base = kb * (4 * NS) + g * NS + li;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      E.col[j] = T.col[base + 16 * j];
+      E.val[j] = T.val[base + 16 * j];
+    }
+  };
+  auto flush = [&](const double2& a, double w0, double w1) {
+    acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, w0, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, w1, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, w0, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, w1, acc11, 0, 0, 0);
+  };
+  int64_t kb = kb0 + gw;
+  Ent cur, nxt;  // the table two blocks ahead is in flight: its wait never stalls a block
+  if (kb < kb1) load(kb, cur);
+  if (kb + wpg < kb1) load(kb + wpg, nxt);
+  for (; kb < kb1; kb += wpg) {
+    const unsigned long long mk = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(cur.mask)) |
+                                  (static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
+                                       static_cast<unsigned>(cur.mask >> 32))) << 32);
+    const int ns = static_cast<int>(mk >> 32);
+    const unsigned starts = static_cast<unsigned>(mk);
+    // gathers in straight-line quads (a wave-uniform test per 4 slots): the bpermutes of a quad
+    // go out together, then its loads; slots past ns hold (row 0, value 0) in the table
+    double2 gt[NS];
+#pragma unroll
+    for (int t4 = 0; t4 < NS; t4 += 4) {
+      if (t4 < ns) {
+        int c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          c[u] = __shfl(cur.col[(t4 + u) >> 4], (g << 4) + ((t4 + u) & 15), 64);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gt[t4 + u] = U2[static_cast<int64_t>(c[u]) * 16 + li];
+      }
+    }
+    Ent nx2;
+    if (kb + 2 * wpg < kb1) load(kb + 2 * wpg, nx2);  // in flight through this block and the next
+    double2 a = make_double2(0.0, 0.0);
+    double w0 = 0.0, w1 = 0.0;
+#pragma unroll
+    for (int t4 = 0; t4 < NS; t4 += 4) {
+      if (t4 < ns) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __shfl(cur.val[(t4 + u) >> 4], (g << 4) + ((t4 + u) & 15), 64);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = t4 + u;
+          if ((starts >> t) & 1u) {
+            if (t > 0) flush(a, w0, w1);
+            a = gt[t];
+            w0 = 0.0;
+            w1 = 0.0;
+          }
+          w0 += v[u] * gt[t].x;
+          w1 += v[u] * gt[t].y;
+        }
+      }
+    }
+    if (ns > 0) flush(a, w0, w1);
+    cur = nxt;
+    nxt = nx2;
+  }
+  for (int w = 0; w < NW; ++w) {
+    if (wid == w) {
+      double v[NA];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc00[i];
+        v[4 + i] = acc01[i];
+        v[8 + i] = acc10[i];
+        v[12 + i] = acc11[i];
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) s_acc[lane * NA + j] = (w == 0 ? 0.0 : s_acc[lane * NA + j]) + v[j];
+    }
+    __syncthreads();
+  }
+  const int np2 = np1 * np1;
+  double* out = partials + static_cast<int64_t>(blockIdx.x) * np2;
+  for (int idx = threadIdx.x; idx < np2; idx += kBlock) {
+    const int a = idx / np1, b = idx - (idx / np1) * np1;
+    const int ta = a >> 4, ia = a & 15, tb = b >> 4, ib = b & 15;
+    const int ln = ((ia & 3) << 4) | ib;
+    out[idx] = s_acc[ln * NA + (2 * ta + tb) * 4 + (ia >> 2)];
+  }
+}
+
+template <int NS>
+static int sym_grid() {
+  static const int grid = [] {
+    int dev = 0, cus = 256, per = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, constraint_gram_sym_kernel<NS>, kBlock, 0) != hipSuccess ||
+        per < 1)
+      per = 1;
+    int t = (cus * per) & ~7;
+    return t < 8 ? 8 : (t > kConGramGrid ? kConGramGrid : t);
+  }();
+  return grid;
+}
+
+hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
+                                      hipStream_t s) {
+  if (np1 > 32) return hipErrorInvalidValue;
+  int grid = 0;
+  if (T.ns != 16) return hipErrorInvalidValue;
+  grid = sym_grid<16>();
+  hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int np2 = np1 * np1;
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(np2), dim3(kBlock), 0, s, np2, grid, partials, G, np1);
   return hipGetLastError();
 }
 

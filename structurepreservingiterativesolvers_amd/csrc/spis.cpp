@@ -110,6 +110,7 @@ struct spis_context {
   double* cg_part = nullptr;           // fused constraint-Gram partials (per wave)
   size_t cg_part_len = 0;
   double* cg_G = nullptr;              // its reduced output (64*64 + 4*64)
+  double* cg_vpart = nullptr;          // K7t: the transpose's linear-term partials
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   std::vector<spis_workspace*> pool;
@@ -123,7 +124,7 @@ struct spis_context {
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
-  int ell_gram = 1;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy (SPIS_OPT_ELL_GRAM)
+  int ell_gram = 3;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy, 3 K7t / K7m, 4 K7m (SPIS_OPT_ELL_GRAM)
   int mgs_chain = 3;                // persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 K2p gathered by workgroup 0, 2 by a dedicated workgroup, 3 K2q pipelined
   int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
   // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
@@ -187,6 +188,13 @@ struct spis_matrix {
   double* stg_val = nullptr;
   int32_t stg_nch = 0;
   bool all_zero = false;
+  GramSplit gram_rows{};  // K7m's XCD-group row ranges (natural row order)
+  // K7t's slot table (symmetric matrices; sym_state -1 unknown, 0 not symmetric, 1 built)
+  int sym_state = -1;
+  int32_t* sym_col = nullptr;
+  double* sym_val = nullptr;
+  unsigned long long* sym_mask = nullptr;
+  int32_t sym_nblk = 0, sym_ns = 0;
   // halo plan
   int32_t n_ghost = 0;
   std::vector<int32_t> nbr, scnt, rcnt, soff, roff;
@@ -547,6 +555,9 @@ extern "C" int spis_context_destroy(spis_context* c) {
     if (c->chain_err) (void)hipHostFree(c->chain_err);
     if (c->gram_part) (void)hipFree(c->gram_part);
     if (c->gram_G) (void)hipFree(c->gram_G);
+    if (c->cg_part) (void)hipFree(c->cg_part);
+    if (c->cg_G) (void)hipFree(c->cg_G);
+    if (c->cg_vpart) (void)hipFree(c->cg_vpart);
     if (c->gram_ptrs) (void)hipFree(c->gram_ptrs);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->gram_pinned) (void)hipHostFree(c->gram_pinned);
@@ -593,7 +604,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
       case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
       case SPIS_OPT_ELL_GRAM:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "ell gram %lld: 0, 1 or 2", (long long)value);
+        if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "ell gram %lld: 0 .. 4", (long long)value);
         c->ell_gram = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN:
@@ -765,6 +776,7 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
     M->n_cols = n_cols;
     M->nnz = nnz;
     M->all_zero = all_zero;
+    gram_split(n_rows, indptr, &M->gram_rows);
     std::vector<int32_t> blk;
     build_row_blocks(n_rows, indptr, blk, M->n_long);
     M->n_blk = static_cast<int32_t>(blk.size()) - 1;
@@ -839,7 +851,7 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     if (M->ell_off) (void)hipFree(M->ell_off);
     for (void* p : {static_cast<void*>(M->stg_row), static_cast<void*>(M->stg_uoff), static_cast<void*>(M->stg_uniq),
                     static_cast<void*>(M->stg_eoff), static_cast<void*>(M->stg_width), static_cast<void*>(M->stg_loc),
-                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc)})
+                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc), static_cast<void*>(M->sym_col), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
       if (p) (void)hipFree(p);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
@@ -1212,6 +1224,147 @@ static int ensure_ell(spis_context* c, spis_matrix* M, EllView* out) {
   return SPIS_OK;
 }
 
+// K7t's slot table (kernels.h SymTabView) of a square matrix that equals its transpose exactly;
+// *ok = false otherwise.  Built once per matrix (ns = slots per block).
+static int ensure_symtab(spis_context* c, spis_matrix* M, int ns, SymTabView* out, bool* ok) {
+  if (M->sym_state == 1 && M->sym_ns != ns) {  // another slot count: rebuild
+    for (void* p : {static_cast<void*>(M->sym_col), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
+      if (p) HIP_TRY(hipFree(p));
+    M->sym_col = nullptr;
+    M->sym_val = nullptr;
+    M->sym_mask = nullptr;
+    M->sym_state = -1;
+  }
+  if (M->sym_state < 0) {
+    M->sym_state = 0;
+    const int64_t n = M->n_rows, nnz = M->nnz;
+    if (M->n_cols != n) {
+      *ok = false;
+      return SPIS_OK;
+    }
+    std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
+    std::vector<double> va(std::max<int64_t>(nnz, 1));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+    if (nnz > 0) {
+      HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+    }
+    // exact symmetry: every row's (col, value) multiset equals the transpose's
+    std::vector<int64_t> tp(n + 1, 0);
+    for (int64_t e = 0; e < nnz; ++e) ++tp[ci[e] + 1];
+    for (int64_t r = 0; r < n; ++r) tp[r + 1] += tp[r];
+    std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
+    std::vector<std::pair<int32_t, double>> te(std::max<int64_t>(nnz, 1));
+    for (int64_t r = 0; r < n; ++r)
+      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) te[fill[ci[e]]++] = {static_cast<int32_t>(r), va[e]};
+    bool sym = true;
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t r = 0; r < n && sym; ++r) {
+      if (tp[r + 1] - tp[r] != rp[r + 1] - rp[r]) {
+        sym = false;
+        break;
+      }
+      row.clear();
+      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) row.push_back({ci[e], va[e]});
+      auto lt = [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
+        return x.first != y.first ? x.first < y.first : x.second < y.second;
+      };
+      std::sort(row.begin(), row.end(), lt);
+      std::vector<std::pair<int32_t, double>> trow(te.begin() + tp[r], te.begin() + tp[r + 1]);
+      std::sort(trow.begin(), trow.end(), lt);
+      for (size_t i = 0; i < row.size() && sym; ++i)
+        sym = row[i].first == trow[i].first && row[i].second == trow[i].second;
+    }
+    if (sym) {
+      // segments of 4-row groups: slot 0 = each row's own U row (value M_rr / 2, duplicates summed),
+      // then its entries with c > r in CSR order, padded (col = the row itself, value 0)
+      std::vector<int32_t> tcol;
+      std::vector<double> tval;
+      std::vector<unsigned long long> tmask;
+      int used = 0;            // slots used in the open block
+      unsigned long long start_bits = 0;
+      auto open_block = [&]() {
+        tcol.resize(tcol.size() + 4 * static_cast<size_t>(ns), 0);
+        tval.resize(tval.size() + 4 * static_cast<size_t>(ns), 0.0);
+        tmask.push_back(0);
+        used = 0;
+        start_bits = 0;
+      };
+      auto close_block = [&]() {
+        if (!tmask.empty()) tmask.back() = start_bits | (static_cast<unsigned long long>(used) << 32);
+      };
+      std::vector<int32_t> up[4];
+      std::vector<double> upv[4];
+      double diag[4];
+      const int64_t ngroups = (n + 3) / 4;
+      for (int64_t q = 0; q < ngroups; ++q) {
+        int longest = 0;
+        for (int g = 0; g < 4; ++g) {
+          up[g].clear();
+          upv[g].clear();
+          diag[g] = 0.0;
+          const int64_t r = 4 * q + g;
+          if (r >= n) continue;
+          for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+            if (ci[e] == r) diag[g] += va[e];
+            else if (ci[e] > r) {
+              up[g].push_back(ci[e]);
+              upv[g].push_back(va[e]);
+            }
+          }
+          longest = std::max<int>(longest, static_cast<int>(up[g].size()));
+        }
+        // segments: own slot + up to ns - 1 entries each
+        int done = 0;
+        bool first = true;
+        while (first || done < longest) {
+          const int take = std::min(ns - 1, longest - done);
+          const int need = 1 + take;
+          if (tmask.empty() || used + need > ns) {
+            close_block();
+            open_block();
+          }
+          const size_t base = (tmask.size() - 1) * 4 * static_cast<size_t>(ns);
+          start_bits |= 1ull << used;
+          for (int g = 0; g < 4; ++g) {
+            const int64_t r = 4 * q + g;
+            const int32_t own = r < n ? static_cast<int32_t>(r) : 0;
+            tcol[base + g * ns + used] = own;
+            tval[base + g * ns + used] = (first && r < n) ? 0.5 * diag[g] : 0.0;
+            for (int t = 0; t < take; ++t) {
+              const int k = done + t;
+              const bool has = k < static_cast<int>(up[g].size());
+              tcol[base + g * ns + used + 1 + t] = has ? up[g][k] : own;
+              tval[base + g * ns + used + 1 + t] = has ? upv[g][k] : 0.0;
+            }
+          }
+          used += need;
+          done += take;
+          first = false;
+        }
+      }
+      close_block();
+      if (tmask.empty()) open_block(), close_block();
+      auto up_ = [&](auto** dst, const auto& v) -> int {
+        using T = typename std::remove_reference<decltype(v)>::type::value_type;
+        HIP_TRY(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
+        if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+        return SPIS_OK;
+      };
+      ST_TRY(up_(&M->sym_col, tcol));
+      ST_TRY(up_(&M->sym_val, tval));
+      ST_TRY(up_(&M->sym_mask, tmask));
+      M->sym_nblk = static_cast<int32_t>(tmask.size());
+      M->sym_ns = ns;
+      M->sym_state = 1;
+    }
+  }
+  *ok = M->sym_state == 1;
+  if (*ok) *out = SymTabView{M->sym_col, M->sym_val, M->sym_mask, M->sym_nblk, M->sym_ns};
+  return SPIS_OK;
+}
+
 // One-time chunking of a constraint matrix for K7s: greedy row chunks of <= kStgRows rows,
 // <= kStgNz ELL entries (16-row slices, each padded to its longest row) and <= kStgUmax distinct
 // columns (the chunk's own rows counted as columns: the rank-1 update reads U_r from the same LDS
@@ -1374,31 +1527,54 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     if (cons[ci].v_dev) vlist.push_back(cons[ci].v_dev);
   struct Launch {
     int ci;
-    bool stg, ell;
+    bool stg, ell, sym;
     EllView ev;
     StgView sv;
+    SymTabView tv;
   };
+  // ell_gram 3: K7t for symmetric matrices, K7m otherwise, the linear terms from the transpose;
+  // 4: K7m for every matrix.  Both read Ut in the MFMA column order.
+  const int eg = c->ell_gram;
+  const bool mfma = np1 <= 32 && eg >= 3;
+  const bool tsym = mfma && eg == 3;
   std::vector<Launch> plan;
   for (int ci = 0; ci < m; ++ci) {
     if (cons[ci].M == nullptr || cons[ci].M->all_zero) continue;
-    Launch L{ci, false, false, {}, {}};
-    if (np1 <= 32 && c->ell_gram == 2) ST_TRY(ensure_stg(c, cons[ci].M, &L.sv, &L.stg));
-    L.ell = !L.stg && np1 <= 32 && c->ell_gram >= 1;
+    Launch L{ci, false, false, false, {}, {}, {}};
+    if (np1 <= 32 && eg == 2) ST_TRY(ensure_stg(c, cons[ci].M, &L.sv, &L.stg));
+    L.ell = !L.stg && np1 <= 32 && (eg == 1 || eg == 2);
     if (L.ell) ST_TRY(ensure_ell(c, cons[ci].M, &L.ev));
+    if (tsym) ST_TRY(ensure_symtab(c, cons[ci].M, 16, &L.tv, &L.sym));
     plan.push_back(L);
   }
   const size_t voff = static_cast<size_t>(m) * np1 * np1;
   const int nv = static_cast<int>(vlist.size());
-  HIP_TRY(launch_transpose_basis(n, p, Z, pitch, x0, ws->Ut, st));
   bool v_done = nv == 0;
+  if (tsym) {  // Ut + the linear terms in one pass over the basis
+    if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
+    HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart,
+                                       c->cg_G + 64 * 64, st));
+    if (nv > 0)
+      HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + 64 * 64, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
+    v_done = true;
+  } else {
+    HIP_TRY(launch_transpose_basis(n, p, Z, pitch, x0, ws->Ut, st, mfma));
+  }
   for (const Launch& L : plan) {
     const CsrView mv = cons[L.ci].M->view();
     const int nvv = v_done ? 0 : nv;
-    if (L.stg)
+    spis_matrix* Mc = cons[L.ci].M;
+    if (L.sym) {
+      HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, c->cg_G, st));
+    } else if (mfma) {
+      HIP_TRY(launch_constraint_gram_mfma(n, np1, &mv, &Mc->gram_rows, ws->Ut, nvv, vlist.data(),
+                                          c->cg_part, c->cg_G, st));
+    } else if (L.stg) {
       HIP_TRY(launch_constraint_gram_stg(n, np1, L.sv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st));
-    else
+    } else {
       HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st,
                                      L.ell ? &L.ev : nullptr));
+    }
     HIP_TRY(hipMemcpyAsync(dst + static_cast<size_t>(L.ci) * np1 * np1, c->cg_G, sizeof(double) * np1 * np1,
                            hipMemcpyDeviceToHost, st));
     if (nvv > 0)
@@ -1406,7 +1582,11 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     v_done = true;
   }
   if (!v_done) {  // linear terms only
-    HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nv, vlist.data(), c->cg_part, c->cg_G, st));
+    if (mfma)
+      HIP_TRY(launch_constraint_gram_mfma(n, np1, nullptr, nullptr, ws->Ut, nv, vlist.data(), c->cg_part,
+                                          c->cg_G, st));
+    else
+      HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nv, vlist.data(), c->cg_part, c->cg_G, st));
     HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + np1 * np1, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
   }
   return SPIS_OK;

@@ -52,7 +52,7 @@ _OPTIONS = {
     "generic_gram": (_lib.OPT_GENERIC_GRAM, None),
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
-    "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2}),
+    "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 3, "gather0": 1, "aggregator": 2, "pipelined": 3}),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
@@ -69,10 +69,11 @@ def set_option(name, value, ctx=None):
     * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
       low-synchronisation option (3 reductions per step; not MGS's rounding);
     * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
-    * ``ell_gram`` ("ell"): the fused constraint reduction reads each constraint matrix as "ell"
-      (sliced ELL; True), "staged" (row chunks whose distinct columns' basis rows are staged in
-      LDS; falls back to "ell" for a matrix with a row that does not fit a chunk) or "csr"
-      (False);
+    * ``ell_gram`` ("mfma"): the fused constraint reduction's kernel: "mfma" (f64 matrix cores;
+      a symmetric constraint matrix through a slot table of its upper triangle, K7t, any other
+      from its CSR, K7m), "mfma_full" (K7m for every matrix), "ell" (sliced ELL; True), "staged"
+      (row chunks whose distinct columns' basis rows are staged in LDS; falls back to "ell" for
+      a matrix with a row that does not fit a chunk) or "csr" (False);
     * ``mgs_chain`` (True = "pipelined"): each Arnoldi step's MGS chain + normalise as one persistent
       launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
       ("gather0"); "pipelined": each dot product one MGS step early by the distributive law

@@ -98,7 +98,12 @@ def test_spmv_bit_exact_vs_scipy(spis, pipe):
 
 def test_spmv_pipe_modes_solver_agree(spis):
     """The solver with each SpMV kernel family: identical steps and branches, iterates equal at
-    roundoff (the modes group the residual / first-dot partial sums per workgroup differently)."""
+    roundoff (the modes group the residual / first-dot partial sums per workgroup differently).
+    Unconstrained residuals agree to 1e-12 r0.  The constrained final step's to the golden
+    contract's 1e-10 r0 only: the host KKT targets -8 ulp of each constraint's magnitude (so the
+    reference's signed checker cannot flip), and whether the unconstrained minimiser already sits
+    there depends on the sign of its constraint value at roundoff (swe M=30: the final residual
+    is 1.0e-12 or 4.4e-11 = 8.5e-12 r0 by mode; the reference's own is 1.6e-12)."""
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.device import set_option
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
@@ -120,7 +125,8 @@ def test_spmv_pipe_modes_solver_agree(spis):
         x, r, st, tr = runs[pipe]
         assert st == s0 and tr == t0, pipe
         assert np.linalg.norm(x - x0) <= 1e-9 * np.linalg.norm(x0), pipe
-        np.testing.assert_allclose(r, r0, rtol=1e-6, atol=1e-12 * r0[0])
+        np.testing.assert_allclose(r[:-1], r0[:-1], rtol=1e-6, atol=1e-12 * r0[0])
+        np.testing.assert_allclose(r[-1], r0[-1], rtol=0, atol=1e-10 * r0[0])
 
 
 def test_residual_norm_and_blas1(spis):
@@ -270,23 +276,24 @@ def test_fused_and_generic_constraint_reduction_agree(spis):
         _lib.check(ctx.L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
     outs = {}
     try:
-        for mode in ("csr", "staged"):  # K7 on the CSR (row-boundary walk) / the chunk-staged copy
+        for mode in ("csr", "staged", "ell", "mfma_full"):  # K7 CSR / staged / ELL, K7m (K7t is the default)
             set_option("ell_gram", mode)
             outs[mode] = swe_ls.cgmresWrapper(dic, x0=x0, k=25, tol=1e-19)
     finally:
-        set_option("ell_gram", "ell")
+        set_option("ell_gram", "mfma")
     for xc, dc in outs.values():
         assert df["x"].trace == dg["x"].trace == dc["x"].trace
         np.testing.assert_allclose(xc, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
     np.testing.assert_allclose(xf, xg, rtol=0, atol=1e-10 * np.linalg.norm(xg))
 
 
-@pytest.mark.parametrize("mode", ["staged", "ell", "csr"])
+@pytest.mark.parametrize("mode", ["staged", "ell", "csr", "mfma", "mfma_full"])
 def test_constraint_terms_kernels_vs_reference(spis, mode):
     """Every K7 matrix form against constraint_container's host algebra (solvers.py:33-36):
     a field-major banded matrix with ragged and empty rows (staged: many chunks, chunk limits hit
-    by rows, distinct columns and nonzeros), and one with a 1500-entry row (staged falls back to
-    ELL), for p + 1 = 2, 10, 32."""
+    by rows, distinct columns and nonzeros), one with a 1500-entry row (staged falls back to
+    ELL; K7t cuts it into segments) and a non-symmetric one (K7t falls back to K7m), for
+    p + 1 = 2, 10, 32."""
     from oracle.cgmres_port import ConstraintTerms
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.device import set_option
@@ -294,7 +301,7 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
     rng = np.random.default_rng(7)
     n = 6000
 
-    def banded(long_row):
+    def banded(long_row, symmetric=True):
         lens = rng.integers(0, 16, size=n)
         lens[[3, 4, 5000]] = 0
         rows = []
@@ -306,16 +313,17 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
             rows[1234] = np.unique(rng.integers(0, n, size=1500))
         indptr = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
         A = sps.csr_matrix((rng.normal(size=indptr[-1]), np.concatenate(rows).astype(np.int32), indptr), shape=(n, n))
-        return (A + A.T).tocsr()
+        return (A + A.T).tocsr() if symmetric else A
 
     class Con:
         pass
 
     set_option("ell_gram", mode)
     try:
-        for long_row in (False, True):
+        # symmetric matrices take K7t in the "mfma" modes, the non-symmetric one K7m
+        for long_row, symmetric in ((False, True), (True, True), (False, False)):
             con = Con()
-            con.M, con.v, con.c = banded(long_row), rng.normal(size=n), 0.3
+            con.M, con.v, con.c = banded(long_row, symmetric), rng.normal(size=n), 0.3
             for p in (1, 9, 31):
                 Z = rng.normal(size=(n, p))
                 x0 = rng.normal(size=n)
@@ -326,7 +334,7 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
                 np.testing.assert_allclose(got.term1, ref.term1, rtol=1e-12, atol=1e-12 * scale)
                 np.testing.assert_allclose(got.term2, ref.term2, rtol=1e-12, atol=1e-12 * scale)
     finally:
-        set_option("ell_gram", "ell")
+        set_option("ell_gram", "mfma")
 
 
 def test_nontemporal_chain_loads_bit_identical(spis):
