@@ -300,8 +300,11 @@ bool first_order_ok(KKTState& st, const QuadCon* cons, const double* y, std::vec
 
 // Second-order test: the Hessian of the Lagrangian, B + sum lam_i S_i, positive definite on the
 // null space of J (a constrained minimum, not a saddle of the indefinite energy constraint).
-// Null space from a Householder QR of J'; Cholesky of the reduced matrix with a shift of
-// 1e-10 of its largest diagonal entry, so a semidefinite direction at roundoff passes.
+// The Householder reflections of a QR of J' are applied to W from both sides (Q' W Q, 4 p^2
+// flops each: the explicit null-space basis and the products N'(W N) cost 2 p^3, 60 of the
+// ~100 us of a p = 30 KKT solve), whose trailing (p - m) block is the reduced Hessian; Cholesky
+// with a shift of 1e-10 of its largest diagonal entry, so a semidefinite direction at roundoff
+// passes.
 bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, const std::vector<double>& lam) {
   const int p = st.p, m = st.m;
   if (m >= p) return true;
@@ -312,7 +315,6 @@ bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, c
       for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
       W[static_cast<size_t>(a) * p + b] = w;
     }
-  // Q (p x p, column-major basis vectors as rows of Qt) from Householder reflections of J'
   std::vector<double> Jt(static_cast<size_t>(p) * m);  // column i = grad c_i
   for (int i = 0; i < m; ++i)
     for (int a = 0; a < p; ++a) {
@@ -320,9 +322,7 @@ bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, c
       for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y[b];
       Jt[static_cast<size_t>(i) * p + a] = t;
     }
-  std::vector<double> Qt(static_cast<size_t>(p) * p, 0.0);  // rows = orthonormal basis
-  for (int a = 0; a < p; ++a) Qt[static_cast<size_t>(a) * p + a] = 1.0;
-  std::vector<double> v(p);
+  std::vector<double> v(p), u(p);
   for (int i = 0; i < m; ++i) {
     double* col = Jt.data() + static_cast<size_t>(i) * p;
     double nrm = 0.0;
@@ -336,34 +336,41 @@ bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, c
     double vv = 0.0;
     for (int a = i; a < p; ++a) vv += v[a] * v[a];
     if (vv == 0.0) continue;
-    auto reflect = [&](double* x) {  // x -= 2 v (v.x) / (v.v)
+    const double s2 = 2.0 / vv;
+    for (int k = i; k < m; ++k) {  // the remaining columns of J'
+      double* x = Jt.data() + static_cast<size_t>(k) * p;
       double t = 0.0;
       for (int a = i; a < p; ++a) t += v[a] * x[a];
-      t = 2.0 * t / vv;
+      t *= s2;
       for (int a = i; a < p; ++a) x[a] -= t * v[a];
-    };
-    for (int k = i; k < m; ++k) reflect(Jt.data() + static_cast<size_t>(k) * p);
-    // accumulate H_i ... applied to e_r: Q = H_0 H_1 ... ; rows of Qt are Q' rows => reflect rows
-    for (int r = 0; r < p; ++r) reflect(Qt.data() + static_cast<size_t>(r) * p);
-  }
-  // Qt row r holds (Q' e_r)' ... with reflections applied to rows, Qt = I H_0 H_1 ... = Q, so
-  // the null space of J is spanned by columns m..p-1 of Q
-  const int nz = p - m;
-  std::vector<double> N(static_cast<size_t>(p) * nz);
-  for (int a = 0; a < p; ++a)
-    for (int c = 0; c < nz; ++c) N[static_cast<size_t>(a) * nz + c] = Qt[static_cast<size_t>(a) * p + m + c];
-  std::vector<double> WN(static_cast<size_t>(p) * nz, 0.0), Rm(static_cast<size_t>(nz) * nz, 0.0);
-  for (int a = 0; a < p; ++a)
-    for (int c = 0; c < nz; ++c) {
-      double t = 0.0;
-      for (int b = 0; b < p; ++b) t += W[static_cast<size_t>(a) * p + b] * N[static_cast<size_t>(b) * nz + c];
-      WN[static_cast<size_t>(a) * nz + c] = t;
     }
+    // W <- H W H with H = I - s2 v v' (W symmetric up to rounding: both sides explicitly)
+    for (int a = 0; a < p; ++a) {  // W <- W H: row a -= s2 (W_a . v) v'
+      double* row = W.data() + static_cast<size_t>(a) * p;
+      double t = 0.0;
+      for (int b = i; b < p; ++b) t += row[b] * v[b];
+      t *= s2;
+      for (int b = i; b < p; ++b) row[b] -= t * v[b];
+    }
+    std::fill(u.begin(), u.end(), 0.0);  // W <- H W: W -= s2 v (v' W)
+    for (int a = i; a < p; ++a) {
+      const double va = v[a];
+      const double* row = W.data() + static_cast<size_t>(a) * p;
+      for (int b = 0; b < p; ++b) u[b] += va * row[b];
+    }
+    for (int a = i; a < p; ++a) {
+      double* row = W.data() + static_cast<size_t>(a) * p;
+      const double f = s2 * v[a];
+      for (int b = 0; b < p; ++b) row[b] -= f * u[b];
+    }
+  }
+  // reduced Hessian: the trailing (p - m) x (p - m) block of Q' W Q
+  const int nz = p - m;
+  std::vector<double> Rm(static_cast<size_t>(nz) * nz);
   double dmax = 0.0;
   for (int c = 0; c < nz; ++c)
     for (int d = 0; d < nz; ++d) {
-      double t = 0.0;
-      for (int a = 0; a < p; ++a) t += N[static_cast<size_t>(a) * nz + c] * WN[static_cast<size_t>(a) * nz + d];
+      const double t = W[static_cast<size_t>(m + c) * p + m + d];
       Rm[static_cast<size_t>(c) * nz + d] = t;
       if (c == d) dmax = std::max(dmax, std::fabs(t));
     }

@@ -1627,13 +1627,17 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
   return SPIS_OK;
 }
 
+// the fused reduction (con_gram_enqueue) serves this step
+static bool fused_con_ok(const spis_context* c, int p, int m, const spis_constraint_desc* cons) {
+  int nlin = 0;
+  for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
+  return !c->comm && p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram;
+}
+
 static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
                                 int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                 QuadCon* out) {
-  int nlin = 0;
-  for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
-  if (!c->comm && p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram)
-    return constraint_terms_fused(c, ws, m, cons, n, p, Z, pitch, x0, out);
+  if (fused_con_ok(c, p, m, cons)) return constraint_terms_fused(c, ws, m, cons, n, p, Z, pitch, x0, out);
   std::vector<const double*> U, V;
   for (int i = 0; i < p; ++i) U.push_back(Z + static_cast<int64_t>(i) * pitch);
   U.push_back(x0);
@@ -2053,7 +2057,7 @@ struct Solver {
     c->prof_iter = j;
     ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
     const LaunchEv le = pd.both();
-    HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
+    HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), b, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
                              c->stream, &le));
     return SPIS_OK;
   }
@@ -2147,8 +2151,8 @@ struct Solver {
     {
       ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
       const LaunchEv le = pd.both();
-      HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), ws->bcopy, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
-                               c->stream, &le));
+      HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), graphable() ? ws->bcopy : b, c->partR, Zv(ja), ws->w, Qv(0),
+                               c->partA, gs, c->stream, &le));
     }
     if (c->comm) {
       ST_TRY(update_comm_finish(j));
@@ -2307,12 +2311,21 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
 
     // r0 = b - A x0 ; beta = ||r0|| ; q0 = r0 / beta      (solvers.py:167-177)
-    if (!ws->bcopy) HIP_TRY(hipMalloc(&ws->bcopy, sizeof(double) * ws->pitch));
-    HIP_TRY(launch_copy(n, b, ws->bcopy, s));
+    // copies: x0 into the workspace (zero padding for K2q's pairs, one buffer for every x0 use);
+    // b only for graph replays (graph nodes never capture caller pointers); x0 into a halo'd
+    // buffer only when the SpMV reads ghost entries
+    if (S.graphable()) {
+      if (!ws->bcopy) HIP_TRY(hipMalloc(&ws->bcopy, sizeof(double) * ws->pitch));
+      HIP_TRY(launch_copy(n, b, ws->bcopy, s));
+    }
     HIP_TRY(launch_copy(n, x0, ws->x0, s));
-    HIP_TRY(launch_copy(n, x0, ws->xj, s));
-    ST_TRY(exchange(c, A, ws->xj));
-    HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, ws->xj, ws->r0, b, c->partA, S.gs, s));
+    const double* xr0 = ws->x0;
+    if (A->n_ghost > 0 || c->comm) {
+      HIP_TRY(launch_copy(n, x0, ws->xj, s));
+      ST_TRY(exchange(c, A, ws->xj));
+      xr0 = ws->xj;
+    }
+    HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s));
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
@@ -2381,6 +2394,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // recomputes x_j after c_{j+1}), and enqueues [U_j res | a_{j+2}] (res + finalize at the end).
     std::vector<double> yspec(k);
     int last_x = -1;  // iteration whose x_j is x[-1]
+    int gram_queued = -1;  // iteration whose constraint reduction is already on the stream
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
       bool fused = false, col_added = false;
       if (L) {
@@ -2408,6 +2422,17 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         } else if (brk && j >= 1 && j + 1 < k) {  // no c_{j+1}: U_{j-1}'s residual on its own
           ST_TRY(S.enqueue_finalize(j - 1));
         }
+      }
+      // L mode, a step that is constrained whatever res_{j-1} says (the forced last step, or
+      // safety set, :230): its reduction goes on the stream now, behind c_{j+1} / U_{j-1}'s
+      // residual, not after the host has waited for that residual (C3: a 20 us gap before it)
+      if (L && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && (j == k - 1 || safety != kSafetyNone) &&
+          fused_con_ok(c, j + 1, o->n_constraints, o->constraints) && !pre_launched) {
+        ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(o->n_constraints, j + 1)));
+        ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, j + 1, ws->Zb, ws->pitch, ws->x0, s,
+                                c->con_pinned));
+        HIP_TRY(hipEventRecord(c->ev_gram, s));
+        gram_queued = j;
       }
       ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : S.wait_update(j - 1));
       prof_drain(c);
@@ -2474,6 +2499,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (m_active > 0 && pre_launched && p == k && m_active == o->n_constraints) {
           ST_TRY(wait_event(c->ev_pre_done));  // reduced early, beside the last Arnoldi step
           con_terms_assemble(m_active, o->constraints, p, c->pre_pinned, cons.data());
+        } else if (m_active > 0 && gram_queued == j && m_active == o->n_constraints) {
+          ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
+          con_terms_assemble(m_active, o->constraints, p, c->con_pinned, cons.data());
         } else if (m_active > 0) {
           if (pre_launched) HIP_TRY(hipStreamWaitEvent(s, c->ev_pre_done, 0));  // shares Ut / Gram buffers
           ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
