@@ -55,7 +55,18 @@ struct CsrView {
   const int2* blk_meta = nullptr;
   int walk = 0;
   int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
+  // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
+  // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at
+  // sl_off[s] + 64 t + l; rows padded to the slice's longest (col = the row, val = 0, skipped
+  // by the row length sl_len)
+  const int32_t* sl_col = nullptr;
+  const double* sl_val = nullptr;
+  const int64_t* sl_off = nullptr;
+  const uint16_t* sl_len = nullptr;
+  int32_t n_sl = 0;
 };
+constexpr int kSellW = 64;       // rows per slice (a wave, lane = row)
+constexpr int kSellMaxLen = 64;  // longest row of a SELL copy (longer: no copy, K1p serves)
 
 // grid sizes (a fixed count when partials are all-reduced across ranks)
 int spmv_grid(const CsrView& A, bool fixed);

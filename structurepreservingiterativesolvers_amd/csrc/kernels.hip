@@ -79,6 +79,35 @@ __device__ __forceinline__ double2 ld_basis(const double2* p, bool nt) {
   return *p;
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// buffer-descriptor loads / stores: one 32-bit lane offset shared by every element of a thread,
+// the element's distance in the scalar offset (no per-element address registers).  The hardware
+// range check does not cover the scalar offset: callers predicate every access themselves.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_double2(__hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)),
+                      __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)));
+}
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 d) {
+  u32x4_t v;
+  v.x = static_cast<unsigned>(__double2loint(d.x));
+  v.y = static_cast<unsigned>(__double2hiint(d.x));
+  v.z = static_cast<unsigned>(__double2loint(d.y));
+  v.w = static_cast<unsigned>(__double2hiint(d.y));
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+// one fp64 through a buffer descriptor at a 32-bit byte offset (K1s gathers: no 64-bit address
+// registers per entry)
+__device__ __forceinline__ double buf_ld1(__amdgpu_buffer_rsrc_t r, int voff) {
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+  return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x));
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1: CSR SpMV, row blocks of <= kItemCap merge items (rows + nnz), products staged in LDS.
 //
@@ -549,6 +578,122 @@ __global__ __launch_bounds__(kBlock) void spmv_pipe2_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1s: SpMV on a SELL-64 copy (sliced ELL, 64-row slices, entries t-major within a slice): one
+// wave per slice, lane = row.  Entry t of all 64 rows is one coalesced 256-B col / 512-B val
+// load, so a wave has its whole slice's (col, val) and gathers in flight with no LDS staging, no
+// barrier and no row-sum phase (K1p: two barriers and an LDS pass per 2048-nnz block).  Each
+// lane sums its row's rounded products left to right (contraction off): SciPy's csr_matvec
+// order, so rows are bit-identical to K1 / K1p and to A @ x.  Padding (t >= the row's length)
+// is loaded (col = the row itself) but never added.  MODE as K1p (0-3 = K1's epilogues on x1,
+// 4 = the dual: residual of x1, Arnoldi of x2).  Walk: XCD-local eighths (walk 1) or
+// grid-stride; partials per workgroup in wave order (deterministic).
+// Measured at C3 (opt-in, SPIS_OPT_SPMV_PIPE = 6): dual 43.2 vs 41.3 us for K1dp (130 VGPRs, 3
+// waves per SIMD, each slice two dependent round trips: col, then the gathers); forced to 4
+// waves per SIMD 46.3 us (spills); with the next slice's (col, val) prefetched (207 VGPRs, 2
+// waves per SIMD) 51.7 us.  The LDS-staged K1dp keeps more bytes in flight per VGPR.
+// ---------------------------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
+    int64_t n, int n_sl, int walk, const int64_t* __restrict__ off, const int32_t* __restrict__ scol,
+    const double* __restrict__ sval, const uint16_t* __restrict__ slen, const double* __restrict__ x1,
+    const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
+    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
+    double* __restrict__ part2) {
+#pragma clang fp contract(off)
+  constexpr bool DUAL = MODE == 4;
+  constexpr int TW = 16;  // entries per lane in flight per chunk
+  constexpr int NW = kBlock / 64;
+  __shared__ double s_wave[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t s0, s1e, ss;
+  if (walk == 1 && (gridDim.x & 7) == 0) {  // XCD x = blockIdx % 8 walks the x-th eighth of the slices
+    const int x = blockIdx.x & 7;
+    s0 = (static_cast<int64_t>(n_sl) * x >> 3) + static_cast<int64_t>(blockIdx.x >> 3) * NW + wid;
+    s1e = static_cast<int64_t>(n_sl) * (x + 1) >> 3;
+    ss = static_cast<int64_t>(gridDim.x >> 3) * NW;
+  } else {
+    s0 = static_cast<int64_t>(blockIdx.x) * NW + wid;
+    s1e = n_sl;
+    ss = static_cast<int64_t>(gridDim.x) * NW;
+  }
+  // gathers through buffer descriptors (32-bit offsets; the host checks 8 n < 2^31)
+  const __amdgpu_buffer_rsrc_t rx1 = vec_rsrc(x1, 8 * n);
+  const __amdgpu_buffer_rsrc_t rx2 = vec_rsrc(DUAL ? x2 : x1, 8 * n);
+  double pt1 = 0.0, pt2 = 0.0;
+  for (int64_t sl = s0; sl < s1e; sl += ss) {
+    const int64_t r = sl * kSellW + lane;
+    const bool valid = r < n;
+    const int len = valid ? static_cast<int>(slen[r]) : 0;
+    const int64_t o = off[sl];
+    const int w = static_cast<int>((off[sl + 1] - o) / kSellW);
+    double a1 = 0.0, a2 = 0.0;
+    for (int t0 = 0; t0 < w; t0 += TW) {
+      int c[TW];
+      double v[TW];
+#pragma unroll
+      for (int u = 0; u < TW; ++u)
+        if (t0 + u < w) {  // wave-uniform
+          c[u] = scol[o + static_cast<int64_t>(t0 + u) * kSellW + lane];
+          v[u] = sval[o + static_cast<int64_t>(t0 + u) * kSellW + lane];
+        }
+      double g1[TW], g2[TW];
+#pragma unroll
+      for (int u = 0; u < TW; ++u)
+        if (t0 + u < w) {
+          g1[u] = buf_ld1(rx1, c[u] * 8);
+          if (DUAL) g2[u] = buf_ld1(rx2, c[u] * 8);
+        }
+#pragma unroll
+      for (int u = 0; u < TW; ++u)
+        if (t0 + u < len) {
+          a1 += v[u] * g1[u];
+          if (DUAL) a2 += v[u] * g2[u];
+        }
+    }
+    if (valid) {
+      if (DUAL) {
+        const double t = a1 - aux1[r];
+        pt1 += t * t;
+        y2[r] = a2;
+        pt2 += aux2[r] * a2;
+      }
+      if (MODE == kEpiPlain) y1[r] = a1;
+      if (MODE == kEpiDot) { y1[r] = a1; pt1 += aux1[r] * a1; }
+      if (MODE == kEpiResNorm) { const double t = a1 - aux1[r]; pt1 += t * t; }
+      if (MODE == kEpiR0) { const double t = aux1[r] - a1; y1[r] = t; pt1 += t * t; }
+    }
+  }
+  if (MODE != kEpiPlain) {
+    const double tot1 = block_sum(pt1, s_wave);
+    double tot2 = 0.0;
+    if (DUAL) tot2 = block_sum(pt2, s_wave);
+    if (threadIdx.x == 0) {
+      part1[blockIdx.x] = tot1;
+      if (DUAL) part2[blockIdx.x] = tot2;
+    }
+  }
+}
+
+hipError_t launch_spmv_sell(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
+                            double* part1, const double* x2, const double* aux2, double* y2, double* part2,
+                            int grid, hipStream_t s, const LaunchEv* ev) {
+  dim3 g(grid), b(kBlock);
+#define SPIS_SELL(M)                                                                                          \
+  launch_k(spmv_sell_kernel<M>, g, b, 0, s, ev, A.n_rows, A.n_sl, A.walk, A.sl_off, A.sl_col, A.sl_val, A.sl_len, \
+           x1, aux1, y1, part1, x2, aux2, y2, part2)
+  switch (mode) {
+    case 0: SPIS_SELL(0); break;
+    case 1: SPIS_SELL(1); break;
+    case 2: SPIS_SELL(2); break;
+    case 3: SPIS_SELL(3); break;
+    default: SPIS_SELL(4); break;
+  }
+#undef SPIS_SELL
+  return hipGetLastError();
+}
+
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
                             int grid, hipStream_t s, const LaunchEv* ev) {
@@ -574,6 +719,7 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev) {
+  if (A.sl_col != nullptr) return launch_spmv_sell(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
   if (A.blk_meta != nullptr)
     return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
   if (A.swz)
@@ -604,6 +750,13 @@ static int pipe_grid_max(int depth) {
 int spmv_grid(const CsrView& A, bool fixed) {
   // fixed (multi-GPU: partial arrays all-reduced element-wise) = the same count on every rank
   if (fixed) return A.blk_meta != nullptr ? kPipeGridFixed : kSpmvGrid;
+  if (A.sl_col != nullptr) {  // K1s: resident workgroups, waves walk the slices
+    static const int gs = resident_grid(spmv_sell_kernel<4>);
+    const int64_t need = (static_cast<int64_t>(A.n_sl) + (kBlock / 64) - 1) / (kBlock / 64);
+    int g = need < gs ? static_cast<int>(need) : gs;
+    if (g > 8) g &= ~7;
+    return g < 1 ? 1 : g;
+  }
   const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth) : kSpmvGrid;
   int g = A.n_blk < cap ? A.n_blk : cap;
   if (A.blk_meta != nullptr && g > 8) g &= ~7;  // the XCD-local walk deals workgroups 8 at a time
@@ -619,6 +772,8 @@ int blas_grid(int64_t n, bool fixed) {
 
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
                        double* partials, int grid, hipStream_t s, const LaunchEv* ev) {
+  if (A.sl_col != nullptr)
+    return launch_spmv_sell(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
   if (A.blk_meta != nullptr)
     return launch_spmv_pipe(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
   dim3 g(grid), b(kBlock);
@@ -995,27 +1150,6 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
   if (blockIdx.x == 0 && tid == 0) *epoch = base + static_cast<unsigned>(j) + 2u;
 }
 
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-// buffer-descriptor loads / stores: one 32-bit lane offset shared by every element of a thread,
-// the element's distance in the scalar offset (no per-element address registers).  The hardware
-// range check does not cover the scalar offset: callers predicate every access themselves.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double* p, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, static_cast<int>(bytes), 0x00020000);
-}
-__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  return make_double2(__hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)),
-                      __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)));
-}
-__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int soff, double2 d) {
-  u32x4_t v;
-  v.x = static_cast<unsigned>(__double2loint(d.x));
-  v.y = static_cast<unsigned>(__double2hiint(d.x));
-  v.z = static_cast<unsigned>(__double2loint(d.y));
-  v.w = static_cast<unsigned>(__double2hiint(d.y));
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
-}
-
 // ---------------------------------------------------------------------------------------------
 // K2q: pipelined MGS chain (SPIS_OPT_MGS_CHAIN = 3, the default).  MGS's projections and updates,
 // with each dot product evaluated LAG steps early by the distributive law:
@@ -1060,6 +1194,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   constexpr int DT = DW * 64;  // data threads
   constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
   __shared__ double2 s_acc[FX ? PER * DT : 1];
+  __shared__ double2 s_x0[FX ? PER * DT : 1];
   __shared__ double s_wave[NV * DW];
   __shared__ double s_h;
   __shared__ int s_fail;
@@ -1093,6 +1228,12 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
 #pragma unroll
     for (int m = 0; m < NS - 1; ++m)
       if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch);
+    if (FX && data) {  // x0 into LDS now (added at the end: its load latency off the tail)
+      const double2* x02 = reinterpret_cast<const double2*>(x0);
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (p0 + k * DT < npair) s_x0[k * DT + tid] = ld_basis(x02 + p0 + k * DT, NT);
+    }
   }
   if (tid == 0) s_fail = 0;
   const double h0 = chain_sum_partials(part_in, n_in, s_wave);
@@ -1322,13 +1463,12 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         if (data && p0 + k * DT < npair)
           q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
       if (FX) {
-        const double2* x02 = reinterpret_cast<const double2*>(x0);
         double2* xo2 = reinterpret_cast<double2*>(xo);
 #pragma unroll
         for (int k = 0; k < PER; ++k)
           if (data && p0 + k * DT < npair) {
             const double2 a = s_acc[k * DT + tid];
-            const double2 b = x02[p0 + k * DT];
+            const double2 b = s_x0[k * DT + tid];
             xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
           }
       }

@@ -132,7 +132,7 @@ struct spis_context {
   // completion event (hipStreamWaitEvent: no blit kernels)
   int overlap_gemv = 1;
   hipEvent_t ev_gemv = nullptr;
-  int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1)
+  int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
   // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
   // on stream3 as soon as its basis exists, beside the last Arnoldi step and update
@@ -188,6 +188,14 @@ struct spis_matrix {
   double* stg_val = nullptr;
   int32_t stg_nch = 0;
   bool all_zero = false;
+  // K1s's SELL-64 copy (built on first use by a solve in SpMV mode 6; sell_state -1 unknown, 0 not
+  // eligible: a row longer than kSellMaxLen or > 25% padding, 1 built)
+  int sell_state = -1;
+  int32_t* sl_col = nullptr;
+  double* sl_val = nullptr;
+  int64_t* sl_off = nullptr;
+  uint16_t* sl_len = nullptr;
+  int32_t n_sl = 0;
   GramSplit gram_rows{};  // K7m's XCD-group row ranges (natural row order)
   // K7t's slot table (symmetric matrices; sym_state -1 unknown, 0 not symmetric, 1 built)
   int sym_state = -1;
@@ -272,6 +280,16 @@ CsrView spis_matrix::dual_view() const {
   // auto: the XCD-local walk while val/col fit the 256 MB Infinity Cache (C3 dual SpMV 42-43 vs
   // 44-45 us grid-stride), the grid-stride walk beyond (C5, 1.5 GB: 502 vs 574 us)
   if (mode == 5) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
+  if (mode == 6 && sell_state == 1) {  // K1s, XCD-local walk
+    v.sl_col = sl_col;
+    v.sl_val = sl_val;
+    v.sl_off = sl_off;
+    v.sl_len = sl_len;
+    v.n_sl = n_sl;
+    v.walk = 1;
+    return v;
+  }
+  if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   if (mode > 0) {
     v.blk_meta = blk_meta_d;
     v.n_blk = n_blk;
@@ -279,6 +297,61 @@ CsrView spis_matrix::dual_view() const {
     v.depth = mode >= 3 ? 2 : 1;
   }
   return v;
+}
+
+// K1s's SELL-64 copy of A (CsrView::sl_*), built once from the device CSR
+static int ensure_sell(spis_context* c, spis_matrix* M) {
+  if (M->sell_state >= 0) return SPIS_OK;
+  M->sell_state = 0;
+  const int64_t n = M->n_rows, nnz = M->nnz;
+  if (n == 0 || M->n_long > 0 || 8 * M->n_cols >= (int64_t(1) << 31)) return SPIS_OK;  // 32-bit gather offsets
+  std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
+  std::vector<double> va(std::max<int64_t>(nnz, 1));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  if (nnz > 0) {
+    HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
+  }
+  const int64_t ns = (n + kSellW - 1) / kSellW;
+  std::vector<int64_t> off(ns + 1, 0);
+  for (int64_t sl = 0; sl < ns; ++sl) {
+    int w = 0;
+    for (int64_t r = sl * kSellW; r < std::min<int64_t>(n, (sl + 1) * kSellW); ++r) w = std::max(w, rp[r + 1] - rp[r]);
+    if (w > kSellMaxLen) return SPIS_OK;
+    off[sl + 1] = off[sl] + static_cast<int64_t>(w) * kSellW;
+  }
+  if (static_cast<double>(off[ns]) > 1.25 * static_cast<double>(std::max<int64_t>(nnz, 1)) + kSellW) return SPIS_OK;
+  const int64_t tot = std::max<int64_t>(off[ns], 1);
+  std::vector<int32_t> scol(tot, 0);
+  std::vector<double> sval(tot, 0.0);
+  std::vector<uint16_t> slen(n);
+  for (int64_t sl = 0; sl < ns; ++sl) {
+    const int64_t w = (off[sl + 1] - off[sl]) / kSellW;
+    for (int l = 0; l < kSellW; ++l) {
+      const int64_t r = sl * kSellW + l;
+      const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
+      if (r < n) slen[r] = static_cast<uint16_t>(len);
+      for (int64_t t = 0; t < w; ++t) {
+        const int64_t e = off[sl] + t * kSellW + l;
+        scol[e] = t < len ? ci[rp[r] + t] : static_cast<int32_t>(r < n ? r : 0);
+        sval[e] = t < len ? va[rp[r] + t] : 0.0;
+      }
+    }
+  }
+  auto up = [&](auto** dst, const auto& v) -> int {
+    using T = typename std::remove_reference<decltype(v)>::type::value_type;
+    HIP_TRY(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    return SPIS_OK;
+  };
+  ST_TRY(up(&M->sl_col, scol));
+  ST_TRY(up(&M->sl_val, sval));
+  ST_TRY(up(&M->sl_off, off));
+  ST_TRY(up(&M->sl_len, slen));
+  M->n_sl = static_cast<int32_t>(ns);
+  M->sell_state = 1;
+  return SPIS_OK;
 }
 
 // ---- live kernel timing ------------------------------------------------------------------------
@@ -624,7 +697,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->early_con = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
-        if (value < 0 || value > 5) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 5", (long long)value);
+        if (value < 0 || value > 6) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 6", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_ORTHOG:
@@ -851,7 +924,9 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     if (M->ell_off) (void)hipFree(M->ell_off);
     for (void* p : {static_cast<void*>(M->stg_row), static_cast<void*>(M->stg_uoff), static_cast<void*>(M->stg_uniq),
                     static_cast<void*>(M->stg_eoff), static_cast<void*>(M->stg_width), static_cast<void*>(M->stg_loc),
-                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc), static_cast<void*>(M->sym_col), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
+                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc), static_cast<void*>(M->sym_col),
+                    static_cast<void*>(M->sl_col), static_cast<void*>(M->sl_val), static_cast<void*>(M->sl_off),
+                    static_cast<void*>(M->sl_len), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
       if (p) (void)hipFree(p);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
@@ -1082,6 +1157,7 @@ extern "C" int spis_memcpy_d2h(spis_context* c, void* dst, const void* src, int6
 extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) {
   ABI_GUARD({
     if (!c || !A || !x || !y) return fail(SPIS_ERR_ARG, "null argument");
+    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));
     ST_TRY(exchange(c, A, x));
     HIP_TRY(launch_spmv(A->dual_view(), kEpiPlain, x, y, nullptr, nullptr, spmv_grid(A->dual_view(), fixed_grid(c)),
                         c->stream));
@@ -1093,6 +1169,7 @@ extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) 
 extern "C" int spis_residual_norm(spis_context* c, spis_matrix* A, double* x, const double* b, double* out) {
   ABI_GUARD({
     if (!c || !A || !x || !b || !out) return fail(SPIS_ERR_ARG, "null argument");
+    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));
     ST_TRY(exchange(c, A, x));
     const int g = spmv_grid(A->dual_view(), fixed_grid(c));
     HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, x, nullptr, b, c->partA, g, c->stream));
@@ -2299,6 +2376,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
 
     // every solver SpMV runs on the kDualCap row blocks, so the fused and the single launches
     // group their partial sums identically (bit-identical results either way)
+    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));  // K1s's copy, once per matrix
     Solver S{c, A, o, ws, b, n, k, spmv_grid(A->dual_view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
     ST_TRY(ensure_pinned(c, S.pinned_need()));
     hipStream_t s = c->stream;
