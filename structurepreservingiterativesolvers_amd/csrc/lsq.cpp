@@ -455,6 +455,46 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
     return second_order_ok(st, cons, yr, lam);
   };
 
+  // 0) SLSQP's first LSQ subproblem (LSEI) triangularises the constraint Jacobian at y0 by
+  //    Householder reflections and stops with "Singular matrix C in LSQ subproblem" (mode 6,
+  //    x = y0) when a diagonal element falls below machine epsilon (absolute, unscaled).  A
+  //    constraint whose gradient is pure roundoff (swe/lkdvRK mass with a massless Krylov space,
+  //    |grad| ~ 1e-18) is infeasible for Newton as well: without this test both starts run to the
+  //    iteration limit (C4: 13.6 ms host time, then the same fallback as the reference's).
+  if (m > 0) {
+    std::vector<double> Jc(static_cast<size_t>(m) * p);
+    for (int i = 0; i < m; ++i)
+      for (int a = 0; a < p; ++a) {
+        double t = cons[i].term1[a];
+        for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y[b];
+        Jc[static_cast<size_t>(i) * p + a] = t;
+      }
+    for (int i = 0; i < m; ++i) {  // Householder QR of the rows (J' columns), pivot by pivot
+      double* ri = Jc.data() + static_cast<size_t>(i) * p;
+      double nrm = 0.0;
+      for (int a = i; a < p; ++a) nrm += ri[a] * ri[a];
+      nrm = std::sqrt(nrm);
+      if (!(nrm >= DBL_EPSILON)) {
+        res.message = SPIS_MSG_SINGULAR_C;
+        return res;  // y = y0
+      }
+      const double alpha = ri[i] > 0 ? -nrm : nrm;
+      std::vector<double> v(ri, ri + p);
+      for (int a = 0; a < i; ++a) v[a] = 0.0;
+      v[i] -= alpha;
+      double vv = 0.0;
+      for (int a = i; a < p; ++a) vv += v[a] * v[a];
+      if (vv == 0.0) continue;
+      for (int k = i + 1; k < m; ++k) {
+        double* rk = Jc.data() + static_cast<size_t>(k) * p;
+        double t = 0.0;
+        for (int a = i; a < p; ++a) t += v[a] * rk[a];
+        t = 2.0 * t / vv;
+        for (int a = i; a < p; ++a) rk[a] -= t * v[a];
+      }
+    }
+  }
+
   // 1) warm start at the reference's y0 (solvers.py:225-227), as SLSQP
   std::vector<double> lam;
   init_lam(y, lam);

@@ -178,3 +178,37 @@ def test_kkt_lkdvrk_gl3_final_step_matches_slsqp(lsq):
         assert lsq.lsq_con_value(k, t.term0, _p(t.term1), _p(t.term2), _p(y)) <= 1e-12
     assert func(y) <= func(sol.x) * (1 + 1e-9)
     assert abs(terms[0].term0) == 0.0 and np.linalg.norm(terms[0].term1) < 1e-12  # the degeneracy
+
+
+def test_kkt_singular_constraint_gradient_exits_as_slsqp(lsq):
+    """Config C4's forced constrained step as the device solver saw it (H, beta, warm start and
+    the three reduced constraints dumped by tools/dump_kkt_case.py from a GPU run): the mass
+    constraint's gradient is roundoff (|term1| ~ 1e-18, term0 ~ 7e-15), so SLSQP's first LSQ
+    subproblem stops with "Singular matrix C in LSQ subproblem" at the warm start.  The KKT solve
+    must exit the same way (message 6, y = y0) instead of running both Newton starts to the
+    iteration limit; the reference then falls back (constraint_checker > ctol), as the oracle
+    does at this size."""
+    import os
+    from oracle.cgmres_port import _slsqp
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "kkt_cases", "kkt_c4_final_step.npz"))
+    H, beta, y0 = z["H"], float(z["beta"]), z["y0"]
+    k = H.shape[1]
+    terms = [(z["t0"][i], z["t1"][i], z["t2"][i]) for i in range(len(z["t0"]))]
+    y, msg, it = kkt(lsq, H, beta, terms, y0)
+    assert msg == 6 and it == 0 and np.array_equal(y, y0)
+    res = np.zeros(k + 1)
+    res[0] = beta
+
+    def func(v):
+        return float(np.sum((res - H @ v) ** 2))
+
+    def jac(v):
+        return -2 * H.T @ (res - H @ v)
+
+    cl = [{"type": "eq", "fun": (lambda v, a=a, b=b, c=c: a + b @ v + v @ c @ v),
+           "jac": (lambda v, b=b, c=c: b + 2 * (v @ c))} for a, b, c in terms]
+    sol = _slsqp(func, y0, jac, cl, 1e-24)
+    assert sol.message == "Singular matrix C in LSQ subproblem"
+    np.testing.assert_array_equal(sol.x, y)
+    assert max(f["fun"](y) for f in cl) > 1e-12  # the reference's checker then falls back
