@@ -1816,7 +1816,10 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
   for (int u = 0; u < kMgsPer; ++u)
     if (base + u * kBlock < npair) yv[u] = y2[base + u * kBlock];
   const double h = sqrt(sum_partials(part_in, n_in, s_wave));
-  if (blockIdx.x == 0 && threadIdx.x == 0) *h_out = h;
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // one 8-B system-scope store: a host spinning on the
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(h_out),  // slot sees it whole
+                       static_cast<unsigned long long>(__double_as_longlong(h)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   // breakdown (h == 0): cgmres/gmres stop (solvers.py:199-202); cgmres_p carries on with the
   // q[j+1] row it never wrote, i.e. zeros (solvers.py:172,376-377) — reproduce that here
   while (base - threadIdx.x < npair) {

@@ -1998,7 +1998,10 @@ struct Solver {
   }
   // true once H[:, j] is complete; false if the stream drained without it (a failed chain)
   int wait_hcol(int j, bool* ok) const {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + j + 1);
+    return wait_slot(reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + j + 1), ok);
+  }
+  // spin until a pinned 8-B slot leaves kHSentinel; false if the stream drained first
+  int wait_slot(const uint64_t* w, bool* ok) const {
     const double t0 = now_s();
     for (unsigned spin = 0;; ++spin) {
       if (__atomic_load_n(w, __ATOMIC_ACQUIRE) != kHSentinel) {
@@ -2406,20 +2409,31 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s));
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
+    // beta: the normalize kernel's one system-scope store into pinned memory; the host spins
+    // until the slot leaves its sentinel (an event marker here cost ~6 us of GPU idle per solve);
+    // several GPUs keep the event (the slot is written after an all-reduce)
+    const bool beta_spin = !c->comm;
+    if (beta_spin) *reinterpret_cast<volatile uint64_t*>(beta_slot) = Solver::kHSentinel;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
-    HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)
+    if (!beta_spin) HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)
     // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
     // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
     // L mode: the solver loop below (lag_chain: K2q chains publish H[:, j] to the host themselves)
     const bool L = S.lag_chain() && c->fuse_spmv && !S.graphable();
     if (stamps) stamps[0] = now_s();
     ST_TRY(S.enqueue_arnoldi(0));
-    HIP_TRY(hipEventRecord(c->ev_arn, s));
+    if (!L) HIP_TRY(hipEventRecord(c->ev_arn, s));  // L mode waits for H[:, 0] itself
     if (k > 1) {
       if (stamps) stamps[1] = now_s();
       ST_TRY(S.enqueue_arnoldi(1, !L));  // L: A_1's chain is enqueued at iteration 0
     }
-    ST_TRY(wait_event(c->ev_gram));
+    if (beta_spin) {
+      bool ok = false;
+      ST_TRY(S.wait_slot(reinterpret_cast<const uint64_t*>(beta_slot), &ok));
+      if (!ok) return fail(SPIS_ERR_STATE, "r0 normalisation drained without publishing beta");
+    } else {
+      ST_TRY(wait_event(c->ev_gram));
+    }
     const double beta = *beta_slot;
     int n_res = 0;
     out->res_host[n_res++] = beta;
@@ -2473,6 +2487,22 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     std::vector<double> yspec(k);
     int last_x = -1;  // iteration whose x_j is x[-1]
     int gram_queued = -1;  // iteration whose constraint reduction is already on the stream
+    int spec_kkt = -1;     // iteration whose KKT solve already ran (ycon, spec_kr)
+    KKTResult spec_kr;
+    // L mode: a forced constrained step's reduction (class-form constraints, fused path) is
+    // queued ahead of the residual of the iterate before it (queue_gram)
+    auto gram_early_ok = [&](int jc) {
+      return o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 &&
+             fused_con_ok(c, jc + 1, o->n_constraints, o->constraints) && !pre_launched;
+    };
+    auto queue_gram = [&](int jc) -> int {
+      ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(o->n_constraints, jc + 1)));
+      ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, s,
+                              c->con_pinned));
+      HIP_TRY(hipEventRecord(c->ev_gram, s));
+      gram_queued = jc;
+      return SPIS_OK;
+    };
     for (int j = 0; j < k && !ws->broke_at_start; ++j) {
       bool fused = false, col_added = false;
       if (L) {
@@ -2504,13 +2534,26 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       // L mode, a step that is constrained whatever res_{j-1} says (the forced last step, or
       // safety set, :230): its reduction goes on the stream now, behind c_{j+1} / U_{j-1}'s
       // residual, not after the host has waited for that residual (C3: a 20 us gap before it)
-      if (L && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && (j == k - 1 || safety != kSafetyNone) &&
-          fused_con_ok(c, j + 1, o->n_constraints, o->constraints) && !pre_launched) {
-        ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(o->n_constraints, j + 1)));
-        ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, j + 1, ws->Zb, ws->pitch, ws->x0, s,
-                                c->con_pinned));
-        HIP_TRY(hipEventRecord(c->ev_gram, s));
-        gram_queued = j;
+      if (L && gram_queued != j && (j == k - 1 || safety != kSafetyNone) && gram_early_ok(j)) ST_TRY(queue_gram(j));
+      // ... and when U_{j-1}'s residual cannot stop the run (safety is not True) and the step
+      // is not timed, LS_j's KKT solve runs now, while the GPU still works on that residual
+      // (it was queued behind this reduction, see the end of the iteration); the result is
+      // used unchanged by the constrained branch below
+      if (L && gram_queued == j && safety != kSafetyTrue && !o->timing && spec_kkt != j) {
+        const double* hp = c->pinned + S.hoff(j);
+        if (hp[j + 1] != 0.0) {
+          ST_TRY(wait_event(c->ev_gram));
+          con_terms_assemble(o->n_constraints, o->constraints, j + 1, c->con_pinned, cons.data());
+          if (!col_added) {
+            for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
+            qr.add_column(j, hcol.data());
+            col_added = true;
+          }
+          std::fill(y0.begin(), y0.end(), 0.0);
+          for (int a = 0; a < j; ++a) y0[a] = yk[a];
+          spec_kr = kkt_newton(j + 1, qr.R(), qr.ld(), qr.g(), o->n_constraints, cons.data(), y0.data(), ycon.data());
+          spec_kkt = j;
+        }
       }
       ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : S.wait_update(j - 1));
       prof_drain(c);
@@ -2577,6 +2620,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (m_active > 0 && pre_launched && p == k && m_active == o->n_constraints) {
           ST_TRY(wait_event(c->ev_pre_done));  // reduced early, beside the last Arnoldi step
           con_terms_assemble(m_active, o->constraints, p, c->pre_pinned, cons.data());
+        } else if (m_active > 0 && spec_kkt == j && m_active == o->n_constraints) {
+          // terms assembled and the KKT solved before res_{j-1} was waited for (above)
         } else if (m_active > 0 && gram_queued == j && m_active == o->n_constraints) {
           ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
           con_terms_assemble(m_active, o->constraints, p, c->con_pinned, cons.data());
@@ -2590,7 +2635,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (m_active == 0) {
           qr.solve(p, ycon.data());
         } else {
-          KKTResult kr = kkt_newton(p, qr.R(), qr.ld(), qr.g(), m_active, cons.data(), y0.data(), ycon.data());
+          const KKTResult kr = (spec_kkt == j && m_active == o->n_constraints)
+                                   ? spec_kr
+                                   : kkt_newton(p, qr.R(), qr.ld(), qr.g(), m_active, cons.data(), y0.data(), ycon.data());
           msg = kr.message;
           ws->last_con.assign(cons.begin(), cons.begin() + m_active);
           ws->last_con_p = p;
@@ -2645,6 +2692,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           if (stamps) stamps[j + 2] = now_s();
           ST_TRY(S.enqueue_dual(j, j + 2));
         } else {
+          // the forced constrained last step's reduction first (its inputs, q_0 .. q_{k-1} and
+          // x0, are complete): the host's KKT then runs while the GPU computes this residual
+          if (j + 1 == k - 1 && gram_early_ok(j + 1)) ST_TRY(queue_gram(j + 1));
           ST_TRY(S.enqueue_residual(j));
         }
       } else if (j + 2 < k && c->fuse_spmv) {
