@@ -1441,6 +1441,17 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       update(hu, S[RM]);
     }
     if (i == j) {  // last: subtract h_j q_j, ||w||^2 through the gatherer, normalise
+      if (FX) {  // x is complete (its last term, q_{px-1}, passed at step j - 1): stored now, its
+                 // write drains during the two exchanges still ahead instead of after them
+        double2* xo2 = reinterpret_cast<double2*>(xo);
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+          if (data && p0 + k * DT < npair) {
+            const double2 a = s_acc[k * DT + tid];
+            const double2 b = s_x0[k * DT + tid];
+            xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
+          }
+      }
       double hj = h0;
       if (j >= 1 && !wait_h(j, &hj)) return false;
       update(hj, S[R]);
@@ -1462,19 +1473,19 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       for (int k = 0; k < PER; ++k)
         if (data && p0 + k * DT < npair)
           q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
-      if (FX) {
-        double2* xo2 = reinterpret_cast<double2*>(xo);
-#pragma unroll
-        for (int k = 0; k < PER; ++k)
-          if (data && p0 + k * DT < npair) {
-            const double2 a = s_acc[k * DT + tid];
-            const double2 b = s_x0[k * DT + tid];
-            xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
-          }
-      }
       return false;
     }
-    if (FX && i < px) {  // x += yx_i q_i (K4's order; x0 is added after the last coefficient)
+    // q_{i+NS-1} into the slot q_{i-1} just left
+    if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
+    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
+    if (i == 0) {
+      if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
+    }
+    if (i + LAG <= j) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
+    // x += yx_i q_i (K4's order; x0 is added after the last coefficient), after this step's
+    // partials are published: its LDS read-modify-write overlaps the exchange instead of
+    // delaying the dots (q_i stays in slot R until the next step's update)
+    if (FX && i < px) {
       const double cf = yx.v[i];
 #pragma unroll
       for (int k = 0; k < PER; ++k)
@@ -1486,13 +1497,6 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
           s_acc[k * DT + tid] = a;
         }
     }
-    // q_{i+NS-1} into the slot q_{i-1} just left
-    if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
-    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
-    if (i == 0) {
-      if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
-    }
-    if (i + LAG <= j) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
     return true;
   };
   for (int i = 0;; i += NS) {
