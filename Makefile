@@ -16,7 +16,7 @@ build/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -c $< -o $@
 
-build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/sptrsv.h $(SRC)/ilu_plan.h $(SRC)/lsq.h include/spis.h
+build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/slab_order.h $(SRC)/sptrsv.h $(SRC)/ilu_plan.h $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -x hip --offload-arch=$(ARCH) -c $< -o $@
 
@@ -36,8 +36,9 @@ $(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
 # host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
-$(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp
-	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp
+$(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp \
+                       $(SRC)/slab_order.h $(SRC)/slab_capi.cpp
+	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp $(SRC)/slab_capi.cpp
 
 clean:
 	rm -rf build $(LIB) $(PKG)/liblsq_host.so
@@ -46,4 +47,6 @@ clean:
 
 # tuning tools (not built by default)
 tools/chainbench: tools/chainbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h
+	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<
+tools/kbench: tools/kbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/slab_order.h
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<

@@ -166,7 +166,7 @@ def main():
                          "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
     ap.add_argument("--gram", default="mfma", choices=["staged", "ell", "csr", "mfma", "mfma_full"],
                     help="constraint-Gram matrix form (SPIS_OPT_ELL_GRAM)")
-    ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "stride2", "xcd2", "auto", "sell"],
+    ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "stride2", "xcd2", "auto", "sell", "xcd_natural"],
                     help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
                          "pipelined XCD-local walk")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
@@ -207,7 +207,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
-                                                                       "sell": 6}[args.spmv_pipe]),
+                                                                       "sell": 6, "xcd_natural": 7}[args.spmv_pipe]),
                "spis_set_option")
 
     if wl["cycles"] > 1:
@@ -262,9 +262,10 @@ def main():
         pipe = "xcd" if 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
     traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",
-             "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk)", "stride2": "spmv_pipe2_kernel<2048, 4>",
+             "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)", "stride2": "spmv_pipe2_kernel<2048, 4>",
              "xcd2": "spmv_pipe2_kernel<2048, 4> (XCD-local walk)",
-             "sell": "spmv_sell_kernel<4> (SELL-64 copy, XCD-local walk)"}[pipe]
+             "sell": "spmv_sell_kernel<4> (SELL-64 copy, XCD-local walk)",
+             "xcd_natural": "spmv_pipe_kernel<2048, 4> (XCD-local walk, natural block order)"}[pipe]
     if fused:  # the dominant SpMV launch: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
         roof = {"kernel": kname + ": true-residual SpMV of x_j, solvers.py:290, fused with the "
                           "Arnoldi SpMV of z_{j+2}, :191; matrix read once",

@@ -148,7 +148,10 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   GEMV launch's own completion event (2; measured equal end to end); 0 = main stream.
  * SPIS_OPT_SPMV_PIPE (default 5): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
  *   software-pipelined row-block kernels; 2 = each XCD's workgroups walk a contiguous eighth of
- *   the row blocks (its share of the gathered vectors stays in its own L2), 1 = grid-stride walk,
+ *   the row blocks (its share of the gathered vectors stays in its own L2) in slab order when the
+ *   upload found one (square matrices whose DoF groups are numbered one after another: the blocks
+ *   sorted by the label their rows' columns carry, spis.cpp build_slab_order), 7 = 2 on the
+ *   blocks' natural order, 1 = grid-stride walk,
  *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight;
  *   5 = 2 while the matrix's val/col fit the 256 MB Infinity Cache, else 1.  Rows are bit-identical in every mode; the reduction partials
  *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.

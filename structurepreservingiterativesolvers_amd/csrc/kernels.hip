@@ -338,7 +338,7 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
 
 __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1, int& bs) {
   const int G = gridDim.x;
-  if (walk == 1 && (G & 7) == 0) {
+  if (walk >= 1 && (G & 7) == 0) {
     const int x = blockIdx.x & 7;
     b0 = static_cast<int>((static_cast<int64_t>(n_blk) * x) >> 3) + (blockIdx.x >> 3);
     b1 = static_cast<int>((static_cast<int64_t>(n_blk) * (x + 1)) >> 3);
@@ -369,8 +369,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   double pt1 = 0.0, pt2 = 0.0;
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
+  const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
   PipeStage<CAP> cur;
-  if (b0 < b1) pipe_load<CAP, MODE, NT>(cur, meta, b0, rp, ci, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE, NT>(cur, meta, b0 * ms, rp, ci, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += bs) {
     const int nb = blk + bs;
     if (cur.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
         if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
         if (MODE == kEpiR0) { const double t = aux1[r0] - s1; y1[r0] = t; pt1 += t * t; }
       }
-      if (nb < b1) pipe_load<CAP, MODE, NT>(cur, meta, nb, rp, ci, va, aux1, aux2);
+      if (nb < b1) pipe_load<CAP, MODE, NT>(cur, meta, nb * ms, rp, ci, va, aux1, aux2);
       continue;
     }
     // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     }
     PipeStage<CAP> nxt;
     nxt.nnz = 0;
-    if (nb < b1) pipe_load<CAP, MODE, NT>(nxt, meta, nb, rp, ci, va, aux1, aux2);
+    if (nb < b1) pipe_load<CAP, MODE, NT>(nxt, meta, nb * ms, rp, ci, va, aux1, aux2);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int i = threadIdx.x + u * kBlock;
@@ -492,19 +493,20 @@ __global__ __launch_bounds__(kBlock) void spmv_pipe2_kernel(
   double pt1 = 0.0, pt2 = 0.0;
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
+  const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
   PipeStage<CAP> s0, s1;
   PipeGath<CAP, MODE> g0, g1n;
   s0.nnz = 0;
   s1.nnz = 0;
-  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0, rp, ci, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0 * ms, rp, ci, va, aux1, aux2);
   if (b0 < b1) pipe_gather<CAP, MODE>(g0, s0, x1, x2);
-  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, b0 + bs, rp, ci, va, aux1, aux2);
+  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, (b0 + bs) * ms, rp, ci, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += bs) {
     // in flight from the previous round: g0 (block blk) and s1 (block blk + bs)
     if (blk + bs < b1) pipe_gather<CAP, MODE>(g1n, s1, x1, x2);
     PipeStage<CAP> s2;
     s2.nnz = 0;
-    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, blk + 2 * bs, rp, ci, va, aux1, aux2);
+    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, (blk + 2 * bs) * ms, rp, ci, va, aux1, aux2);
     if (s0.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
       double acc1 = 0.0, acc2 = 0.0;
       for (int i = s0.nz0 + threadIdx.x; i < s0.nz0 + s0.nnz; i += kBlock) {
@@ -926,6 +928,14 @@ hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double*
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(1))) unsigned long long chain_gu64;
 constexpr unsigned long long kChainWaitTicks = 50000000ull;  // 0.5 s at 100 MHz
+// SPIS_CHAIN_TRACE (tools/chainbench only, never in libspis): K2q phase timestamps (100 MHz
+// s_memrealtime) of data workgroup 0, the last data workgroup and the gatherer
+#ifdef SPIS_CHAIN_TRACE
+__device__ unsigned long long g_chain_trace[3][48];
+#define CHAIN_TR(row, idx) (g_chain_trace[row][idx] = __builtin_amdgcn_s_memrealtime())
+#else
+#define CHAIN_TR(row, idx) ((void)0)
+#endif
 
 __device__ __forceinline__ void chain_store(unsigned long long* p, unsigned tag, unsigned half) {
   __hip_atomic_store((chain_gu64*)p, (static_cast<unsigned long long>(tag) << 32) | half, __ATOMIC_RELAXED,
@@ -1236,11 +1246,14 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     }
   }
   if (tid == 0) s_fail = 0;
+  const int tr_row = blockIdx.x == 0 ? 0 : agg ? 2 : static_cast<int>(blockIdx.x) == GD - 1 ? 1 : -1;
+  if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 0);
   const double h0 = chain_sum_partials(part_in, n_in, s_wave);
   if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
     const double t = chain_sum_partials(xpart, n_x, s_wave);
     if (tid == 0) publish(x_out, t, flag, seq);
   }
+  if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 1);
 
   if (agg) {  // ---- the gatherer: one wave sums, forms h_m and publishes it
     if (tid >= 64) return;
@@ -1327,6 +1340,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
                              __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
+      if (lane == 0) CHAIN_TR(2, 2 + m);
       if (!ok) return;
 #pragma unroll
       for (int l = 0; l + 1 < LAG; ++l) hl[l] = hl[l + 1];
@@ -1366,6 +1380,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     }
     __syncthreads();
     *out = s_h;
+    if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 2 + m);
     const bool failed = s_fail != 0;
     __syncthreads();  // s_h is rewritten by the next wait
     return !failed;
@@ -1473,6 +1488,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       for (int k = 0; k < PER; ++k)
         if (data && p0 + k * DT < npair)
           q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+      if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 40);
       return false;
     }
     // q_{i+NS-1} into the slot q_{i-1} just left

@@ -1,0 +1,64 @@
+// slab_order.h — host-side slab order of the SpMV row blocks (spis.cpp at upload, tools/kbench,
+// the host test library).
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+namespace spis {
+
+// Slab order of the row blocks for the XCD-local walk (each XCD takes a contiguous eighth of the
+// table, so its gathers of x stay in its own L2 when its rows' columns are close).  FE matrices
+// often number DoF groups one after another (swe RT2 x DG0: edge, interior and cell DoFs): a
+// contiguous eighth of the rows is then one group's slab, whose columns sit in three distant
+// ranges of x shared with two other XCDs (C3: each 128-B line of x fetched by 3.0 XCDs).  One
+// pass of label propagation fixes that: rows get kSlabLabels labels by contiguous nnz ranges,
+// then each row takes the label most of its columns carry (a coupled DoF of another group adopts
+// the slab of the DoFs it couples to), a block the label most of its rows carry, and the blocks
+// are stably sorted by label (C3: 3.0 -> 1.14 XCDs per line).  Rows are unchanged (each row
+// sum bit-identical); only which workgroup adds a row into its partial dot products changes.
+// Square matrices only (a column is a row); false when the order would equal the contiguous one.
+constexpr int kSlabLabels = 64;
+inline bool build_slab_order(int64_t n, const int32_t* rp, const int32_t* ci, const std::vector<int32_t>& blk,
+                             std::vector<int32_t>& pairs) {
+  const int64_t nnz = rp[n];
+  const int64_t nb = static_cast<int64_t>(blk.size()) - 1;
+  if (n < 1 || nnz < 1 || nb < 16) return false;
+  std::vector<uint8_t> lab0(n), lab(n);
+  for (int64_t r = 0; r < n; ++r)
+    lab0[r] = static_cast<uint8_t>(std::min<int64_t>(kSlabLabels - 1, static_cast<int64_t>(rp[r]) * kSlabLabels / nnz));
+  int cnt[kSlabLabels];
+  for (int64_t r = 0; r < n; ++r) {
+    std::fill(cnt, cnt + kSlabLabels, 0);
+    for (int32_t i = rp[r]; i < rp[r + 1]; ++i) ++cnt[lab0[ci[i]]];
+    int best = lab0[r];  // ties (and empty rows) keep the row's own label
+    for (int l = 0; l < kSlabLabels; ++l)
+      if (cnt[l] > cnt[best]) best = l;
+    lab[r] = static_cast<uint8_t>(best);
+  }
+  std::vector<std::pair<int, int64_t>> key(nb);
+  bool moved = false;
+  for (int64_t b = 0; b < nb; ++b) {
+    std::fill(cnt, cnt + kSlabLabels, 0);
+    for (int32_t r = blk[b]; r < blk[b + 1]; ++r) ++cnt[lab[r]];
+    int best = 0;
+    for (int l = 1; l < kSlabLabels; ++l)
+      if (cnt[l] > cnt[best]) best = l;
+    key[b] = {best, b};
+    if (b > 0 && best < key[b - 1].first) moved = true;
+  }
+  if (!moved) return false;
+  std::sort(key.begin(), key.end());
+  pairs.resize(4 * nb);  // per block (row start, nz start, row end, nz end): the kernels' int2 pairs
+  for (int64_t i = 0; i < nb; ++i) {
+    const int64_t b = key[i].second;
+    pairs[4 * i] = blk[b];
+    pairs[4 * i + 1] = rp[blk[b]];
+    pairs[4 * i + 2] = blk[b + 1];
+    pairs[4 * i + 3] = rp[blk[b + 1]];
+  }
+  return true;
+}
+
+}  // namespace spis

@@ -27,6 +27,7 @@
 
 #include "ilu_plan.h"
 #include "kernels.h"
+#include "slab_order.h"
 #include "lsq.h"
 #include "sptrsv.h"
 #include "spis.h"
@@ -177,6 +178,7 @@ struct spis_matrix {
   int32_t* blk_row_d = nullptr;  // row blocks of <= kDualCap nnz / items for the fused dual SpMV
   int32_t n_blk_d = 0;
   int2* blk_meta_d = nullptr;    // blk_row's blocks (<= kPipeCap nnz) as (row start, nz start): the pipelined kernels' table
+  int2* blk_slab_d = nullptr;    // the same blocks as (start, end) pairs in slab order (XCD-local walk 2), or null
   // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
@@ -290,6 +292,13 @@ CsrView spis_matrix::dual_view() const {
     return v;
   }
   if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
+  if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
+  else if (mode == 2 && blk_slab_d != nullptr) {
+    v.blk_meta = blk_slab_d;
+    v.n_blk = n_blk;
+    v.walk = 2;
+    return v;
+  }
   if (mode > 0) {
     v.blk_meta = blk_meta_d;
     v.n_blk = n_blk;
@@ -697,7 +706,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->early_con = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
-        if (value < 0 || value > 6) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 6", (long long)value);
+        if (value < 0 || value > 7) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 7", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_ORTHOG:
@@ -870,6 +879,11 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       for (size_t i = 0; i < blk.size(); ++i) meta[i] = make_int2(blk[i], indptr[blk[i]]);
       HIP_TRY(hipMalloc(&M->blk_meta_d, sizeof(int2) * meta.size()));
       HIP_TRY(hipMemcpy(M->blk_meta_d, meta.data(), sizeof(int2) * meta.size(), hipMemcpyHostToDevice));
+      std::vector<int32_t> pairs;
+      if (n_ghost == 0 && build_slab_order(n_rows, indptr, indices, blk, pairs)) {
+        HIP_TRY(hipMalloc(&M->blk_slab_d, sizeof(int32_t) * pairs.size()));
+        HIP_TRY(hipMemcpy(M->blk_slab_d, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice));
+      }
     }
     {  // the fused residual + Arnoldi SpMV stages two product arrays: half-size blocks keep its LDS
       int32_t n_long_d = 0;  // at 16 KiB per workgroup (kbench: 52 vs 62 us at C3)
@@ -919,6 +933,7 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->blk_row);
     (void)hipFree(M->blk_row_d);
     (void)hipFree(M->blk_meta_d);
+    (void)hipFree(M->blk_slab_d);
     if (M->ell_col) (void)hipFree(M->ell_col);
     if (M->ell_val) (void)hipFree(M->ell_val);
     if (M->ell_off) (void)hipFree(M->ell_off);

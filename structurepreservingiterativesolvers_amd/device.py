@@ -58,7 +58,7 @@ _OPTIONS = {
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
-                                        "sell": 6}),
+                                        "sell": 6, "xcd_natural": 7}),
 }
 
 

@@ -69,10 +69,10 @@ def _matrices():
     return out
 
 
-@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd2", "stride2", "off", "auto", "sell"])
+@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd2", "stride2", "off", "auto", "sell", "xcd_natural"])
 def test_spmv_bit_exact_vs_scipy(spis, pipe):
-    """Every SpMV kernel (SPIS_OPT_SPMV_PIPE: pipelined XCD-local / grid-stride walk, unpipelined)
-    is bit-exact vs SciPy on rows that fit a row block (<= 1024 nnz: the solver's table); longer
+    """Every SpMV kernel (SPIS_OPT_SPMV_PIPE: pipelined XCD-local walk in slab / natural block
+    order, grid-stride walk, unpipelined, SELL) is bit-exact vs SciPy on rows that fit a row block (<= 1024 nnz: the solver's table); longer
     rows take the workgroup-wide reduction (1e-12)."""
     from structurepreservingiterativesolvers_amd import primitives as P
     from structurepreservingiterativesolvers_amd.device import set_option
@@ -114,14 +114,14 @@ def test_spmv_pipe_modes_solver_agree(spis):
     A, b = dic["A"], dic["b"]
     runs = {}
     try:
-        for pipe in ("off", "stride", "xcd", "stride2", "xcd2", "sell"):
+        for pipe in ("off", "stride", "xcd", "stride2", "xcd2", "sell", "xcd_natural"):
             set_option("spmv_pipe", pipe)
             x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
             runs[pipe] = (x, np.asarray(d["res"]), d["steps"], d["x"].trace)
     finally:
         set_option("spmv_pipe", "auto")
     x0, r0, s0, t0 = runs["off"]
-    for pipe in ("stride", "xcd", "stride2", "xcd2", "sell"):
+    for pipe in ("stride", "xcd", "stride2", "xcd2", "sell", "xcd_natural"):
         x, r, st, tr = runs[pipe]
         assert st == s0 and tr == t0, pipe
         assert np.linalg.norm(x - x0) <= 1e-9 * np.linalg.norm(x0), pipe

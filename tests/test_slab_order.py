@@ -1,0 +1,86 @@
+"""Slab order of the SpMV row blocks (csrc/slab_order.h via the host-only liblsq_host.so), on CPU.
+
+The XCD-local SpMV walk (SPIS_OPT_SPMV_PIPE 2, the default at C3) gives each XCD a contiguous
+eighth of the block table.  The upload reorders the table so that an eighth is a spatial slab
+across the DoF groups the FE numbering puts one after another; rows are untouched.  Checked here:
+the table is a permutation of the blocks with consistent nz offsets, the share of 128-B lines of
+the gathered vector that several eighths touch drops on the swe matrix (M=30), and a banded
+matrix (already slab-like) keeps its natural order."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sps
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "structurepreservingiterativesolvers_amd", "liblsq_host.so")
+PI = C.POINTER(C.c_int32)
+
+
+@pytest.fixture(scope="module")
+def host():
+    if not os.path.exists(LIB):
+        pytest.skip("liblsq_host.so not built (make)")
+    L = C.CDLL(LIB)
+    L.slab_order_blocks.argtypes = [C.c_int64, PI, PI, PI, C.c_int64, PI]
+    L.slab_order_blocks.restype = C.c_int
+    return L
+
+
+def _blocks(A, rows=256):
+    n = A.shape[0]
+    return np.ascontiguousarray(np.append(np.arange(0, n, rows), n), dtype=np.int32)
+
+
+def _order(host, A, blk):
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+    out = np.zeros(4 * (len(blk) - 1), dtype=np.int32)
+    ok = host.slab_order_blocks(A.shape[0], rp.ctypes.data_as(PI), ci.ctypes.data_as(PI), blk.ctypes.data_as(PI),
+                                len(blk), out.ctypes.data_as(PI))
+    return ok, out.reshape(-1, 4)
+
+
+def _lines_per_eighth(A, spans):
+    """Sum over eighths of the table of the 16-entry lines of x its rows gather / total lines."""
+    rp, ci = A.indptr, A.indices
+    nb = len(spans)
+    tot = 0
+    for g in range(8):
+        sel = spans[nb * g // 8: nb * (g + 1) // 8]
+        cols = np.concatenate([ci[rp[r0]:rp[r1]] for r0, r1 in sel])
+        tot += np.unique(cols // 16).size
+    return tot / ((A.shape[1] + 15) // 16)
+
+
+def test_swe_slab_order(host):
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    A = dic["A"].tocsr()
+    blk = _blocks(A)
+    ok, pairs = _order(host, A, blk)
+    assert ok == 1
+    # a permutation of the blocks, nz offsets from indptr
+    natural = np.stack([blk[:-1], blk[1:]], axis=1)
+    got = pairs[:, [0, 2]]
+    assert sorted(map(tuple, got)) == sorted(map(tuple, natural))
+    np.testing.assert_array_equal(pairs[:, 1], A.indptr[pairs[:, 0]])
+    np.testing.assert_array_equal(pairs[:, 3], A.indptr[pairs[:, 2]])
+    before = _lines_per_eighth(A, natural)
+    after = _lines_per_eighth(A, got)
+    assert before > 3.0 and after < 0.6 * before, (before, after)  # C3 (M=289): 3.0 -> 1.14
+
+
+def test_banded_keeps_natural_order(host):
+    n = 20000
+    A = sps.diags([np.ones(n - 1), 2 * np.ones(n), np.ones(n - 1)], [-1, 0, 1], format="csr")
+    ok, _ = _order(host, A, _blocks(A))
+    assert ok == 0
+
+
+def test_too_few_blocks(host):
+    A = sps.random(1000, 1000, density=0.01, format="csr", random_state=1)
+    ok, _ = _order(host, A, _blocks(A, rows=256))
+    assert ok == 0

@@ -1,7 +1,12 @@
+#!/bin/bash
+# A/B of bench options, interleaved: tools/ab_bench.sh ROUNDS "opts A" "opts B" ...
+# ("-" = no options); prints it/s and the dual / chain kernel means per run.
 set -e
-for r in 1 2 3; do
-  for opt in "" "--graphs" "--no-fuse"; do
-    v=$(python bench.py --no-cpu-baseline --steps 20 $opt | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']), round(d['kernels']['iteration_us'],1))")
-    echo "run$r [$opt] $v"
+rounds=$1; shift
+for r in $(seq 1 "$rounds"); do
+  for opt in "$@"; do
+    o=$opt; [ "$o" = - ] && o=""
+    v=$(timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 3 $o | python -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); k=d['kernels']; print('%.0f it/s dual %.1f chain %.1f arnoldi %.1f' % (d['value'], k['spmv_dual_us'], k['mgs_chain_us_mean'], k['spmv_arnoldi_us']))")
+    echo "round $r [$opt]: $v"
   done
 done

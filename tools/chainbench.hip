@@ -6,8 +6,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
+#define SPIS_CHAIN_TRACE 1
 #include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
 
 using namespace spis;
@@ -61,6 +63,40 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   std::vector<double> y(64, 0.01);
   // the chain reads w and never writes it: repeated launches see the same inputs
+  if (argc > 3 && std::string(argv[3]) == "trace") {  // phase timestamps of K2q + FX (the solver's chain)
+    set_chain_lag(2);
+    for (int j : {1, 5, 15, 29}) {
+      auto run = [&]() {
+        CK(launch_mgs_chain(n, w, Q, pitch, j, part, 1024, hcol_dev, gran, ep, err, s, nullptr, nullptr, 0, nullptr,
+                            nullptr, nullptr, true, 1, gsub, y.data(), j, x0, xo));
+      };
+      for (int r = 0; r < 3; ++r) run();
+      CK(hipStreamSynchronize(s));
+      for (int rep = 0; rep < 3; ++rep) {
+        unsigned long long tr[3][48] = {};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_trace), tr, sizeof(tr)));
+        CK(hipEventRecord(e0, s));
+        run();
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_chain_trace), sizeof(tr)));
+        unsigned long long t0 = ~0ull;
+        for (int r = 0; r < 3; ++r)
+          if (tr[r][0] && tr[r][0] < t0) t0 = tr[r][0];
+        printf("j=%2d event %.1f us\n", j, 1e3 * ms);
+        const char* rn[3] = {"wg0", "wgL", "gat"};
+        for (int r = 0; r < 3; ++r) {
+          printf("  %s start %.2f loaded %.2f |", rn[r], 0.01 * (tr[r][0] - t0), 0.01 * (tr[r][1] - t0));
+          for (int m = 1; m <= j + 1; ++m) printf(" %.2f", tr[r][2 + m] ? 0.01 * (tr[r][2 + m] - t0) : -1.0);
+          if (r < 2) printf(" | stored %.2f", 0.01 * (tr[r][40] - t0));
+          printf("\n");
+        }
+      }
+    }
+    return 0;
+  }
   const char* names[] = {"K2p agg", "K2q", "K2q+gemv", "gemv"};
   for (int lag = 1; lag <= 2; ++lag)
   for (int nt = 0; nt < 2; ++nt)

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
+#include "../structurepreservingiterativesolvers_amd/csrc/slab_order.h"
 
 using namespace spis;
 
@@ -560,6 +561,37 @@ int main(int argc, char** argv) {
                              dpr + 4096);
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, dmeta,
                            nbd, 1, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+      }
+      // the same on the solver's default table (kPipeCap = 2048-nnz blocks, resident grid): 5 warm,
+      // then 5 cold
+      std::vector<int2> meta2(blk.size());
+      for (size_t i = 0; i < blk.size(); ++i) meta2[i] = make_int2(blk[i], rp[blk[i]]);
+      int2* dmeta2;
+      CK(hipMalloc(&dmeta2, 8 * meta2.size()));
+      CK(hipMemcpy(dmeta2, meta2.data(), 8 * meta2.size(), hipMemcpyHostToDevice));
+      const int g2 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
+      printf("pmc mode: kPipeCap dual on %d blocks, grid %d\n", nb, g2);
+      for (int i = 0; i < 10; ++i) {
+        if (i >= 5)
+          hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
+                             dpr + 4096);
+        hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva, dmeta2, nb, 1, dx,
+                           dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+      }
+      // and on the solver's default order (slab-ordered (start, end) pairs, walk 2): 5 warm, 5 cold
+      std::vector<int32_t> pairs;
+      if (build_slab_order(n, rp.data(), ci.data(), blk, pairs)) {
+        int2* dpairs;
+        CK(hipMalloc(&dpairs, 4 * pairs.size()));
+        CK(hipMemcpy(dpairs, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice));
+        printf("pmc mode: slab-ordered dual on %d blocks\n", nb);
+        for (int i = 0; i < 10; ++i) {
+          if (i >= 5)
+            hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                               reinterpret_cast<const double2*>(bx), dpr + 4096);
+          hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva,
+                             dpairs, nb, 2, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+        }
       }
       CK(hipStreamSynchronize(s));
       CK(hipFree(bx));

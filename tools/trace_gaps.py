@@ -3,8 +3,8 @@ import collections
 import csv
 import sys
 
-KEYS = ['mgs_chain', 'spmv_pipe_kernel<1024, 4', 'spmv_pipe_kernel<1024, 3', 'spmv_pipe_kernel<1024, 1',
-        'spmv_pipe_kernel<1024, 2', 'spmv_dual', 'mgs_step', 'spmv_rowblock_kernel<1>', 'spmv_rowblock_kernel<2>', 'spmv_rowblock_kernel<3>',
+KEYS = ['mgs_chain', 'spmv_pipe_kernel<2048, 4', 'spmv_pipe_kernel<2048, 3', 'spmv_pipe_kernel<2048, 1',
+        'spmv_pipe_kernel<2048, 2', 'spmv_dual', 'mgs_step', 'spmv_rowblock_kernel<1>', 'spmv_rowblock_kernel<2>', 'spmv_rowblock_kernel<3>',
         'spmv_rowblock_kernel<0>', 'constraint_gram', 'gemv', 'normalize', 'transpose', 'gram_reduce',
         'copy_kernel', 'fillBuffer', 'copyBuffer', 'dot', 'finalize']
 
@@ -17,7 +17,7 @@ def short(n):
 
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
-R0 = ('spmv_rowblock_kernel<3>', 'spmv_pipe_kernel<1024, 3')  # r0 = b - A x0 opens every solve
+R0 = ('spmv_rowblock_kernel<3>', 'spmv_pipe_kernel<2048, 3')  # r0 = b - A x0 opens every solve
 idx = [i for i, r in enumerate(rows) if any(k in r['Kernel_Name'] for k in R0)]
 s0, s1 = idx[-2], idx[-1]
 seg = rows[s0:s1]
