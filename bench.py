@@ -138,8 +138,8 @@ def build_workload(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
                     help="SURVEY §8 configuration (c3 = the BASELINE.json line)")
     ap.add_argument("--M", type=int, default=None, help="mesh size override (swe: N = 12 M^2 per GPU)")

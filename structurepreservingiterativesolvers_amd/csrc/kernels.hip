@@ -1205,7 +1205,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
   __shared__ double2 s_acc[FX ? PER * DT : 1];
   __shared__ double2 s_x0[FX ? PER * DT : 1];
-  __shared__ double s_wave[NV * DW];
+  __shared__ double s_wave[2 * NV * DW];  // publish_m's wave sums by m's parity: step 0 publishes E_1
+                                         // and E_2 back to back (E_2's sums are written while E_1's
+                                         // may still be read); chain_sum_partials uses the first 4
   __shared__ double s_h;
   __shared__ int s_fail;
   const int G = gridDim.x;
@@ -1388,12 +1390,13 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   // the workgroup's partials of E_m: v[0] = a_m, v[1 + d] = G(m, m - LAG + d) when ng > 0
   // (granules {tag, half}, sc1 stores from a data wave)
   auto publish_m = [&](const double (&v)[NV], bool with_g, int m) {
+    double* sw = s_wave + (m & 1) * (NV * DW);
     double wv[NV];
 #pragma unroll
     for (int c = 0; c < NV; ++c) wv[c] = (c == 0 || with_g) ? wave_sum_dpp(v[c]) : 0.0;
     if (data && (tid & 63) == 0) {
 #pragma unroll
-      for (int c = 0; c < NV; ++c) s_wave[c * DW + (tid >> 6)] = wv[c];
+      for (int c = 0; c < NV; ++c) sw[c * DW + (tid >> 6)] = wv[c];
     }
     __syncthreads();
     if (tid == 0) {
@@ -1401,9 +1404,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
 #pragma unroll
       for (int c = 0; c < NV; ++c) {
         if (c > 0 && (!with_g || m - LAG + (c - 1) < 0)) continue;
-        double t = s_wave[c * DW];
+        double t = sw[c * DW];
 #pragma unroll
-        for (int q = 1; q < DW; ++q) t += s_wave[c * DW + q];
+        for (int q = 1; q < DW; ++q) t += sw[c * DW + q];
         const unsigned long long bb = static_cast<unsigned long long>(__double_as_longlong(t));
         unsigned long long* sl = c == 0 ? aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG + 2 * blockIdx.x
                                         : gslots + static_cast<size_t>(LAG - c) * 2 * kChainMaxWG + 2 * blockIdx.x;

@@ -293,10 +293,11 @@ CsrView spis_matrix::dual_view() const {
   }
   if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
-  else if (mode == 2 && blk_slab_d != nullptr) {
+  else if ((mode == 2 || mode == 4) && blk_slab_d != nullptr) {
     v.blk_meta = blk_slab_d;
     v.n_blk = n_blk;
     v.walk = 2;
+    v.depth = mode == 4 ? 2 : 1;
     return v;
   }
   if (mode > 0) {

@@ -619,6 +619,76 @@ int main(int argc, char** argv) {
     printf("%-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
            100.0 * bytes / (us * 1e-6) / 8e12);
   };
+  if (argc > 2 && std::string(argv[2]) == "slab") {
+    // the solver's dual (kPipeCap table) in natural vs slab block order, resident grid vs more
+    // workgroups, nontemporal matrix loads; warm (back to back: the matrix Infinity-Cache
+    // resident, as in the solver) and cold
+    double *dx2, *dw, *db, *pa, *pb;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&db, 8 * pitch));
+    CK(hipMalloc(&pa, 8 * 16384));
+    CK(hipMalloc(&pb, 8 * 16384));
+    std::vector<double> h2(pitch);
+    for (int64_t i = 0; i < pitch; ++i) h2[i] = i < n ? 1e-3 * ((i * 104729) % 997) - 0.4 : 0.0;
+    CK(hipMemcpy(dx2, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    std::vector<int32_t> blk, pairs;
+    blocks(n, rp.data(), kPipeCap, 256, kPipeCap, blk);
+    const int nb = static_cast<int>(blk.size()) - 1;
+    std::vector<int2> meta(nb + 1);
+    for (int i = 0; i <= nb; ++i) meta[i] = make_int2(blk[i], rp[blk[i]]);
+    int2 *mn, *ms;
+    CK(hipMalloc(&mn, 8 * meta.size()));
+    CK(hipMemcpy(mn, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice));
+    if (!build_slab_order(n, rp.data(), ci.data(), blk, pairs)) {
+      printf("no slab order\n");
+      return 1;
+    }
+    CK(hipMalloc(&ms, 4 * pairs.size()));
+    CK(hipMemcpy(ms, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice));
+    const int64_t big = int64_t(1) << 26;
+    double* bx;
+    CK(hipMalloc(&bx, 8 * big));
+    CK(hipMemset(bx, 0, 8 * big));
+    const int gr = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
+    printf("blocks %d, resident grid %d (NT %d, WPE2 %d)\n", nb, gr, resident_grid(spmv_pipe_kernel<kPipeCap, 4, true>),
+           resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 2>));
+    auto run = [&](const char* name, auto&& launch) {
+      for (int cold = 0; cold < 2; ++cold) {
+        double tot = 0;
+        const int reps = 30;
+        for (int r = 0; r < reps + 3; ++r) {
+          if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                                       reinterpret_cast<const double2*>(bx), pb + 8192);
+          launch();
+          CK(hipEventSynchronize(e1));
+          float ms_;
+          CK(hipEventElapsedTime(&ms_, e0, e1));
+          if (r >= 3) tot += ms_;
+        }
+        const double us = 1e3 * tot / reps;
+        printf("%s %-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", cold ? "COLD" : "WARM", name, us,
+               SD / (us * 1e-6) / 1e9, 100.0 * SD / (us * 1e-6) / 8e12);
+      }
+    };
+    char nm[128];
+#define SLABRUN(LABEL, NTV, WPEV, MT, WALK, G)                                                                  \
+  snprintf(nm, sizeof nm, "%s grid=%d", LABEL, G);                                                             \
+  run(nm, [&] {                                                                                                \
+    hipExtLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, \
+                          dci, dva, MT, nb, WALK, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);             \
+  })
+    SLABRUN("natural", false, 1, mn, 1, gr);
+    SLABRUN("slab", false, 1, ms, 2, gr);
+    for (int g : {512, 1024, 1280}) { SLABRUN("slab", false, 1, ms, 2, g); }
+    SLABRUN("slab NT", true, 1, ms, 2, gr);
+    SLABRUN("slab WPE2", false, 2, ms, 2, gr);
+    SLABRUN("slab WPE2", false, 2, ms, 2, 1024);
+#undef SLABRUN
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "cap") {
     // K1dp / K1p block capacity: 512 / 1024 / 2048 nnz per row block (<= 256 rows), warm (back to
     // back: the matrix Infinity-Cache resident, as in the solver) and cold; rows checked bit-equal
