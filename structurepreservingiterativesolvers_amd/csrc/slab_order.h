@@ -20,12 +20,12 @@ namespace spis {
 // sum bit-identical); only which workgroup adds a row into its partial dot products changes.
 // Square matrices only (a column is a row); false when the order would equal the contiguous one.
 constexpr int kSlabLabels = 64;
-inline bool build_slab_order(int64_t n, const int32_t* rp, const int32_t* ci, const std::vector<int32_t>& blk,
-                             std::vector<int32_t>& pairs) {
+// the rows' slab labels (one propagation pass over the matrix's pattern); false if too small
+inline bool slab_labels(int64_t n, const int32_t* rp, const int32_t* ci, std::vector<uint8_t>& lab) {
   const int64_t nnz = rp[n];
-  const int64_t nb = static_cast<int64_t>(blk.size()) - 1;
-  if (n < 1 || nnz < 1 || nb < 16) return false;
-  std::vector<uint8_t> lab0(n), lab(n);
+  if (n < 1 || nnz < 1) return false;
+  std::vector<uint8_t> lab0(n);
+  lab.assign(n, 0);
   for (int64_t r = 0; r < n; ++r)
     lab0[r] = static_cast<uint8_t>(std::min<int64_t>(kSlabLabels - 1, static_cast<int64_t>(rp[r]) * kSlabLabels / nnz));
   int cnt[kSlabLabels];
@@ -37,28 +37,53 @@ inline bool build_slab_order(int64_t n, const int32_t* rp, const int32_t* ci, co
       if (cnt[l] > cnt[best]) best = l;
     lab[r] = static_cast<uint8_t>(best);
   }
-  std::vector<std::pair<int, int64_t>> key(nb);
+  return true;
+}
+
+// a stable order of items by label; false when it is the natural one
+inline bool slab_sort(const std::vector<uint8_t>& item_lab, std::vector<int64_t>& order) {
+  const int64_t m = static_cast<int64_t>(item_lab.size());
   bool moved = false;
-  for (int64_t b = 0; b < nb; ++b) {
+  for (int64_t i = 1; i < m && !moved; ++i) moved = item_lab[i] < item_lab[i - 1];
+  if (!moved) return false;
+  order.resize(m);
+  for (int64_t i = 0; i < m; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return item_lab[a] < item_lab[b]; });
+  return true;
+}
+
+// the row blocks blk in slab order of the rows' labels lab
+inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab, const std::vector<int32_t>& blk,
+                             std::vector<int32_t>& pairs) {
+  const int64_t nb = static_cast<int64_t>(blk.size()) - 1;
+  if (nb < 16) return false;
+  std::vector<uint8_t> blab(nb);
+  int cnt[kSlabLabels];
+  for (int64_t b = 0; b < nb; ++b) {  // a block: the label most of its rows carry
     std::fill(cnt, cnt + kSlabLabels, 0);
     for (int32_t r = blk[b]; r < blk[b + 1]; ++r) ++cnt[lab[r]];
     int best = 0;
     for (int l = 1; l < kSlabLabels; ++l)
       if (cnt[l] > cnt[best]) best = l;
-    key[b] = {best, b};
-    if (b > 0 && best < key[b - 1].first) moved = true;
+    blab[b] = static_cast<uint8_t>(best);
   }
-  if (!moved) return false;
-  std::sort(key.begin(), key.end());
+  std::vector<int64_t> order;
+  if (!slab_sort(blab, order)) return false;
   pairs.resize(4 * nb);  // per block (row start, nz start, row end, nz end): the kernels' int2 pairs
   for (int64_t i = 0; i < nb; ++i) {
-    const int64_t b = key[i].second;
+    const int64_t b = order[i];
     pairs[4 * i] = blk[b];
     pairs[4 * i + 1] = rp[blk[b]];
     pairs[4 * i + 2] = blk[b + 1];
     pairs[4 * i + 3] = rp[blk[b + 1]];
   }
   return true;
+}
+
+inline bool build_slab_order(int64_t n, const int32_t* rp, const int32_t* ci, const std::vector<int32_t>& blk,
+                             std::vector<int32_t>& pairs) {
+  std::vector<uint8_t> lab;
+  return static_cast<int64_t>(blk.size()) > 16 && slab_labels(n, rp, ci, lab) && build_slab_order(rp, lab, blk, pairs);
 }
 
 }  // namespace spis
