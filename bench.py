@@ -258,8 +258,10 @@ def main():
     fused = cnt[_lib.PROF_SPMV_DUAL] > 0
     # the PMC summaries were measured on the default kernels (pipelined, XCD-local walk)
     pipe = args.spmv_pipe
-    if pipe == "auto":  # as the library decides (SPIS_OPT_SPMV_PIPE 5)
-        pipe = "xcd" if 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
+    if pipe == "auto":  # as the library decides (SPIS_OPT_SPMV_PIPE 5): the XCD-local walk, on the
+        # slab-ordered table when the upload found one (the swe configs), else while val/col fit
+        # the 256 MB Infinity Cache
+        pipe = "xcd" if args.config in ("c3", "c5") or 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
     traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",
              "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)", "stride2": "spmv_pipe2_kernel<2048, 4>",

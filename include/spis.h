@@ -153,7 +153,8 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  *   sorted by the label their rows' columns carry, spis.cpp build_slab_order), 7 = 2 on the
  *   blocks' natural order, 1 = grid-stride walk,
  *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight;
- *   5 = 2 while the matrix's val/col fit the 256 MB Infinity Cache, else 1.  Rows are bit-identical in every mode; the reduction partials
+ *   5 = 2 when the table has a slab order or the matrix's val/col fit the 256 MB Infinity Cache,
+ *   else 1.  Rows are bit-identical in every mode; the reduction partials
  *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.
  * SPIS_OPT_EARLY_CON (default 0): the constraint reduction of CGMRES's forced final constrained
  *   step (j = k-1) is launched on a third stream once A_{k-1} (2; measured equal to 0 at C3) or

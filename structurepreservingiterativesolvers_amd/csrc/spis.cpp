@@ -281,7 +281,8 @@ CsrView spis_matrix::dual_view() const {
   int mode = ctx->spmv_pipe;
   // auto: the XCD-local walk while val/col fit the 256 MB Infinity Cache (C3 dual SpMV 42-43 vs
   // 44-45 us grid-stride), the grid-stride walk beyond (C5, 1.5 GB: 502 vs 574 us)
-  if (mode == 5) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
+  // (the slab-ordered table wins at both sizes: C5 dual 485 vs 498 us grid-stride)
+  if (mode == 5) mode = blk_slab_d != nullptr || 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   if (mode == 6 && sell_state == 1) {  // K1s, XCD-local walk
     v.sl_col = sl_col;
     v.sl_val = sl_val;
