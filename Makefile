@@ -16,7 +16,7 @@ build/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -c $< -o $@
 
-build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/slab_order.h $(SRC)/sptrsv.h $(SRC)/ilu_plan.h $(SRC)/lsq.h include/spis.h
+build/spis.o: $(SRC)/spis.cpp $(SRC)/kernels.h $(SRC)/slab_order.h $(SRC)/col16.h $(SRC)/sptrsv.h $(SRC)/ilu_plan.h $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -x hip --offload-arch=$(ARCH) -c $< -o $@
 
@@ -37,7 +37,7 @@ $(LIB): $(OBJS)
 
 # host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
 $(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp \
-                       $(SRC)/slab_order.h $(SRC)/slab_capi.cpp
+                       $(SRC)/slab_order.h $(SRC)/col16.h $(SRC)/slab_capi.cpp
 	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp $(SRC)/slab_capi.cpp
 
 clean:
@@ -48,5 +48,5 @@ clean:
 # tuning tools (not built by default)
 tools/chainbench: tools/chainbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<
-tools/kbench: tools/kbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/slab_order.h
+tools/kbench: tools/kbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/slab_order.h $(SRC)/col16.h
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<

@@ -38,10 +38,10 @@ METRIC = "CGMRES iterations/sec + SpMV achieved HBM GB/s, N=10^6 DoF CSR fp64"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def spmv_bytes(n_rows, nnz):
-    """Algorithmic bytes of one CSR SpMV: fp64 val + int32 col per nnz,
-    int32 rowptr, x read once, y written once."""
-    return 12 * nnz + 4 * (n_rows + 1) + 16 * n_rows
+def spmv_bytes(n_rows, nnz, col_bytes=4):
+    """Algorithmic bytes of one CSR SpMV: fp64 val + int32 col per nnz (int16 with
+    the 16-bit column copy, SPIS_OPT_COL16), int32 rowptr, x read once, y written once."""
+    return (8 + col_bytes) * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
 def mgs_bytes(n, p, chain=True):
@@ -51,10 +51,10 @@ def mgs_bytes(n, p, chain=True):
     return 8 * n * (p + 2) if chain else 32 * n * p + 16 * n
 
 
-def dual_bytes(n_rows, nnz):
+def dual_bytes(n_rows, nnz, col_bytes=4):
     """Algorithmic bytes of the fused residual + Arnoldi SpMV: the matrix once, x_j and b read
     (true residual, solvers.py:290), z_{j+2} read and w written (Arnoldi, :191)."""
-    return 12 * nnz + 4 * (n_rows + 1) + 32 * n_rows
+    return (8 + col_bytes) * nnz + 4 * (n_rows + 1) + 32 * n_rows
 
 
 def load_traffic(name="spmv_traffic.json"):
@@ -169,6 +169,8 @@ def main():
     ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "stride2", "xcd2", "auto", "sell", "xcd_natural"],
                     help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
                          "pipelined XCD-local walk")
+    ap.add_argument("--col16", type=int, default=1, choices=[0, 1, 2],
+                    help="16-bit column copy for the pipelined SpMV: 1 beyond the Infinity Cache, 2 always, 0 never")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
                     help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
@@ -204,6 +206,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, args.chain), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_COL16, args.col16), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
@@ -241,10 +244,13 @@ def main():
     _lib.check(L.spis_profile_enable(ctx.handle, 0), "spis_profile_enable")
     elapsed = t1 - t0
 
-    S = spmv_bytes(n, A.nnz)
+    # the 16-bit column copy (SPIS_OPT_COL16, as the library decides: the swe matrices have one)
+    c16 = args.col16 == 2 or (args.col16 == 1 and 12 * A.nnz > 256 * 1024 * 1024 and args.config in ("c3", "c5"))
+    cb = 2 if c16 else 4
+    S = spmv_bytes(n, A.nnz, cb)
     spmv_ms = ms[_lib.PROF_SPMV] / max(cnt[_lib.PROF_SPMV], 1)
     spmv_gbs = S / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
-    SD = dual_bytes(n, A.nnz)
+    SD = dual_bytes(n, A.nnz, cb)
     dual_ms = ms[_lib.PROF_SPMV_DUAL] / max(cnt[_lib.PROF_SPMV_DUAL], 1)
     dual_gbs = SD / (dual_ms * 1e-3) / 1e9 if dual_ms > 0 else 0.0
     sampled = [j + 1 for j in range(0, args.k, max(args.prof_period, 1))]
@@ -262,12 +268,14 @@ def main():
         # slab-ordered table when the upload found one (the swe configs), else while val/col fit
         # the 256 MB Infinity Cache
         pipe = "xcd" if args.config in ("c3", "c5") or 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
-    traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" else None
+    traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" and not c16 else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",
              "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)", "stride2": "spmv_pipe2_kernel<2048, 4>",
              "xcd2": "spmv_pipe2_kernel<2048, 4> (XCD-local walk)",
              "sell": "spmv_sell_kernel<4> (SELL-64 copy, XCD-local walk)",
              "xcd_natural": "spmv_pipe_kernel<2048, 4> (XCD-local walk, natural block order)"}[pipe]
+    if c16 and pipe in ("stride", "xcd", "xcd_natural"):
+        kname = kname.replace(", 4>", ", 4, C16>").replace(")", ", 16-bit columns)")
     if fused:  # the dominant SpMV launch: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
         roof = {"kernel": kname + ": true-residual SpMV of x_j, solvers.py:290, fused with the "
                           "Arnoldi SpMV of z_{j+2}, :191; matrix read once",

@@ -164,7 +164,13 @@ int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t
  * SPIS_OPT_NT_BASIS (default 2): the persistent MGS chain loads basis vectors with nontemporal
  *   loads, so re-streaming the basis every Arnoldi step does not evict the matrix from the
  *   256 MB Infinity Cache before the next SpMV; 2 = when the matrix and the k+1 basis vectors
- *   exceed 256 MB, 1 = always, 0 = never.  Results identical. */
+ *   exceed 256 MB, 1 = always, 0 = never.  Results identical.
+ * SPIS_OPT_COL16 (default 1): the pipelined SpMV (K1p / K1dp, one-deep) reads the matrix's
+ *   columns from a 16-bit copy made at upload when every row block spans <= 4 ranges of 2^14
+ *   columns (csrc/col16.h: a 2-bit base index + 14-bit offset per nonzero, 4 base columns per
+ *   block): 10 instead of 12 bytes per nonzero.  1 = when val/col exceed the 256 MB Infinity
+ *   Cache (C5: dual 470 vs 494 us; a cache-resident C3 matrix is faster on 32-bit columns,
+ *   37.6 vs 39.5 us), 2 = always, 0 = never.  Rows bit-identical. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -175,7 +181,8 @@ enum spis_option {
   SPIS_OPT_OVERLAP_GEMV = 7,
   SPIS_OPT_SPMV_PIPE = 8,
   SPIS_OPT_EARLY_CON = 9,
-  SPIS_OPT_NT_BASIS = 10
+  SPIS_OPT_NT_BASIS = 10,
+  SPIS_OPT_COL16 = 11
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -26,6 +26,7 @@ OPT_FUSE_SPMV, OPT_GENERIC_GRAM, OPT_GRAPHS, OPT_ORTHOG, OPT_ELL_GRAM, OPT_MGS_C
 OPT_SPMV_PIPE = 8
 OPT_EARLY_CON = 9
 OPT_NT_BASIS = 10
+OPT_COL16 = 11
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

@@ -54,6 +54,9 @@ struct CsrView {
   // blockIdx; 1 = XCD-local (workgroups blockIdx % 8 == x walk the x-th eighth of the blocks).
   const int2* blk_meta = nullptr;
   int walk = 0;
+  // C16 (col16.h): 16-bit columns + per-block base columns, in the table's block order
+  const uint16_t* col16 = nullptr;
+  const int4* blk_base = nullptr;
   int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
   // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
   // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at

@@ -300,15 +300,34 @@ struct PipeStage {
   double vals[kPer];
   int rs, re;     // this thread's row bounds relative to nz0 (rows r0 + threadIdx.x)
   double a1, a2;  // the row's aux values (b / q0 / aux)
+  int bs0, bs1, bs2, bs3;  // C16: the block's base columns (col16.h; plain ints: the stage must
+                          // stay in registers)
 };
 
-template <int CAP, int MODE, bool NT = false>
-__device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int blk,
+// C16: column = base[k] + offset of a 16-bit entry (k = the top 2 bits)
+__device__ __forceinline__ int col16_decode(unsigned v, int b0, int b1, int b2, int b3) {
+  const unsigned k = v >> 14;
+  const int base = (k & 2u) ? ((k & 1u) ? b3 : b2) : ((k & 1u) ? b1 : b0);
+  return base + static_cast<int>(v & 0x3fffu);
+}
+
+// block lb of the table (entries lb * ms, lb * ms + 1: ms = 1 consecutive starts, 2 (start, end)
+// pairs); C16: the columns from the 16-bit copy and the block's bases base[lb]
+template <int CAP, int MODE, bool NT = false, bool C16 = false>
+__device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int lb, int ms,
                                           const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                          const uint16_t* __restrict__ c16, const int4* __restrict__ base,
                                           const double* __restrict__ va, const double* __restrict__ aux1,
                                           const double* __restrict__ aux2) {
-  const int2 m0 = meta[blk];
-  const int2 m1 = meta[blk + 1];
+  const int2 m0 = meta[lb * ms];
+  const int2 m1 = meta[lb * ms + 1];
+  if (C16) {
+    const int* bp = reinterpret_cast<const int*>(base) + 4 * lb;
+    st.bs0 = bp[0];
+    st.bs1 = bp[1];
+    st.bs2 = bp[2];
+    st.bs3 = bp[3];
+  }
   st.r0 = m0.x;
   st.r1 = m1.x;
   st.nz0 = m0.y;
@@ -317,7 +336,11 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
 #pragma unroll
   for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
     const int i = threadIdx.x + u * kBlock;
-    if (NT) {  // streamed once: keep L2 for the gathered vectors
+    if (C16) {
+      st.cols[u] = i < st.nnz ? c16[st.nz0 + i] : 0;  // raw: decoded at the gathers, so the prefetch
+                                                      // stays in flight (0 decodes to a column of the block)
+      st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
+    } else if (NT) {  // streamed once: keep L2 for the gathered vectors
       st.cols[u] = i < st.nnz ? __builtin_nontemporal_load(ci + st.nz0 + i) : 0;
       st.vals[u] = i < st.nnz ? __builtin_nontemporal_load(va + st.nz0 + i) : 0.0;
     } else {
@@ -352,13 +375,14 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 
 // x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
 // x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half
-template <int CAP, int MODE, bool NT = false, int WPE = 1>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void spmv_pipe_kernel(
+// C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
+template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16 ? 3 : 8))) void spmv_pipe_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2) {
+    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
   constexpr bool DUAL = MODE == 4;
   constexpr int kPer = PipeStage<CAP>::kPer;
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
@@ -371,7 +395,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   block_walk(n_blk, walk, b0, b1, bs);
   const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
   PipeStage<CAP> cur;
-  if (b0 < b1) pipe_load<CAP, MODE, NT>(cur, meta, b0 * ms, rp, ci, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE, NT, C16>(cur, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += bs) {
     const int nb = blk + bs;
     if (cur.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
@@ -379,8 +403,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
       {
         double acc1 = 0.0, acc2 = 0.0;
         for (int i = cur.nz0 + threadIdx.x; i < cur.nz0 + cur.nnz; i += kBlock) {
-          acc1 += va[i] * x1[ci[i]];
-          if (DUAL) acc2 += va[i] * x2[ci[i]];
+          const int c = C16 ? col16_decode(c16[i], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : ci[i];
+          acc1 += va[i] * x1[c];
+          if (DUAL) acc2 += va[i] * x2[c];
         }
         s1 = block_sum(acc1, s_wave);
         if (DUAL) s2 = block_sum(acc2, s_wave);
@@ -398,7 +423,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
         if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
         if (MODE == kEpiR0) { const double t = aux1[r0] - s1; y1[r0] = t; pt1 += t * t; }
       }
-      if (nb < b1) pipe_load<CAP, MODE, NT>(cur, meta, nb * ms, rp, ci, va, aux1, aux2);
+      if (nb < b1) pipe_load<CAP, MODE, NT, C16>(cur, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
       continue;
     }
     // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
@@ -406,12 +431,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     double g1[kPer], g2[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      g1[u] = x1[cur.cols[u]];
-      if (DUAL) g2[u] = x2[cur.cols[u]];
+      const int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
+      g1[u] = x1[c];
+      if (DUAL) g2[u] = x2[c];
     }
     PipeStage<CAP> nxt;
     nxt.nnz = 0;
-    if (nb < b1) pipe_load<CAP, MODE, NT>(nxt, meta, nb * ms, rp, ci, va, aux1, aux2);
+    if (nb < b1) pipe_load<CAP, MODE, NT, C16>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int i = threadIdx.x + u * kBlock;
@@ -498,15 +524,15 @@ __global__ __launch_bounds__(kBlock) void spmv_pipe2_kernel(
   PipeGath<CAP, MODE> g0, g1n;
   s0.nnz = 0;
   s1.nnz = 0;
-  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0 * ms, rp, ci, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
   if (b0 < b1) pipe_gather<CAP, MODE>(g0, s0, x1, x2);
-  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, (b0 + bs) * ms, rp, ci, va, aux1, aux2);
+  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, b0 + bs, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += bs) {
     // in flight from the previous round: g0 (block blk) and s1 (block blk + bs)
     if (blk + bs < b1) pipe_gather<CAP, MODE>(g1n, s1, x1, x2);
     PipeStage<CAP> s2;
     s2.nnz = 0;
-    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, (blk + 2 * bs) * ms, rp, ci, va, aux1, aux2);
+    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, blk + 2 * bs, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
     if (s0.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
       double acc1 = 0.0, acc2 = 0.0;
       for (int i = s0.nz0 + threadIdx.x; i < s0.nz0 + s0.nnz; i += kBlock) {
@@ -704,9 +730,12 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   if (A.depth == 2)                                                                                             \
     launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
+  else if (A.col16 != nullptr)                                                                                  \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,        \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
-             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2)
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
@@ -743,10 +772,11 @@ static int resident_grid(F kernel) {
   return t < 8 ? 8 : (t > kSpmvGrid ? kSpmvGrid : t);
 }
 
-static int pipe_grid_max(int depth) {
+static int pipe_grid_max(int depth, bool c16) {
   static const int g1 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
+  static const int g1c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 1, true>);
   static const int g2 = resident_grid(spmv_pipe2_kernel<kPipeCap, 4>);
-  return depth == 2 ? g2 : g1;
+  return depth == 2 ? g2 : c16 ? g1c : g1;
 }
 
 int spmv_grid(const CsrView& A, bool fixed) {
@@ -759,7 +789,7 @@ int spmv_grid(const CsrView& A, bool fixed) {
     if (g > 8) g &= ~7;
     return g < 1 ? 1 : g;
   }
-  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth) : kSpmvGrid;
+  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth, A.col16 != nullptr) : kSpmvGrid;
   int g = A.n_blk < cap ? A.n_blk : cap;
   if (A.blk_meta != nullptr && g > 8) g &= ~7;  // the XCD-local walk deals workgroups 8 at a time
   return g < 1 ? 1 : g;

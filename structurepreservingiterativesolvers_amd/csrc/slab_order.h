@@ -54,7 +54,7 @@ inline bool slab_sort(const std::vector<uint8_t>& item_lab, std::vector<int64_t>
 
 // the row blocks blk in slab order of the rows' labels lab
 inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab, const std::vector<int32_t>& blk,
-                             std::vector<int32_t>& pairs) {
+                             std::vector<int32_t>& pairs, std::vector<int64_t>* order_out = nullptr) {
   const int64_t nb = static_cast<int64_t>(blk.size()) - 1;
   if (nb < 16) return false;
   std::vector<uint8_t> blab(nb);
@@ -77,6 +77,7 @@ inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab,
     pairs[4 * i + 2] = blk[b + 1];
     pairs[4 * i + 3] = rp[blk[b + 1]];
   }
+  if (order_out) order_out->swap(order);
   return true;
 }
 

@@ -28,6 +28,7 @@
 #include "ilu_plan.h"
 #include "kernels.h"
 #include "slab_order.h"
+#include "col16.h"
 #include "lsq.h"
 #include "sptrsv.h"
 #include "spis.h"
@@ -133,6 +134,7 @@ struct spis_context {
   // completion event (hipStreamWaitEvent: no blit kernels)
   int overlap_gemv = 1;
   hipEvent_t ev_gemv = nullptr;
+  int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
   // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
@@ -179,6 +181,9 @@ struct spis_matrix {
   int32_t n_blk_d = 0;
   int2* blk_meta_d = nullptr;    // blk_row's blocks (<= kPipeCap nnz) as (row start, nz start): the pipelined kernels' table
   int2* blk_slab_d = nullptr;    // the same blocks as (start, end) pairs in slab order (XCD-local walk 2), or null
+  uint16_t* col16_d = nullptr;   // C16 copy of the columns (col16.h), or null
+  int4* base_nat_d = nullptr;     // its per-block bases, natural block order
+  int4* base_slab_d = nullptr;    // the same in slab order
   // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
@@ -213,6 +218,7 @@ struct spis_matrix {
   double* send_buf = nullptr;
   CsrView view() const { return CsrView{n_rows, indptr, indices, vals, blk_row, n_blk}; }
   CsrView dual_view() const;
+  bool use_col16() const;
 };
 
 struct ConCache {
@@ -275,6 +281,14 @@ static void drop_graphs(spis_workspace* ws) {
 // ------------------------------------------------------------------------------------------------
 static bool fixed_grid(const spis_context* c) { return c->comm != nullptr; }
 
+// C16 (SPIS_OPT_COL16): 1 = when val/col exceed the 256 MB Infinity Cache (C5 dual 470 vs
+// 494 us: HBM-bound, 2 B less per nonzero pays; C3, cache-resident: 39.5 vs 37.6 us, the
+// 16-bit loads and the decode cost more than the bytes saved), 2 = always, 0 = never
+bool spis_matrix::use_col16() const {
+  if (col16_d == nullptr || ctx->col16 == 0) return false;
+  return ctx->col16 == 2 || 12.0 * static_cast<double>(nnz) > 256.0 * 1024 * 1024;
+}
+
 // the solver's SpMV table: kDualCap row blocks, run by the pipelined kernels unless disabled
 CsrView spis_matrix::dual_view() const {
   CsrView v{n_rows, indptr, indices, vals, blk_row_d, n_blk_d, false};
@@ -299,6 +313,10 @@ CsrView spis_matrix::dual_view() const {
     v.n_blk = n_blk;
     v.walk = 2;
     v.depth = mode == 4 ? 2 : 1;
+    if (v.depth == 1 && use_col16()) {
+      v.col16 = col16_d;
+      v.blk_base = base_slab_d;
+    }
     return v;
   }
   if (mode > 0) {
@@ -306,6 +324,10 @@ CsrView spis_matrix::dual_view() const {
     v.n_blk = n_blk;
     v.walk = (mode & 1) == 0 ? 1 : 0;
     v.depth = mode >= 3 ? 2 : 1;
+    if (v.depth == 1 && use_col16()) {
+      v.col16 = col16_d;
+      v.blk_base = base_nat_d;
+    }
   }
   return v;
 }
@@ -711,6 +733,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         if (value < 0 || value > 7) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 7", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
         return SPIS_OK;
+      case SPIS_OPT_COL16:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "col16 %lld: 0, 1 or 2", (long long)value);
+        c->col16 = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
@@ -882,9 +908,29 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       HIP_TRY(hipMalloc(&M->blk_meta_d, sizeof(int2) * meta.size()));
       HIP_TRY(hipMemcpy(M->blk_meta_d, meta.data(), sizeof(int2) * meta.size(), hipMemcpyHostToDevice));
       std::vector<int32_t> pairs;
-      if (n_ghost == 0 && build_slab_order(n_rows, indptr, indices, blk, pairs)) {
+      std::vector<int64_t> order;
+      std::vector<uint8_t> lab;
+      if (n_ghost == 0 && static_cast<int64_t>(blk.size()) > 16 && slab_labels(n_rows, indptr, indices, lab) &&
+          build_slab_order(indptr, lab, blk, pairs, &order)) {
         HIP_TRY(hipMalloc(&M->blk_slab_d, sizeof(int32_t) * pairs.size()));
         HIP_TRY(hipMemcpy(M->blk_slab_d, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice));
+      }
+      // C16: the 16-bit column copy with each block's bases, in natural and in slab order
+      std::vector<uint16_t> c16;
+      std::vector<int32_t> bases;
+      if (nnz > 0 && build_col16(indptr, indices, blk, c16, bases)) {
+        HIP_TRY(hipMalloc(&M->col16_d, sizeof(uint16_t) * c16.size()));
+        HIP_TRY(hipMemcpy(M->col16_d, c16.data(), sizeof(uint16_t) * c16.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&M->base_nat_d, sizeof(int32_t) * bases.size()));
+        HIP_TRY(hipMemcpy(M->base_nat_d, bases.data(), sizeof(int32_t) * bases.size(), hipMemcpyHostToDevice));
+        if (M->blk_slab_d != nullptr) {
+          std::vector<int32_t> bs(bases.size());
+          for (size_t i = 0; i < order.size(); ++i)
+            std::copy(bases.begin() + kCol16Bases * order[i], bases.begin() + kCol16Bases * (order[i] + 1),
+                      bs.begin() + kCol16Bases * i);
+          HIP_TRY(hipMalloc(&M->base_slab_d, sizeof(int32_t) * bs.size()));
+          HIP_TRY(hipMemcpy(M->base_slab_d, bs.data(), sizeof(int32_t) * bs.size(), hipMemcpyHostToDevice));
+        }
       }
     }
     {  // the fused residual + Arnoldi SpMV stages two product arrays: half-size blocks keep its LDS
@@ -935,6 +981,9 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->blk_row);
     (void)hipFree(M->blk_row_d);
     (void)hipFree(M->blk_meta_d);
+    (void)hipFree(M->col16_d);
+    (void)hipFree(M->base_nat_d);
+    (void)hipFree(M->base_slab_d);
     (void)hipFree(M->blk_slab_d);
     if (M->ell_col) (void)hipFree(M->ell_col);
     if (M->ell_val) (void)hipFree(M->ell_val);

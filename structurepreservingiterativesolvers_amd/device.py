@@ -59,6 +59,7 @@ _OPTIONS = {
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
                                         "sell": 6, "xcd_natural": 7}),
+    "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
 }
 
 

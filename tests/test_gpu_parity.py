@@ -96,6 +96,49 @@ def test_spmv_bit_exact_vs_scipy(spis, pipe):
         set_option("spmv_pipe", "auto")
 
 
+@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd_natural"])
+def test_spmv_col16_bit_exact_vs_scipy(spis, pipe):
+    """The pipelined SpMV on the 16-bit column copy (SPIS_OPT_COL16 = 2: forced at any size; by
+    default only beyond the Infinity Cache) is bit-exact vs SciPy (decoded columns, same gathers
+    and sums), long rows included (1e-12, as above)."""
+    from structurepreservingiterativesolvers_amd import primitives as P
+    from structurepreservingiterativesolvers_amd.device import set_option
+
+    rng = np.random.default_rng(5)
+    set_option("spmv_pipe", pipe)
+    set_option("col16", True)
+    try:
+        for name, A in _matrices().items():
+            x = rng.normal(size=A.shape[1])
+            y = P.spmv(A, x)
+            yref = A @ x
+            long_rows = np.flatnonzero(np.diff(A.indptr) > 1024)
+            mask = np.ones(A.shape[0], dtype=bool)
+            mask[long_rows] = False
+            assert np.array_equal(y[mask], yref[mask]), name
+            if long_rows.size:
+                np.testing.assert_allclose(y[long_rows], yref[long_rows], rtol=1e-12)
+            r = P.residual_norm(A, x, yref + 1e-3)
+            np.testing.assert_allclose(r, np.linalg.norm(A @ x - (yref + 1e-3)), rtol=1e-12)
+        # the solver on it: the same steps, iterates bitwise equal to the 32-bit columns' (same
+        # table, same partial grouping)
+        from structurepreservingiterativesolvers_amd import solvers
+        from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+        from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+        dic, _ = sa.linforms(M=30)
+        cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+        x16, d16 = solvers.cgmres(dic["A"], dic["b"], np.zeros_like(dic["b"]), 25, tol=1e-19, conlist=cons)
+        set_option("col16", False)
+        x32, d32 = solvers.cgmres(dic["A"], dic["b"], np.zeros_like(dic["b"]), 25, tol=1e-19, conlist=cons)
+        assert d16["steps"] == d32["steps"]
+        assert np.array_equal(x16, x32)
+        assert np.array_equal(np.asarray(d16["res"]), np.asarray(d32["res"]))
+    finally:
+        set_option("spmv_pipe", "auto")
+        set_option("col16", "auto")
+
+
 def test_spmv_pipe_modes_solver_agree(spis):
     """The solver with each SpMV kernel family: identical steps and branches, iterates equal at
     roundoff (the modes group the residual / first-dot partial sums per workgroup differently).

@@ -5,7 +5,9 @@ eighth of the block table.  The upload reorders the table so that an eighth is a
 across the DoF groups the FE numbering puts one after another; rows are untouched.  Checked here:
 the table is a permutation of the blocks with consistent nz offsets, the share of 128-B lines of
 the gathered vector that several eighths touch drops on the swe matrix (M=30), and a banded
-matrix (already slab-like) keeps its natural order."""
+matrix (already slab-like) keeps its natural order.  The 16-bit column copy of the same blocks
+(csrc/col16.h) decodes to the original columns exactly, and is refused for a block that spans
+more than four ranges of 2^14 columns."""
 import ctypes as C
 import os
 
@@ -83,4 +85,52 @@ def test_banded_keeps_natural_order(host):
 def test_too_few_blocks(host):
     A = sps.random(1000, 1000, density=0.01, format="csr", random_state=1)
     ok, _ = _order(host, A, _blocks(A, rows=256))
+    assert ok == 0
+
+
+# ---- the 16-bit column copy (csrc/col16.h) ------------------------------------------------------
+def _col16(host, A, blk):
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+    c16 = np.zeros(max(A.nnz, 1), dtype=np.uint16)
+    bases = np.zeros(4 * (len(blk) - 1), dtype=np.int32)
+    host.col16_encode.argtypes = [PI, PI, PI, C.c_int64, C.POINTER(C.c_uint16), PI]
+    host.col16_encode.restype = C.c_int
+    ok = host.col16_encode(rp.ctypes.data_as(PI), ci.ctypes.data_as(PI), blk.ctypes.data_as(PI), len(blk),
+                           c16.ctypes.data_as(C.POINTER(C.c_uint16)), bases.ctypes.data_as(PI))
+    return ok, c16, bases.reshape(-1, 4)
+
+
+def _decode(A, blk, c16, bases):
+    out = np.empty(A.nnz, dtype=np.int64)
+    for b in range(len(blk) - 1):
+        e0, e1 = A.indptr[blk[b]], A.indptr[blk[b + 1]]
+        v = c16[e0:e1].astype(np.int64)
+        out[e0:e1] = bases[b][v >> 14] + (v & 0x3FFF)
+    return out
+
+
+def test_col16_round_trip_swe(host):
+    """Every column of the swe operator decodes exactly from (2-bit base index, 14-bit offset)."""
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    A = sa.linforms(M=30)[0]["A"].tocsr()
+    blk = _blocks(A, rows=200)
+    ok, c16, bases = _col16(host, A, blk)
+    assert ok == 1
+    np.testing.assert_array_equal(_decode(A, blk, c16, bases), A.indices)
+
+
+def test_col16_long_row_and_refusal(host):
+    # one long row over 3 ranges decodes; a row over 5 distant ranges has no 16-bit copy
+    n = 100000
+    cols = np.array([0, 1, 20000, 20001, 70000, 99999])
+    A = sps.csr_matrix((np.ones(6), (np.zeros(6, dtype=int), cols)), shape=(n, n))
+    blk = np.array([0, 1, n], dtype=np.int32)
+    ok, c16, bases = _col16(host, A, blk)
+    assert ok == 1
+    np.testing.assert_array_equal(_decode(A, blk, c16, bases), A.indices)
+    cols = np.array([0, 20000, 40000, 60000, 80000])
+    A = sps.csr_matrix((np.ones(5), (np.zeros(5, dtype=int), cols)), shape=(n, n))
+    ok, _, _ = _col16(host, A, blk)
     assert ok == 0

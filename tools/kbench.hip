@@ -11,6 +11,7 @@
 
 #include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
 #include "../structurepreservingiterativesolvers_amd/csrc/slab_order.h"
+#include "../structurepreservingiterativesolvers_amd/csrc/col16.h"
 
 using namespace spis;
 
@@ -560,7 +561,7 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
                              dpr + 4096);
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, dmeta,
-                           nbd, 1, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+                           nbd, 1, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
       }
       // the same on the solver's default table (kPipeCap = 2048-nnz blocks, resident grid): 5 warm,
       // then 5 cold
@@ -576,7 +577,7 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
                              dpr + 4096);
         hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva, dmeta2, nb, 1, dx,
-                           dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+                           dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
       }
       // and on the solver's default order (slab-ordered (start, end) pairs, walk 2): 5 warm, 5 cold
       std::vector<int32_t> pairs;
@@ -590,7 +591,7 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
                                reinterpret_cast<const double2*>(bx), dpr + 4096);
           hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva,
-                             dpairs, nb, 2, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart);
+                             dpairs, nb, 2, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
         }
       }
       CK(hipStreamSynchronize(s));
@@ -642,10 +643,29 @@ int main(int argc, char** argv) {
     int2 *mn, *ms;
     CK(hipMalloc(&mn, 8 * meta.size()));
     CK(hipMemcpy(mn, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice));
-    if (!build_slab_order(n, rp.data(), ci.data(), blk, pairs)) {
+    std::vector<uint8_t> lab;
+    std::vector<int64_t> order;
+    if (!slab_labels(n, rp.data(), ci.data(), lab) || !build_slab_order(rp.data(), lab, blk, pairs, &order)) {
       printf("no slab order\n");
       return 1;
     }
+    std::vector<uint16_t> c16;
+    std::vector<int32_t> bases;
+    if (!build_col16(rp.data(), ci.data(), blk, c16, bases)) {
+      printf("no col16 copy\n");
+      return 1;
+    }
+    std::vector<int32_t> bslab(bases.size());
+    for (size_t i = 0; i < order.size(); ++i)
+      for (int q = 0; q < kCol16Bases; ++q) bslab[kCol16Bases * i + q] = bases[kCol16Bases * order[i] + q];
+    uint16_t* dc16;
+    int4 *dbn, *dbs;
+    CK(hipMalloc(&dc16, 2 * c16.size()));
+    CK(hipMemcpy(dc16, c16.data(), 2 * c16.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dbn, 4 * bases.size()));
+    CK(hipMemcpy(dbn, bases.data(), 4 * bases.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dbs, 4 * bslab.size()));
+    CK(hipMemcpy(dbs, bslab.data(), 4 * bslab.size(), hipMemcpyHostToDevice));
     CK(hipMalloc(&ms, 4 * pairs.size()));
     CK(hipMemcpy(ms, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice));
     const int64_t big = int64_t(1) << 26;
@@ -678,7 +698,7 @@ int main(int argc, char** argv) {
   snprintf(nm, sizeof nm, "%s grid=%d", LABEL, G);                                                             \
   run(nm, [&] {                                                                                                \
     hipExtLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, \
-                          dci, dva, MT, nb, WALK, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);             \
+                          dci, dva, MT, nb, WALK, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);             \
   })
     SLABRUN("natural", false, 1, mn, 1, gr);
     SLABRUN("slab", false, 1, ms, 2, gr);
@@ -687,6 +707,44 @@ int main(int argc, char** argv) {
     SLABRUN("slab WPE2", false, 2, ms, 2, gr);
     SLABRUN("slab WPE2", false, 2, ms, 2, 1024);
 #undef SLABRUN
+    const int gc = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 1, true>);
+    printf("C16 resident grid %d\n", gc);
+    const double SD16 = SD - 2.0 * nnz;
+    auto run16 = [&](const char* name, const int2* mt, int walk, const int4* bb, int G) {
+      for (int cold = 0; cold < 2; ++cold) {
+        double tot = 0;
+        const int reps = 30;
+        for (int r = 0; r < reps + 3; ++r) {
+          if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                                       reinterpret_cast<const double2*>(bx), pb + 8192);
+          hipExtLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, false, 1, true>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0,
+                                drp, dci, dva, mt, nb, walk, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, dc16, bb);
+          CK(hipEventSynchronize(e1));
+          float ms_;
+          CK(hipEventElapsedTime(&ms_, e0, e1));
+          if (r >= 3) tot += ms_;
+        }
+        const double us = 1e3 * tot / reps;
+        printf("%s %-44s %8.2f us  %7.0f GB/s of 10 B/nnz  (%.0f%% of 8 TB/s)\n", cold ? "COLD" : "WARM", name, us,
+               SD16 / (us * 1e-6) / 1e9, 100.0 * SD16 / (us * 1e-6) / 8e12);
+      }
+    };
+    run16("C16 natural", mn, 1, dbn, gc);
+    run16("C16 slab", ms, 2, dbs, gc);
+    {  // rows bit-equal to the 32-bit columns
+      std::vector<double> w1(n), w2(n);
+      hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(gr), dim3(kBlock), 0, s, drp, dci, dva, ms, nb, 2, dx, db,
+                         (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, false, 1, true>), dim3(gc), dim3(kBlock), 0, s, drp, dci, dva, ms,
+                         nb, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, dc16, dbs);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(w2.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+      printf("C16 vs 32-bit columns, dual rows: %lld differ\n", (long long)bad);
+    }
     return 0;
   }
   if (argc > 2 && std::string(argv[2]) == "cap") {
@@ -747,12 +805,12 @@ int main(int argc, char** argv) {
   snprintf(nm, sizeof nm, "dual cap%d grid=%d", CAPV, G);                                                      \
   run(nm, SD, [&] {                                                                                            \
     hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
-                          dva, MT, NB, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);                      \
+                          dva, MT, NB, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                      \
   });                                                                                                          \
   snprintf(nm, sizeof nm, "K1 dot cap%d grid=%d", CAPV, G);                                                    \
   run(nm, S, [&] {                                                                                             \
     hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 1, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
-                          dva, MT, NB, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);                                     \
+                          dva, MT, NB, 1, dx, dQ, dw, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                                     \
   })
     for (int g : {1280, 2048}) { CAPRUN(512, m5, nb5, g); }
     for (int g : {1024, 1280}) { CAPRUN(1024, m1, nb1, g); }
@@ -760,9 +818,9 @@ int main(int argc, char** argv) {
 #undef CAPRUN
     {  // rows bit-equal across capacities (each row sum is left to right in every table)
       hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, m1,
-                         nb1, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+                         nb1, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       hipLaunchKernelGGL((spmv_pipe_kernel<2048, 4, false, 1>), dim3(768), dim3(kBlock), 0, s, drp, dci, dva, m2,
-                         nb2, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb);
+                         nb2, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       CK(hipStreamSynchronize(s));
       std::vector<double> w1(n), w2(n);
       CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
@@ -849,7 +907,7 @@ int main(int argc, char** argv) {
   snprintf(nm, sizeof nm, "dual pipe walk=1 %s grid=%d", NAME, G);                                            \
   timeit(nm, 50, SD, [&] {                                                                                    \
     hipLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, drp, dci, dva, mt, \
-                       nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);                                  \
+                       nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                                  \
   })
       VAR("nt", 1024, true, 1, 1280);
       for (int g : {768, 1024, 1280, 2048}) {
@@ -866,7 +924,7 @@ int main(int argc, char** argv) {
       }
       {  // pipe2 bit identity vs pipe at the same grid / walk
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+                           nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
         hipLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pc, dx2, dQ, dw2, pd);
         CK(hipStreamSynchronize(s));
@@ -917,7 +975,7 @@ int main(int argc, char** argv) {
           snprintf(nm, sizeof nm, "dual pipe walk=1 grid=%d", g);
           cold(nm, SD, [&] {
             hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
-                                  dci, dva, mt, nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb);
+                                  dci, dva, mt, nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
           });
         }
         for (int g : {768, 1024, 2048}) {
@@ -944,7 +1002,7 @@ int main(int argc, char** argv) {
           snprintf(nm, sizeof nm, "K1 dot pipe walk=1 grid=%d", g);
           cold(nm, S, [&] {
             hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
-                                  dci, dva, mt, nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb);
+                                  dci, dva, mt, nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
           });
           snprintf(nm, sizeof nm, "K1 dot pipe2 walk=1 grid=%d", g);
           cold(nm, S, [&] {
@@ -958,24 +1016,24 @@ int main(int argc, char** argv) {
       snprintf(nm, sizeof nm, "dual pipe walk=1 x2=x1 grid=1280");
       timeit(nm, 50, SD, [&] {
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "dual pipe walk=1 q0=b grid=1280");
       timeit(nm, 50, SD, [&] {
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx, db, (double*)nullptr, pa, dx2, db, dw, pb);
+                           nb, 1, dx, db, (double*)nullptr, pa, dx2, db, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "single pipe walk=1 ResNorm grid=1280");
       timeit(nm, 50, S, [&] {
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "2x single pipe walk=1 (ResNorm + Dot) grid=1280");
       timeit(nm, 50, SD, [&] {
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb);
+                           nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
         hipLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
-                           nb, 1, dx2, dQ, dw, pb, dx, dQ, dw, pb);
+                           nb, 1, dx2, dQ, dw, pb, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
 #undef VAR
     }
