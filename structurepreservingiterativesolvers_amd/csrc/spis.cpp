@@ -2340,9 +2340,10 @@ struct Solver {
 
   // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
   int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
-    if (c->overlap_gemv && !c->comm && p <= kYArg) {
+    if (c->overlap_gemv && p <= kYArg) {
       // U_j's GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM
-      // traffic) still running on the main stream; the dual SpMV waits for it.  Safe: every
+      // traffic; multi-GPU: its per-step all-reduces) still running on the main stream; the dual
+      // SpMV (multi-GPU: x_j's halo exchange before it) waits for it.  Safe: every
       // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
       // published U_{j-1}'s residual started, and the GEMV's inputs were written before that.
       if (c->overlap_gemv == 2) {
