@@ -97,6 +97,43 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "ring") {  // K2q + FX at other (data waves, pairs, ring) shapes
+    const int64_t npr = (n + 1) >> 1;
+    YArg ya;
+    for (int i = 0; i < kYArg; ++i) ya.v[i] = 0.01;
+    auto shape = [&](const char* name, auto kern, int DW, int PER) {
+      const int64_t span = int64_t(DW) * 64 * PER;
+      const int GD = static_cast<int>((npr + span - 1) / span);
+      if (GD > kChainMaxWG - 1) {
+        printf("%s: %d workgroups, too many\n", name, GD);
+        return;
+      }
+      for (int j : {5, 15, 29}) {
+        auto run = [&]() {
+          hipLaunchKernelGGL(kern, dim3(GD + 1), dim3(DW * 64 + 64), 0, s, n, w, Q, pitch, j, part, 1024, hcol_dev, gran,
+                             ep, err, (const double*)nullptr, 0, (double*)nullptr, (unsigned long long*)nullptr,
+                             (const unsigned long long*)nullptr, gsub, ya, j, x0, xo);
+        };
+        for (int r = 0; r < 3; ++r) run();
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int r = 0; r < reps; ++r) run();
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned he = 0;
+        CK(hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost));
+        printf("%-28s GD %3d j=%2d %7.1f us%s\n", name, GD, j, 1e3 * ms / reps, he ? "  CHAIN ERROR" : "");
+        if (he) return;
+      }
+    };
+    shape("DW8 PER4 NS5 (default)", mgs_chain_lag_kernel<8, 4, 5, 2, true, true>, 8, 4);
+    shape("DW7 PER5 NS5", mgs_chain_lag_kernel<7, 5, 5, 2, true, true>, 7, 5);
+    shape("DW7 PER5 NS6", mgs_chain_lag_kernel<7, 5, 6, 2, true, true>, 7, 5);
+    shape("DW6 PER6 NS6", mgs_chain_lag_kernel<6, 6, 6, 2, true, true>, 6, 6);
+    return 0;
+  }
   const char* names[] = {"K2p agg", "K2q", "K2q+gemv", "gemv"};
   for (int lag = 1; lag <= 2; ++lag)
   for (int nt = 0; nt < 2; ++nt)
