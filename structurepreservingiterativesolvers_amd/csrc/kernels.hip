@@ -3388,7 +3388,8 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
 template <int NS>
 __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabView T,
                                                                         const double* __restrict__ Ut,
-                                                                        double* __restrict__ partials, int np1) {
+                                                                        double* __restrict__ partials, int np1,
+                                                                        int chunk) {
   constexpr int NW = kBlock / 64;
   constexpr int NJ = NS / 16;  // table entries per lane and block
   constexpr int NA = 16;
@@ -3401,9 +3402,17 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
   // waves take the blocks round-robin over the whole table: blocks differ widely in cost (an
   // edge-row block of swe holds one segment, a rho-row block sixteen, with 4 MFMAs each), and
   // giving each XCD a contiguous eighth (K7m's schedule) measured 251 vs 141 us at C3
-  const int64_t wpg = static_cast<int64_t>(gridDim.x) * NW;
-  const int64_t gw = static_cast<int64_t>(blockIdx.x) * NW + wid;
-  const int64_t kb0 = 0;
+  // chunk > 0 (opt-in): XCD-local schedule.  Chunk q of `chunk` consecutive blocks belongs to XCD
+  // q mod 8 (blockIdx % 8); that XCD's waves take its chunks' blocks round-robin, so neighbouring
+  // rows' Ut gathers mostly meet in one L2 while every XCD still sees the whole field mix.
+  // The wave's i-th block is blk(L0 + i * wpg), increasing in i (gridDim.x is a multiple of 8).
+  const bool xl = chunk > 0;
+  const int64_t wpg = xl ? static_cast<int64_t>(gridDim.x >> 3) * NW : static_cast<int64_t>(gridDim.x) * NW;
+  const int64_t gw = xl ? static_cast<int64_t>(blockIdx.x >> 3) * NW + wid : static_cast<int64_t>(blockIdx.x) * NW + wid;
+  const int64_t xcd = blockIdx.x & 7;
+  auto blk = [&](int64_t L) -> int64_t {
+    return xl ? ((L / chunk) * 8 + xcd) * chunk + (L % chunk) : L;
+  };
   const int64_t kb1 = T.nblk;
   v4d_t acc00 = {0.0, 0.0, 0.0, 0.0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
   struct Ent {  // zero-initialised: a block past the range is never loaded, never undefined
@@ -3426,11 +3435,11 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
     acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, w0, acc10, 0, 0, 0);
     acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, w1, acc11, 0, 0, 0);
   };
-  int64_t kb = kb0 + gw;
+  int64_t L = gw;
   Ent cur, nxt;  // the table two blocks ahead is in flight: its wait never stalls a block
-  if (kb < kb1) load(kb, cur);
-  if (kb + wpg < kb1) load(kb + wpg, nxt);
-  for (; kb < kb1; kb += wpg) {
+  if (blk(L) < kb1) load(blk(L), cur);
+  if (blk(L + wpg) < kb1) load(blk(L + wpg), nxt);
+  for (; blk(L) < kb1; L += wpg) {
     const unsigned long long mk = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(cur.mask)) |
                                   (static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
                                        static_cast<unsigned>(cur.mask >> 32))) << 32);
@@ -3451,7 +3460,7 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
       }
     }
     Ent nx2;
-    if (kb + 2 * wpg < kb1) load(kb + 2 * wpg, nx2);  // in flight through this block and the next
+    if (blk(L + 2 * wpg) < kb1) load(blk(L + 2 * wpg), nx2);  // in flight through this block and the next
     double2 a = make_double2(0.0, 0.0);
     double w0 = 0.0, w1 = 0.0;
 #pragma unroll
@@ -3523,7 +3532,12 @@ hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double
   int grid = 0;
   if (T.ns != 16) return hipErrorInvalidValue;
   grid = sym_grid<16>();
-  hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1);
+  static const int chunk = [] {  // SPIS_K7T_CHUNK: blocks per XCD-local chunk (0: whole-table round robin)
+    const char* e = std::getenv("SPIS_K7T_CHUNK");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 0;
+  }();
+  hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int np2 = np1 * np1;
