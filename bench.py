@@ -44,11 +44,30 @@ def spmv_bytes(n_rows, nnz, col_bytes=4):
     return (8 + col_bytes) * nnz + 4 * (n_rows + 1) + 16 * n_rows
 
 
-def mgs_bytes(n, p, chain=True):
-    """Algorithmic bytes of one MGS chain over p basis vectors + normalise.  Persistent chain
-    (K2p): y and q_0 read once, each further q_i once, q_p written; per-step launches: per step
-    read y, q_i, q_{i+1}, write y; normalise reads y, writes q."""
-    return 8 * n * (p + 2) if chain else 32 * n * p + 16 * n
+def mgs_chain_bytes(n, k, chain):
+    """Mean algorithmic bytes of one sampled MGS chain (+ normalise) of a CGMRES(k) solve.  The
+    sampled iteration advances by one position per solve (spis.cpp ProfEv, prof_phase), so over
+    the timed solves every chain position j = 0 .. k-1 is sampled equally often; the byte count
+    is the mean over j of the kernel that runs there:
+      K2q (chain 3, (N+1)/2 <= 522,240 pairs): 8 N (j + 3) (w and q_0 .. q_j read, q_{j+1}
+          written) + 16 N for the update GEMV it carries from j >= 1 (x0 read, x_{j-1} written);
+      K2p (chain 1-2, N/2 <= 2^19): 8 N (j + 3);
+      K2b (chain >= 2 beyond): 16 N (j + 1) + 16 N (q_i and q_{i+1} streamed per MGS step, w
+          read once, q_{j+1} written);
+      per-step launches (chain 0): 32 N (j + 1) + 16 N (y, q_i, q_{i+1} read, y written; the
+          normalise reads y, writes q)."""
+    tot = 0.0
+    for j in range(k):
+        if chain == 3 and (n + 1) // 2 <= 255 * 512 * 4:
+            b = 8 * n * (j + 3) + (16 * n if j >= 1 else 0)
+        elif chain >= 1 and n // 2 <= 256 * 256 * 8 and not (chain >= 2 and n // 2 > 255 * 256 * 8):
+            b = 8 * n * (j + 3)
+        elif chain >= 2:
+            b = 16 * n * (j + 1) + 16 * n
+        else:
+            b = 32 * n * (j + 1) + 16 * n
+        tot += b
+    return tot / k
 
 
 def dual_bytes(n_rows, nnz, col_bytes=4):
@@ -77,6 +96,7 @@ def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
         blas_threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:  # pragma: no cover
         blas_threads = 1
+    cores = len(os.sched_getaffinity(0))  # the host cores this process may run on
     x0 = np.zeros_like(dic["b"])
     iters = 0
     solves = 0
@@ -91,10 +111,12 @@ def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
     return {
         "value": iters / dt,
         "unit": "iterations/s",
-        "cores": int(blas_threads),
+        "cores": int(cores),
+        "blas_threads": int(blas_threads),
         "kind": "port",
         "sample": f"{solves} full CGMRES({k}) solve(s) of the same N={len(x0)} system ({iters} iterations, "
-                  f"{dt:.1f} s); SciPy csr_matvec single-threaded, OpenBLAS {blas_threads} threads",
+                  f"{dt:.1f} s); SciPy csr_matvec single-threaded, OpenBLAS {blas_threads} threads on "
+                  f"{cores} affinity cores",
     }
 
 
@@ -112,7 +134,7 @@ def build_workload(args):
         desc = f"swe-shaped RT2xDG0 CSR (config {args.config.upper()}, M={M}), mass+energy constraints"
         if args.config == "c5":
             D, c3 = assembly.extra_constraint(len(x0), dic["z0"], seed=2)
-            conlist.append(ls._Constraint(D, None, c3))
+            conlist.append(ls._Constraint(D, np.zeros(len(x0)), c3))
             desc += " + synthetic third constraint (seed 2)"
         return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "desc": desc,
                 "cycles": args.cycles if args.config == "c5" else 1}
@@ -148,6 +170,7 @@ def main():
     ap.add_argument("--tol", type=float, default=1e-19)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true", help="skip the standalone cold-cache SpMV timing")
     ap.add_argument("--force-distributed", action="store_true",
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
@@ -253,10 +276,9 @@ def main():
     SD = dual_bytes(n, A.nnz, cb)
     dual_ms = ms[_lib.PROF_SPMV_DUAL] / max(cnt[_lib.PROF_SPMV_DUAL], 1)
     dual_gbs = SD / (dual_ms * 1e-3) / 1e9 if dual_ms > 0 else 0.0
-    sampled = [j + 1 for j in range(0, args.k, max(args.prof_period, 1))]
-    p_mean = float(np.mean(sampled))  # basis size of the sampled (timed) MGS chains
     mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
-    mgs_gbs = mgs_bytes(n, p_mean, n // 2 <= 256 * 256 * 8) / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 else 0.0
+    mgs_b = mgs_chain_bytes(n, args.k, args.chain if args.orthog == "mgs" else -1)
+    mgs_gbs = mgs_b / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 and args.orthog == "mgs" else None
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
     # the committed PMC summaries were measured on the C3 matrix: reported for that workload only
@@ -288,6 +310,22 @@ def main():
                 "frac": spmv_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": S,
                 "avg_launch_us": 1e3 * spmv_ms, "launches": int(cnt[_lib.PROF_SPMV])}
     roof["traffic"] = None if traffic is None else traffic.get("bytes_per_launch")
+    # the same launch standalone (spis_spmv_bench: the solver's table, walk and grid), back to back
+    # and behind a 1 GiB cache-evicting read, so the fraction is also quoted with the matrix and
+    # the vectors coming from HBM, not from the 256 MB Infinity Cache
+    if not args.no_cold:
+        kind = 1 if fused else 0
+        bytes_l = SD if fused else S
+        us = {}
+        for cold in (0, 1):
+            v = C.c_double()
+            _lib.check(L.spis_spmv_bench(ctx.handle, device_matrix(A, ctx=ctx).handle, kind, cold, 20, C.byref(v)),
+                       "spis_spmv_bench")
+            us[cold] = v.value
+        roof["standalone_warm_us"] = us[0]
+        roof["avg_launch_us_cold"] = us[1]
+        roof["achieved_cold"] = bytes_l / (us[1] * 1e-6) / 1e9
+        roof["frac_cold"] = roof["achieved_cold"] / HBM_PEAK_GBS
     out = {
         "metric": METRIC,
         "value": iters / elapsed,

@@ -112,6 +112,12 @@ enum spis_prof_kind {
 };
 int spis_profile_enable(spis_context* ctx, int32_t on);
 int spis_profile_read(spis_context* ctx, double ms_out[SPIS_PROF_KINDS], int64_t count_out[SPIS_PROF_KINDS]);
+/* Standalone timing of the solver's own SpMV launch (its table, walk and grid) for roofline
+ * reporting: kind 0 = the Arnoldi SpMV (w = A z + q0.w partials, solvers.py:191), 1 = the fused
+ * dual (||A x_j - b||^2 with A z_{j+2}, :290 + :191).  cold = 1 evicts L2 and the 256 MB Infinity
+ * Cache (a 1 GiB streaming read) before every launch; *us_out = mean launch time (us) over reps
+ * launches, from events carried by the launch itself.  Single GPU, square matrices. */
+int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t cold, int32_t reps, double* us_out);
 
 /* ---- options -------------------------------------------------------------------
  * SPIS_OPT_FUSE_SPMV (default 1): the true-residual SpMV of update j and the Arnoldi SpMV of

@@ -115,6 +115,7 @@ SIGNATURES = [
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),
+    ("spis_spmv_bench", C.c_int, [_VP, _VP, _I32, _I32, _I32, _PD]),
     ("spis_set_option", C.c_int, [_VP, _I32, _I64]),
     ("spis_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("spis_comm_init", C.c_int, [_VP, _I32, _I32, C.POINTER(C.c_uint8)]),

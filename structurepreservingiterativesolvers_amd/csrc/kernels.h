@@ -234,6 +234,8 @@ hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hi
                            const unsigned long long* seq = nullptr);
 hipError_t launch_axpy(int64_t n, double h, const double* x, double* y, hipStream_t s);
 hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
+// streaming read of n doubles (16-B aligned, n even): evicts L2 and the Infinity Cache
+hipError_t launch_stream_read(int64_t n, const double* x, double* sink, hipStream_t s);
 // send[i] = x[idx[i]]
 hipError_t launch_gather(int64_t m, const int32_t* idx, const double* x, double* send,
                          hipStream_t s);

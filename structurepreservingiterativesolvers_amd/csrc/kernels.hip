@@ -1769,7 +1769,9 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             double* gsub, const double* yx_host, int px, const double* x0, double* xo) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
-  if (aggregator && npair > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b (K2q falls back to it)
+  // K2q counts (n + 1) / 2 pairs (an odd n's last pair padded): its fallback test must too
+  const int64_t npk = gsub != nullptr ? (n + 1) >> 1 : npair;
+  if (aggregator && npk > (kChainMaxWG - 1) * int64_t(kBlock) * 8) {  // K2b (K2q falls back to it)
     if (px > 0) return hipErrorInvalidValue;  // the fused GEMV is K2q's only
     if (npair > kChainBigMaxPairs) return hipErrorInvalidValue;
     const int64_t wd = kChainMaxWG - 1;
@@ -2318,6 +2320,25 @@ hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s) {
   if (g > 4 * kRedGrid) g = 4 * kRedGrid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(kBlock), 0, s, n, x, y);
+  return hipGetLastError();
+}
+
+// cache eviction for cold-cache measurements (spis_spmv_bench): a streaming read of a buffer
+// larger than the 256 MB Infinity Cache, summed into one sink word so it is not dead code
+__global__ __launch_bounds__(kBlock) void stream_read_kernel(int64_t n2, const double2* __restrict__ x,
+                                                             double* __restrict__ sink) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  double acc = 0.0;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n2; e += stride) {
+    const double2 v = x[e];
+    acc += v.x + v.y;
+  }
+  if (acc == 1.2345678e300) sink[0] = acc;  // never true for the zero-filled buffer
+}
+
+hipError_t launch_stream_read(int64_t n, const double* x, double* sink, hipStream_t s) {
+  hipLaunchKernelGGL(stream_read_kernel, dim3(4096), dim3(kBlock), 0, s, n >> 1, reinterpret_cast<const double2*>(x),
+                     sink);
   return hipGetLastError();
 }
 

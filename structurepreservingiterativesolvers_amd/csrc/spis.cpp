@@ -777,6 +777,62 @@ extern "C" int spis_profile_read(spis_context* c, double ms_out[SPIS_PROF_KINDS]
   })
 }
 
+// Standalone timing of the solver's SpMV launches on the solver's own table and kernel choice
+// (dual_view, spmv_grid), for the bench's roofline: kind 0 = the Arnoldi SpMV (w = A z, q0.w
+// partials, solvers.py:191), kind 1 = the fused dual (||A x - b||^2 of x_j with A z of z_{j+2},
+// :290 + :191).  cold = 1: a 1 GiB streaming read before every timed launch evicts L2 and the
+// 256 MB Infinity Cache, so the matrix and the vectors come from HBM; cold = 0: back to back.
+// us_out = mean launch duration over reps (the launch's own start/stop events).
+extern "C" int spis_spmv_bench(spis_context* c, spis_matrix* A, int32_t kind, int32_t cold, int32_t reps,
+                               double* us_out) {
+  ABI_GUARD({
+    if (!c || !A || !us_out || reps < 1 || kind < 0 || kind > 1) return fail(SPIS_ERR_ARG, "bad argument");
+    if (A->ctx != c || A->n_rows != A->n_cols || c->comm) return fail(SPIS_ERR_ARG, "single-GPU square matrix only");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n = A->n_rows;
+    const int64_t pn = (n + 63) / 64 * 64;
+    const int64_t big = int64_t(1) << 27;  // 1 GiB of doubles
+    double* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, sizeof(double) * (5 * pn + 2 * kSpmvGrid + 8 + (cold ? big : 0))));
+    std::unique_ptr<double, void (*)(double*)> guard(buf, [](double* p) { (void)hipFree(p); });
+    double *x = buf, *z = buf + pn, *bb = buf + 2 * pn, *w = buf + 3 * pn, *q0 = buf + 4 * pn;
+    double *p1 = buf + 5 * pn, *p2 = p1 + kSpmvGrid, *sink = p2 + kSpmvGrid, *fl = sink + 8;
+    {
+      std::vector<double> h(static_cast<size_t>(pn));
+      for (int64_t i = 0; i < pn; ++i) h[i] = i < n ? 1e-3 * static_cast<double>((i * 104729) % 997) - 0.4 : 0.0;
+      for (double* d : {x, z, bb, q0}) HIP_TRY(hipMemcpy(d, h.data(), sizeof(double) * pn, hipMemcpyHostToDevice));
+    }
+    if (cold) HIP_TRY(hipMemsetAsync(fl, 0, sizeof(double) * big, c->stream));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    const CsrView v = A->dual_view();
+    const int g = spmv_grid(v, false);
+    double tot = 0.0;
+    int st = SPIS_OK;
+    for (int r = -2; r < reps && st == SPIS_OK; ++r) {
+      if (cold) {
+        hipError_t e = launch_stream_read(big, fl, sink, c->stream);
+        if (e != hipSuccess) { st = fail(SPIS_ERR_HIP, "flush: %s", hipGetErrorString(e)); break; }
+      }
+      const LaunchEv le{e0, e1};
+      const hipError_t e = kind == 0 ? launch_spmv(v, kEpiDot, z, w, q0, p2, g, c->stream, &le)
+                                     : launch_spmv_dual(v, x, bb, p1, z, w, q0, p2, g, c->stream, &le);
+      if (e != hipSuccess) { st = fail(SPIS_ERR_HIP, "spmv: %s", hipGetErrorString(e)); break; }
+      if (hipEventSynchronize(e1) != hipSuccess) { st = fail(SPIS_ERR_HIP, "event"); break; }
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) { st = fail(SPIS_ERR_HIP, "elapsed"); break; }
+      if (r >= 0) tot += ms;
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (st != SPIS_OK) return st;
+    *us_out = 1e3 * tot / reps;
+    return SPIS_OK;
+  })
+}
+
 // ------------------------------------------------------------------------------------------------
 // RCCL
 // ------------------------------------------------------------------------------------------------
@@ -2056,7 +2112,8 @@ struct Solver {
   // with its own y (stream order on the side stream); a stop at j-1 leaves x_j unused (x_j and
   // x_{j-1} live in separate buffers).  Results are identical to the unspeculated path.
   bool lag_chain() const {
-    return c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && (n >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8;
+    // K2q pads an odd n's last pair: its capacity test counts (n + 1) / 2 pairs, as the launch does
+    return c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8;
   }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
   void arm_hcol(int j) {  // before A_j's chain is enqueued
@@ -2122,7 +2179,9 @@ struct Solver {
     const LaunchEv e_last = pm.last();
     const bool agg = c->mgs_chain >= 2;
     // K2q (mode 3): the pipelined chain, while it fits K2p's register slices (K2b beyond)
-    double* gsub = c->mgs_chain == 3 ? c->chain_gsub : nullptr;
+    // (never under CGS2: its steps j + 1 <= kCgsMax write no Gram entries G(m, m-1), G(m, m-2), so a
+    // later K2q step would read stale ones; those steps take K2p with the aggregator instead)
+    double* gsub = (c->mgs_chain == 3 && !c->cgs2) ? c->chain_gsub : nullptr;
     // nontemporal basis loads when the matrix and the basis overflow the 256 MB Infinity Cache:
     // the chain then leaves the matrix resident for the next SpMV (C3: dual SpMV 49 -> 42 us,
     // chain +1-2 us, +2.9%; C4, whose working set fits, measured 1% slower with them)
