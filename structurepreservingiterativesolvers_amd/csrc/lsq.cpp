@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 
 #include "spis.h"
 
@@ -111,6 +112,17 @@ struct KKTState {
   std::vector<double> B, b0;            // grad f = B y - b0, B = 2 R'R, b0 = 2 R' g
   std::vector<std::vector<double>> S;   // T + T'
   std::vector<double> tau;              // target offsets (c_i(y) = -tau_i)
+  // scaled constraints (kkt_newton): values are the unscaled constraint's, as the reference's
+  // checker evaluates it, times 1 / scale, so their sign is exactly the checker's
+  const QuadCon* orig = nullptr;
+  std::vector<double> inv_s;
+  const double* R = nullptr;  // upper triangular p x p, column-major, leading dimension ld
+  const double* g = nullptr;
+  int ld = 0;
+
+  double cval(const QuadCon* cons, int i, const double* y) const {
+    return orig ? con_value(orig[i], p, y) * inv_s[i] : con_value(cons[i], p, y);
+  }
 
   void residual(const QuadCon* cons, const double* y, const double* lam, double* F,
                 std::vector<double>& J) const {
@@ -129,7 +141,7 @@ struct KKTState {
       for (int i = 0; i < m; ++i) t += J[static_cast<size_t>(i) * p + a] * lam[i];
       F[a] = t;
     }
-    for (int i = 0; i < m; ++i) F[p + i] = con_value(cons[i], p, y) + tau[i];
+    for (int i = 0; i < m; ++i) F[p + i] = cval(cons, i, y) + tau[i];
   }
 };
 
@@ -143,7 +155,7 @@ double norm2(const double* v, int n) {
 
 namespace {
 
-// Outcome of one Newton run on the KKT system.
+// Outcome of one SQP run on the KKT system.
 enum class Stop { kFloor, kSmallStep, kStall, kIterLimit, kSingular, kNonFinite };
 
 struct Run {
@@ -167,11 +179,135 @@ void grad_scale(const KKTState& st, const double* y, const double* lam, const do
   }
 }
 
-// Newton with a merit line search on ||F|| from (y, lam); both updated in place
-Run newton_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& lam, int max_iter) {
+// Positive definiteness of the reduced Hessian N'(W + delta I)N on the null space of the m x p
+// Jacobian (Jt: p x m, column i = grad c_i; both copied, they are transformed in place): the
+// Householder reflections of a QR of J' are applied to W from both sides (Q' W Q, 4 p^2 flops each;
+// the explicit null-space basis and the products N'(W N) would cost 2 p^3), whose trailing
+// (p - m) block is the reduced Hessian; Cholesky with a shift of shift_rel times its largest
+// diagonal entry.
+bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, double delta, double shift_rel) {
+  if (m >= p) return true;
+  for (int a = 0; a < p; ++a) W[static_cast<size_t>(a) * p + a] += delta;
+  std::vector<double> v(p), u(p);
+  for (int i = 0; i < m; ++i) {
+    double* col = Jt.data() + static_cast<size_t>(i) * p;
+    double nrm = 0.0;
+    for (int a = i; a < p; ++a) nrm += col[a] * col[a];
+    nrm = std::sqrt(nrm);
+    if (nrm == 0.0) continue;
+    const double alpha = col[i] > 0 ? -nrm : nrm;
+    std::fill(v.begin(), v.end(), 0.0);
+    for (int a = i; a < p; ++a) v[a] = col[a];
+    v[i] -= alpha;
+    double vv = 0.0;
+    for (int a = i; a < p; ++a) vv += v[a] * v[a];
+    if (vv == 0.0) continue;
+    const double s2 = 2.0 / vv;
+    for (int k = i; k < m; ++k) {  // the remaining columns of J'
+      double* x = Jt.data() + static_cast<size_t>(k) * p;
+      double t = 0.0;
+      for (int a = i; a < p; ++a) t += v[a] * x[a];
+      t *= s2;
+      for (int a = i; a < p; ++a) x[a] -= t * v[a];
+    }
+    // W <- H W H with H = I - s2 v v' (W symmetric up to rounding: both sides explicitly)
+    for (int a = 0; a < p; ++a) {  // W <- W H: row a -= s2 (W_a . v) v'
+      double* row = W.data() + static_cast<size_t>(a) * p;
+      double t = 0.0;
+      for (int b = i; b < p; ++b) t += row[b] * v[b];
+      t *= s2;
+      for (int b = i; b < p; ++b) row[b] -= t * v[b];
+    }
+    std::fill(u.begin(), u.end(), 0.0);  // W <- H W: W -= s2 v (v' W)
+    for (int a = i; a < p; ++a) {
+      const double va = v[a];
+      const double* row = W.data() + static_cast<size_t>(a) * p;
+      for (int b = 0; b < p; ++b) u[b] += va * row[b];
+    }
+    for (int a = i; a < p; ++a) {
+      double* row = W.data() + static_cast<size_t>(a) * p;
+      const double f = s2 * v[a];
+      for (int b = 0; b < p; ++b) row[b] -= f * u[b];
+    }
+  }
+  const int nz = p - m;
+  std::vector<double> Rm(static_cast<size_t>(nz) * nz);
+  double dmax = 0.0;
+  for (int c = 0; c < nz; ++c)
+    for (int d = 0; d < nz; ++d) {
+      const double t = W[static_cast<size_t>(m + c) * p + m + d];
+      Rm[static_cast<size_t>(c) * nz + d] = t;
+      if (c == d) dmax = std::max(dmax, std::fabs(t));
+    }
+  const double shift = shift_rel * dmax;
+  for (int c = 0; c < nz; ++c) {  // in-place Cholesky
+    double d = Rm[static_cast<size_t>(c) * nz + c] + shift;
+    for (int k = 0; k < c; ++k) d -= Rm[static_cast<size_t>(c) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    Rm[static_cast<size_t>(c) * nz + c] = d;
+    for (int r = c + 1; r < nz; ++r) {
+      double t = Rm[static_cast<size_t>(r) * nz + c];
+      for (int k = 0; k < c; ++k) t -= Rm[static_cast<size_t>(r) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
+      Rm[static_cast<size_t>(r) * nz + c] = t / d;
+    }
+  }
+  return true;
+}
+
+// Hessian of the Lagrangian B + sum lam_i S_i (p x p) and J' (p x m) at (y, lam); J (m x p) given
+void lagrangian_hessian(const KKTState& st, const double* lam, const std::vector<double>& J, std::vector<double>& W,
+                        std::vector<double>& Jt) {
+  const int p = st.p, m = st.m;
+  W.resize(static_cast<size_t>(p) * p);
+  Jt.resize(static_cast<size_t>(p) * m);
+  for (int a = 0; a < p; ++a)
+    for (int b = 0; b < p; ++b) {
+      double w = st.B[static_cast<size_t>(a) * p + b];
+      for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
+      W[static_cast<size_t>(a) * p + b] = w;
+    }
+  for (int i = 0; i < m; ++i)
+    for (int a = 0; a < p; ++a) Jt[static_cast<size_t>(i) * p + a] = J[static_cast<size_t>(i) * p + a];
+}
+
+// SQP on the KKT system from (y, lam), both updated in place.  Each iteration solves
+//   [W + delta I  J'] [d    ]   [-grad f    ]
+//   [J            0 ] [lam+ ] = [-(c + tau) ]
+// with W the Lagrangian Hessian and delta >= 0 the smallest shift (0, then 1e-12 .. 1e2 of W's
+// scale) that makes the reduced Hessian positive definite: with delta = 0 this is Newton's step
+// on the KKT conditions (quadratic convergence at a constrained minimum); with delta > 0 the
+// step descends the exact L1 merit f + mu sum |c_i + tau_i| (mu > max |lam+|, SLSQP's merit),
+// so a run is not attracted by constrained saddles and maxima of the indefinite energy
+// constraint, as Newton on ||F|| is (C5 restart cycle 8: ||F|| Newton from the warm start
+// converged to a saddle at f = 2.3e-2 where SLSQP finds the minimum, f = 7.0e-3).  Steps are
+// accepted on the merit, or, in the locally convex regime (delta = 0), on a decrease of ||F||
+// (the merit can reject full Newton steps near a solution: Maratos).  The constraints are
+// scaled to unit gradient at the start (kkt_newton), so mu is not set by a degenerate row.
+Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& lam, int max_iter) {
   const int p = st.p, m = st.m, n = p + m;
-  std::vector<double> J(static_cast<size_t>(m) * p), F(n), Fn(n), K, rhs(n), yn(p), ln(m);
+  std::vector<double> J(static_cast<size_t>(m) * p), F(n), Fn(n), K, rhs(n), yn(p), ln(m), W, Jt, gf(p);
   Run run;
+  double mu = 0.0;
+  double bscale = 0.0;
+  for (int a = 0; a < p; ++a) bscale = std::max(bscale, std::fabs(st.B[static_cast<size_t>(a) * p + a]));
+  if (!(bscale > 0.0)) bscale = 1.0;
+  // f - rho^2 = ||g - R v||^2 from the residual itself (1/2 v'Bv - b0'v cancels to roundoff of
+  // |b0| |v| near a solution whose f is ~1e-21, so merit comparisons would be noise)
+  auto fval = [&](const double* v) {
+    double t = 0.0;
+    for (int a = 0; a < p; ++a) {
+      double r = st.g[a];
+      for (int b = a; b < p; ++b) r -= st.R[static_cast<size_t>(b) * st.ld + a] * v[b];
+      t += r * r;
+    }
+    return t;
+  };
+  auto viol = [&](const double* v) {
+    double t = 0.0;
+    for (int i = 0; i < m; ++i) t += std::fabs(st.cval(cons, i, v) + st.tau[i]);
+    return t;
+  };
   int it = 0;
   for (; it < max_iter; ++it) {
     // offsets: a few ulps of each constraint's rounding scale, so that the COMPUTED value
@@ -182,39 +318,52 @@ Run newton_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>
     run.fn = fn;
     if (!std::isfinite(fn)) { run.stop = Stop::kNonFinite; break; }
     {  // converged at the rounding floor: the gradient part of F within 64 ulps of its terms'
-       // scale and every constraint at its target (c_i in [-2 tau_i, 0]).  Newton steps from
-       // here are noise; the line search would backtrack ~30 times per step (~60 us at p = 30)
+       // scale and every constraint at its target (c_i in [-2 tau_i, 0]).  Steps from here are
+       // noise; the line search would backtrack ~30 times per step (~60 us at p = 30)
       double gn, gs;
       grad_scale(st, y, lam.data(), F.data(), J, &gn, &gs);
       bool cons_ok = true;
       for (int i = 0; i < m; ++i) cons_ok = cons_ok && std::fabs(F[p + i]) <= st.tau[i];
       if (cons_ok && gn <= 64.0 * DBL_EPSILON * gs) { run.stop = Stop::kFloor; break; }
     }
+    for (int a = 0; a < p; ++a) {
+      double t = -st.b0[a];
+      for (int b = 0; b < p; ++b) t += st.B[static_cast<size_t>(a) * p + b] * y[b];
+      gf[a] = t;
+    }
+    lagrangian_hessian(st, lam.data(), J, W, Jt);
+    double delta = 0.0;
+    bool pd = reduced_pd(W, Jt, p, m, 0.0, 0.0);
+    for (int e = -12; !pd && e <= 2; e += 2) {
+      delta = bscale * std::pow(10.0, e);
+      pd = reduced_pd(W, Jt, p, m, delta, 0.0);
+    }
+    if (!pd) { run.stop = Stop::kSingular; break; }
     K.assign(static_cast<size_t>(n) * n, 0.0);
-    for (int a = 0; a < p; ++a)
-      for (int b = 0; b < p; ++b) {
-        double w = st.B[static_cast<size_t>(a) * p + b];
-        for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
-        K[static_cast<size_t>(a) * n + b] = w;
-      }
+    for (int a = 0; a < p; ++a) {
+      for (int b = 0; b < p; ++b) K[static_cast<size_t>(a) * n + b] = W[static_cast<size_t>(a) * p + b];
+      K[static_cast<size_t>(a) * n + a] += delta;
+    }
     for (int i = 0; i < m; ++i)
       for (int a = 0; a < p; ++a) {
         K[static_cast<size_t>(a) * n + p + i] = J[static_cast<size_t>(i) * p + a];
         K[static_cast<size_t>(p + i) * n + a] = J[static_cast<size_t>(i) * p + a];
       }
-    for (int r = 0; r < n; ++r) rhs[r] = -F[r];
+    for (int a = 0; a < p; ++a) rhs[a] = -gf[a];
+    for (int i = 0; i < m; ++i) rhs[p + i] = -F[p + i];
     if (!lu_solve(n, K, rhs.data())) { run.stop = Stop::kSingular; break; }
-    {  // a Newton step below the stopping size: take it unless it raises ||F||, and stop (no
-       // backtracking: at roundoff level the sufficient-decrease test cannot pass and would cost
-       // 40 residual evaluations)
+    const double* d = rhs.data();
+    const double* lp = rhs.data() + p;
+    {  // a step below the stopping size: take it unless it raises ||F||, and stop (no
+       // backtracking: at roundoff level no sufficient-decrease test can pass)
       double step = 0.0, ymax = 0.0;
       for (int a = 0; a < p; ++a) {
-        step = std::max(step, std::fabs(rhs[a]));
-        ymax = std::max(ymax, std::fabs(y[a] + rhs[a]));
+        step = std::max(step, std::fabs(d[a]));
+        ymax = std::max(ymax, std::fabs(y[a] + d[a]));
       }
       if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax)) {
-        for (int a = 0; a < p; ++a) yn[a] = y[a] + rhs[a];
-        for (int i = 0; i < m; ++i) ln[i] = lam[i] + rhs[p + i];
+        for (int a = 0; a < p; ++a) yn[a] = y[a] + d[a];
+        for (int i = 0; i < m; ++i) ln[i] = lp[i];
         st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
         const double fnew = norm2(Fn.data(), n);
         if (std::isfinite(fnew) && fnew <= fn) {
@@ -227,32 +376,47 @@ Run newton_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>
         break;
       }
     }
-    double alpha = 1.0;
-    double fnew = 0.0;
-    // up to 40 halvings (alpha >= 2^-39): far from the solution the merit function can need
-    // short steps; near it the rounding-floor test above ends the run before any halving
+    double lmax = 0.0;
+    for (int i = 0; i < m; ++i) lmax = std::max(lmax, std::fabs(lp[i]));
+    mu = std::max(mu, 2.0 * lmax);
+    const double v0 = viol(y);
+    const double phi0 = fval(y) + mu * v0;
+    double dd = 0.0;  // directional derivative of the merit along d (J d = -(c + tau))
+    for (int a = 0; a < p; ++a) dd += gf[a] * d[a];
+    dd -= mu * v0;
+    double alpha = 1.0, fnew = 0.0;
+    bool ok = false;
     for (int ls = 0; ls < 40; ++ls) {
-      for (int a = 0; a < p; ++a) yn[a] = y[a] + alpha * rhs[a];
-      for (int i = 0; i < m; ++i) ln[i] = lam[i] + alpha * rhs[p + i];
+      for (int a = 0; a < p; ++a) yn[a] = y[a] + alpha * d[a];
+      for (int i = 0; i < m; ++i) ln[i] = lam[i] + alpha * (lp[i] - lam[i]);
       st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
       fnew = norm2(Fn.data(), n);
-      if (std::isfinite(fnew) && fnew <= (1.0 - 1e-4 * alpha) * fn) break;
+      if (std::isfinite(fnew)) {
+        const double phin = fval(yn.data()) + mu * viol(yn.data());
+        if ((dd < 0.0 && phin <= phi0 + 1e-4 * alpha * dd) || (delta == 0.0 && fnew <= (1.0 - 1e-4 * alpha) * fn)) {
+          ok = true;
+          break;
+        }
+      }
       alpha *= 0.5;
     }
+    if (!ok) { run.stop = Stop::kStall; ++it; break; }
     double step = 0.0, ymax = 0.0;
     for (int a = 0; a < p; ++a) {
       step = std::max(step, std::fabs(yn[a] - y[a]));
       ymax = std::max(ymax, std::fabs(yn[a]));
+      y[a] = yn[a];
     }
-    if (std::isfinite(fnew) && fnew <= fn) {
-      for (int a = 0; a < p; ++a) y[a] = yn[a];
-      for (int i = 0; i < m; ++i) lam[i] = ln[i];
-      run.fn = fnew;
-    }
+    for (int i = 0; i < m; ++i) lam[i] = ln[i];
+    run.fn = fnew;
     if (step <= 4.0 * DBL_EPSILON * (1.0 + ymax)) { run.stop = Stop::kSmallStep; ++it; break; }
-    if (!(fnew < fn)) { run.stop = Stop::kStall; ++it; break; }
   }
   run.iterations = it;
+#ifdef SPIS_KKT_DEBUG
+  fprintf(stderr, "  sqp_run: stop=%d it=%d fn=%.3e mu=%.3e lam=", static_cast<int>(run.stop), it, run.fn, mu);
+  for (int i = 0; i < m; ++i) fprintf(stderr, "%.3e ", lam[i]);
+  fprintf(stderr, "\n");
+#endif
   return run;
 }
 
@@ -299,95 +463,16 @@ bool first_order_ok(KKTState& st, const QuadCon* cons, const double* y, std::vec
 }
 
 // Second-order test: the Hessian of the Lagrangian, B + sum lam_i S_i, positive definite on the
-// null space of J (a constrained minimum, not a saddle of the indefinite energy constraint).
-// The Householder reflections of a QR of J' are applied to W from both sides (Q' W Q, 4 p^2
-// flops each: the explicit null-space basis and the products N'(W N) cost 2 p^3, 60 of the
-// ~100 us of a p = 30 KKT solve), whose trailing (p - m) block is the reduced Hessian; Cholesky
-// with a shift of 1e-10 of its largest diagonal entry, so a semidefinite direction at roundoff
-// passes.
+// null space of J (a constrained minimum, not a saddle of the indefinite energy constraint);
+// Cholesky with a shift of 1e-10 of its largest diagonal entry, so a semidefinite direction at
+// roundoff passes.
 bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, const std::vector<double>& lam) {
   const int p = st.p, m = st.m;
   if (m >= p) return true;
-  std::vector<double> W(static_cast<size_t>(p) * p);
-  for (int a = 0; a < p; ++a)
-    for (int b = 0; b < p; ++b) {
-      double w = st.B[static_cast<size_t>(a) * p + b];
-      for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
-      W[static_cast<size_t>(a) * p + b] = w;
-    }
-  std::vector<double> Jt(static_cast<size_t>(p) * m);  // column i = grad c_i
-  for (int i = 0; i < m; ++i)
-    for (int a = 0; a < p; ++a) {
-      double t = cons[i].term1[a];
-      for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y[b];
-      Jt[static_cast<size_t>(i) * p + a] = t;
-    }
-  std::vector<double> v(p), u(p);
-  for (int i = 0; i < m; ++i) {
-    double* col = Jt.data() + static_cast<size_t>(i) * p;
-    double nrm = 0.0;
-    for (int a = i; a < p; ++a) nrm += col[a] * col[a];
-    nrm = std::sqrt(nrm);
-    if (nrm == 0.0) continue;
-    const double alpha = col[i] > 0 ? -nrm : nrm;
-    std::fill(v.begin(), v.end(), 0.0);
-    for (int a = i; a < p; ++a) v[a] = col[a];
-    v[i] -= alpha;
-    double vv = 0.0;
-    for (int a = i; a < p; ++a) vv += v[a] * v[a];
-    if (vv == 0.0) continue;
-    const double s2 = 2.0 / vv;
-    for (int k = i; k < m; ++k) {  // the remaining columns of J'
-      double* x = Jt.data() + static_cast<size_t>(k) * p;
-      double t = 0.0;
-      for (int a = i; a < p; ++a) t += v[a] * x[a];
-      t *= s2;
-      for (int a = i; a < p; ++a) x[a] -= t * v[a];
-    }
-    // W <- H W H with H = I - s2 v v' (W symmetric up to rounding: both sides explicitly)
-    for (int a = 0; a < p; ++a) {  // W <- W H: row a -= s2 (W_a . v) v'
-      double* row = W.data() + static_cast<size_t>(a) * p;
-      double t = 0.0;
-      for (int b = i; b < p; ++b) t += row[b] * v[b];
-      t *= s2;
-      for (int b = i; b < p; ++b) row[b] -= t * v[b];
-    }
-    std::fill(u.begin(), u.end(), 0.0);  // W <- H W: W -= s2 v (v' W)
-    for (int a = i; a < p; ++a) {
-      const double va = v[a];
-      const double* row = W.data() + static_cast<size_t>(a) * p;
-      for (int b = 0; b < p; ++b) u[b] += va * row[b];
-    }
-    for (int a = i; a < p; ++a) {
-      double* row = W.data() + static_cast<size_t>(a) * p;
-      const double f = s2 * v[a];
-      for (int b = 0; b < p; ++b) row[b] -= f * u[b];
-    }
-  }
-  // reduced Hessian: the trailing (p - m) x (p - m) block of Q' W Q
-  const int nz = p - m;
-  std::vector<double> Rm(static_cast<size_t>(nz) * nz);
-  double dmax = 0.0;
-  for (int c = 0; c < nz; ++c)
-    for (int d = 0; d < nz; ++d) {
-      const double t = W[static_cast<size_t>(m + c) * p + m + d];
-      Rm[static_cast<size_t>(c) * nz + d] = t;
-      if (c == d) dmax = std::max(dmax, std::fabs(t));
-    }
-  const double shift = 1e-10 * dmax;
-  for (int c = 0; c < nz; ++c) {  // in-place Cholesky
-    double d = Rm[static_cast<size_t>(c) * nz + c] + shift;
-    for (int k = 0; k < c; ++k) d -= Rm[static_cast<size_t>(c) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
-    if (!(d > 0.0)) return false;
-    d = std::sqrt(d);
-    Rm[static_cast<size_t>(c) * nz + c] = d;
-    for (int r = c + 1; r < nz; ++r) {
-      double t = Rm[static_cast<size_t>(r) * nz + c];
-      for (int k = 0; k < c; ++k) t -= Rm[static_cast<size_t>(r) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
-      Rm[static_cast<size_t>(r) * nz + c] = t / d;
-    }
-  }
-  return true;
+  std::vector<double> J(static_cast<size_t>(m) * p), F(p + m), W, Jt;
+  st.residual(cons, y, lam.data(), F.data(), J);
+  lagrangian_hessian(st, lam.data(), J, W, Jt);
+  return reduced_pd(W, Jt, p, m, 0.0, 1e-10);
 }
 
 }  // namespace
@@ -403,6 +488,9 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   KKTState st;
   st.p = p;
   st.m = m;
+  st.R = R;
+  st.g = g;
+  st.ld = ld;
   st.B.assign(static_cast<size_t>(p) * p, 0.0);
   st.b0.assign(p, 0.0);
   for (int a = 0; a < p; ++a) {
@@ -445,16 +533,6 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
     if (lu_solve(m, JJ, r.data()))
       for (int i = 0; i < m; ++i) lam[i] = r[i];
   };
-  // accepted: a run that reached the rounding floor, or stopped otherwise at a point that passes
-  // the first-order test; and in either case a constrained minimum (second-order test)
-  auto accept = [&](const Run& run, const double* yr, std::vector<double>& lam) {
-    if (run.stop == Stop::kSingular || run.stop == Stop::kNonFinite || run.stop == Stop::kIterLimit) return false;
-    for (int a = 0; a < p; ++a)
-      if (!std::isfinite(yr[a])) return false;
-    if (run.stop != Stop::kFloor && !first_order_ok(st, cons, yr, lam)) return false;
-    return second_order_ok(st, cons, yr, lam);
-  };
-
   // 0) SLSQP's first LSQ subproblem (LSEI) triangularises the constraint Jacobian at y0 by
   //    Householder reflections and stops with "Singular matrix C in LSQ subproblem" (mode 6,
   //    x = y0) when a diagonal element falls below machine epsilon (absolute, unscaled).  A
@@ -495,41 +573,83 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
     }
   }
 
-  // 1) warm start at the reference's y0 (solvers.py:225-227), as SLSQP
-  std::vector<double> lam;
-  init_lam(y, lam);
-  Run r1 = newton_run(st, cons, y, lam, max_iter);
-  res.iterations = r1.iterations;
-  if (accept(r1, y, lam)) return res;
+  // the constraints scaled to unit gradient at y0: an equality constraint's feasible set does not
+  // depend on its scale, but the merit's penalty weight does (the swe mass constraint's gradient
+  // is roundoff, |term1| ~ 1e-11, at a restart whose x0 already conserves mass: unscaled, its
+  // multiplier is ~1e9 and sets mu).  The signed checker and the tau targets are relative, so
+  // they carry over unchanged.
+  std::vector<QuadCon> sc(cons, cons + m);
+  st.orig = cons;
+  st.inv_s.assign(m, 1.0);
+  for (int i = 0; i < m; ++i) {
+    double nrm = 0.0;
+    for (int a = 0; a < p; ++a) {
+      double t = cons[i].term1[a];
+      for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y0[b];
+      nrm += t * t;
+    }
+    nrm = std::sqrt(nrm);
+    if (!(nrm > 0.0) || !std::isfinite(nrm)) continue;
+    const double f = 1.0 / nrm;
+    st.inv_s[i] = f;
+    sc[i].term0 *= f;
+    for (double& t : sc[i].term1) t *= f;
+    for (double& t : sc[i].term2) t *= f;
+    for (double& t : st.S[i]) t *= f;
+  }
+  const QuadCon* cs = sc.data();
+  auto run_from = [&](double* ys, std::vector<double>& lam) {
+    init_lam(ys, lam);
+    return sqp_run(st, cs, ys, lam, max_iter);
+  };
+  auto accept_s = [&](const Run& run, const double* yr, std::vector<double>& lam) {
+    if (run.stop == Stop::kSingular || run.stop == Stop::kNonFinite || run.stop == Stop::kIterLimit) return false;
+    for (int a = 0; a < p; ++a)
+      if (!std::isfinite(yr[a])) return false;
+    if (run.stop != Stop::kFloor && !first_order_ok(st, cs, yr, lam)) return false;
+    return second_order_ok(st, cs, yr, lam);
+  };
 
-  // 2) restart from the unconstrained minimiser (R y = g), the point SLSQP's first QP step
-  //    heads for
-  std::vector<double> y2(p), lam2;
+  // starts, the first verified constrained minimum wins: 1) the reference's warm start y0
+  // (solvers.py:225-227), as SLSQP; 2) the unconstrained minimiser (R y = g), the point SLSQP's
+  // first QP step heads for; 3) y = 0, i.e. x0 itself (feasible at a restart whose x0 satisfies
+  // the constraints)
+  std::vector<std::vector<double>> ys(3, std::vector<double>(p, 0.0));
+  for (int a = 0; a < p; ++a) ys[0][a] = y0[a];
   for (int i = p - 1; i >= 0; --i) {
     double t = g[i];
-    for (int k = i + 1; k < p; ++k) t -= R[static_cast<size_t>(k) * ld + i] * y2[k];
+    for (int k = i + 1; k < p; ++k) t -= R[static_cast<size_t>(k) * ld + i] * ys[1][k];
     const double d = R[static_cast<size_t>(i) * ld + i];
-    y2[i] = d != 0.0 ? t / d : 0.0;
+    ys[1][i] = d != 0.0 ? t / d : 0.0;
   }
-  init_lam(y2.data(), lam2);
-  Run r2 = newton_run(st, cons, y2.data(), lam2, max_iter);
-  res.iterations += r2.iterations;
-  if (accept(r2, y2.data(), lam2)) {
-    for (int a = 0; a < p; ++a) y[a] = y2[a];
-    return res;
+  bool y0_zero = true;
+  for (int a = 0; a < p; ++a) y0_zero = y0_zero && y0[a] == 0.0;
+  const int n_starts = y0_zero ? 2 : 3;
+  std::vector<Run> runs;
+  int best = -1;
+  for (int sidx = 0; sidx < n_starts; ++sidx) {
+    std::vector<double> lam;
+    runs.push_back(run_from(ys[sidx].data(), lam));
+    res.iterations += runs.back().iterations;
+    if (accept_s(runs.back(), ys[sidx].data(), lam)) {
+      for (int a = 0; a < p; ++a) y[a] = ys[sidx][a];
+      return res;
+    }
+    bool fin = runs.back().stop != Stop::kNonFinite;
+    for (int a = 0; a < p; ++a) fin = fin && std::isfinite(ys[sidx][a]);
+    if (fin && (best < 0 || runs.back().fn < runs[best].fn)) best = sidx;
   }
-  // neither start reached a verified constrained minimum: report it (the caller warns, as the
+  // no start reached a verified constrained minimum: report it (the caller warns, as the
   // reference does for a non-success SLSQP exit, :280-284) and keep the finite point with the
-  // smaller KKT residual
-  bool f1 = r1.stop != Stop::kNonFinite, f2 = r2.stop != Stop::kNonFinite;
-  for (int a = 0; a < p; ++a) {
-    f1 = f1 && std::isfinite(y[a]);
-    f2 = f2 && std::isfinite(y2[a]);
+  // smallest KKT residual
+  if (best >= 0) {
+    for (int a = 0; a < p; ++a) y[a] = ys[best][a];
+  } else {
+    res.finite = false;
   }
-  if (f2 && (!f1 || r2.fn < r1.fn))
-    for (int a = 0; a < p; ++a) y[a] = y2[a];
-  if (!f1 && !f2) res.finite = false;
-  res.message = (r1.stop == Stop::kSingular && r2.stop == Stop::kSingular) ? SPIS_MSG_SINGULAR_C : SPIS_MSG_ITER_LIMIT;
+  bool all_singular = true;
+  for (const Run& r : runs) all_singular = all_singular && r.stop == Stop::kSingular;
+  res.message = all_singular ? SPIS_MSG_SINGULAR_C : SPIS_MSG_ITER_LIMIT;
   return res;
 }
 

@@ -212,3 +212,63 @@ def test_kkt_singular_constraint_gradient_exits_as_slsqp(lsq):
     assert sol.message == "Singular matrix C in LSQ subproblem"
     np.testing.assert_array_equal(sol.x, y)
     assert max(f["fun"](y) for f in cl) > 1e-12  # the reference's checker then falls back
+
+
+@pytest.mark.parametrize("case", ["kkt_c5_cycle8", "kkt_c5_cycle9"])
+def test_kkt_c5_restart_cycles_match_slsqp(lsq, case):
+    """Config C5's forced constrained steps (swe M=913, mass + energy + the synthetic third
+    constraint, restarted CGMRES(30)) as the round-2 device solver received them (H, beta, warm
+    start and the three reduced constraints, tools/dump_c5_kkt.py): x0 already satisfies every
+    constraint (term0 = 0) and the mass constraint's gradient is roundoff (|term1| ~ 1e-12).  On
+    these inputs the reference's SLSQP (solvers.py:251-255) returns a feasible point (at its
+    iteration limit for cycle 8, so the branch is "con" with a RuntimeWarning), while Newton on
+    ||F|| from both of its starts converged to a constrained saddle (cycle 8: f = 2.3e-2 against
+    SLSQP's 7.0e-3) and the device fell back.  The SQP solve must find SLSQP's minimum."""
+    import os
+    from oracle.cgmres_port import _slsqp
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "kkt_cases", case + ".npz"))
+    H, beta, y0 = z["H"], float(z["beta"]), z["y0"]
+    k = H.shape[1]
+    terms = [(z["t0"][i], z["t1"][i], z["t2"][i]) for i in range(len(z["t0"]))]
+    res = np.zeros(k + 1)
+    res[0] = beta
+
+    def func(v):
+        return float(np.sum((res - H @ v) ** 2))
+
+    def jac(v):
+        return -2 * H.T @ (res - H @ v)
+
+    cl = [{"type": "eq", "fun": (lambda v, a=a, b=b, c=c: a + b @ v + v @ c @ v),
+           "jac": (lambda v, b=b, c=c: b + 2 * (v @ c))} for a, b, c in terms]
+    sol = _slsqp(func, y0, jac, cl, 1e-24)
+    assert max(f["fun"](sol.x) for f in cl) <= 1e-12  # the reference keeps its constrained step
+    y, msg, _ = kkt(lsq, H, beta, terms, y0)
+    assert msg == 0
+    for t0, t1, t2 in terms:  # the signed checker passes (solvers.py:267)
+        assert lsq.lsq_con_value(k, t0, _p(t1), _p(t2), _p(y)) <= 1e-12
+    assert func(y) <= func(sol.x) * (1 + 1e-12)
+    assert np.linalg.norm(y - sol.x) <= 1e-6 * np.linalg.norm(sol.x)
+
+
+def test_kkt_checker_sign_at_rounding_floor(lsq):
+    """swe M=30 CGMRES(25)'s forced constrained step as the device solver received it (SpMV mode
+    "off", tools/dump_pipe_modes_kkt.py): the warm start already sits at the rounding floor
+    (f ~ 1e-21), with the mass constraint's value +1.8e-12 as the reference's checker evaluates
+    it.  The solve must not stop there: the constraint values it tests are the unscaled ones, the
+    checker's (solvers.py:14-18,267), so the returned y passes the signed check."""
+    import os
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "kkt_cases", "kkt_swe_m30_final_step.npz"))
+    H, beta, y0 = z["H"], float(z["beta"]), z["y0"]
+    k = H.shape[1]
+    terms = [(z["t0"][i], z["t1"][i], z["t2"][i]) for i in range(len(z["t0"]))]
+    assert max(lsq.lsq_con_value(k, a, _p(b), _p(c), _p(y0)) for a, b, c in terms) > 1e-12
+    y, msg, _ = kkt(lsq, H, beta, terms, y0)
+    assert msg == 0
+    for t0, t1, t2 in terms:
+        assert lsq.lsq_con_value(k, t0, _p(t1), _p(t2), _p(y)) <= 0.0
+    res = np.zeros(k + 1)
+    res[0] = beta
+    assert np.sum((res - H @ y) ** 2) <= 1e-20 * beta ** 2
