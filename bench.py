@@ -13,11 +13,13 @@ before the timed region.
   c5  swe M=913, N=10,002,828, 3 constraints (+ the synthetic third), restarted CGMRES(30),
       one step = one restarted solve of --cycles cycles (default 10)
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): one global solve of
-N x 1,002,252 DoF row-partitioned over the N ranks (weak scaling), RCCL
-all-reduce for every dot/norm, halo exchange before every SpMV.  ``value`` =
-iterations x N / time (Mdof-normalised iterations per second of the whole
-job), max time over ranks.
+Multi-GPU (``--gpus N`` under torch.distributed.run, distributed.dist_workload): one global
+solve row-partitioned over the N ranks (field-interleaved blocks), RCCL all-reduces (two per
+Arnoldi step: MGS's projections in one, the norm in the other) and a halo exchange before every
+SpMV.  c3 (default): N x 1,002,252 DoF (weak scaling), ``value`` = iterations x N / time (the
+whole job's Mdof-normalised iterations per second), max time over ranks; c4: the C4 lkdvRK GL(3)
+problem (N = 300,006) row-split (strong scaling); c5: the C5 swe problem (strong); c2: lkdv with
+~1e5 DoF per GPU (weak).
 
 Prints ONE JSON line on rank 0.
 """
@@ -173,6 +175,9 @@ def main():
     ap.add_argument("--no-cold", action="store_true", help="skip the standalone cold-cache SpMV timing")
     ap.add_argument("--force-distributed", action="store_true",
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
+    ap.add_argument("--dist-mgs", type=int, default=1, choices=[0, 1],
+                    help="several GPUs (SPIS_OPT_DIST_MGS): 1 MGS's projections in one all-reduce per Arnoldi "
+                         "step, 0 one all-reduce per projection")
     ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
     ap.add_argument("--no-overlap", action="store_true", help="update GEMV on the main stream (no side stream)")

@@ -176,7 +176,13 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  *   columns (csrc/col16.h: a 2-bit base index + 14-bit offset per nonzero, 4 base columns per
  *   block): 10 instead of 12 bytes per nonzero.  1 = when val/col exceed the 256 MB Infinity
  *   Cache (C5: dual 470 vs 494 us; a cache-resident C3 matrix is faster on 32-bit columns,
- *   37.6 vs 39.5 us), 2 = always, 0 = never.  Rows bit-identical. */
+ *   37.6 vs 39.5 us), 2 = always, 0 = never.  Rows bit-identical.
+ * SPIS_OPT_DIST_MGS (default 1): several GPUs (after spis_comm_init), Arnoldi steps with at most
+ *   32 basis vectors: MGS's projections in inverse-compact-WY form, h_l = q_l.w - sum_{m<l} h_m
+ *   q_l.q_m, from one pass and one all-reduce (every q_l.w and the newest Gram row), then the
+ *   update with ||w'||^2 and a second all-reduce: 2 all-reduces per Arnoldi step instead of
+ *   MGS's j + 2.  MGS in exact arithmetic (the pipelined single-GPU chain's correction terms with
+ *   an unbounded lag); roundoff differs.  0 = one MGS step launch and all-reduce per projection. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -188,7 +194,8 @@ enum spis_option {
   SPIS_OPT_SPMV_PIPE = 8,
   SPIS_OPT_EARLY_CON = 9,
   SPIS_OPT_NT_BASIS = 10,
-  SPIS_OPT_COL16 = 11
+  SPIS_OPT_COL16 = 11,
+  SPIS_OPT_DIST_MGS = 12
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -145,6 +145,14 @@ hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t p
                           hipStream_t s, const LaunchEv* ev = nullptr);
 hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
                              bool dot, double* part, int grid, hipStream_t s);
+// K2w (multi-GPU MGS, one reduction for the projections): partials of q_l . w (l < nv) and of
+// q_l . q_{nv-1} (l < nv - 1) -> part rows [0, nv) and [nv, 2 nv - 1), grid columns each
+hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
+                           hipStream_t s, const LaunchEv* ev = nullptr);
+// one workgroup: those dots, Gram row nv - 1 into G (kCgsMax x kCgsMax), h_l = q_l . w -
+// sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
+hipError_t launch_icwy_coef(const double* part, int n_in, int nv, double* G, double* coef, double* h_out,
+                            hipStream_t s);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
@@ -237,6 +245,9 @@ hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
 // streaming read of n doubles (16-B aligned, n even): evicts L2 and the Infinity Cache
 hipError_t launch_stream_read(int64_t n, const double* x, double* sink, hipStream_t s);
 // send[i] = x[idx[i]]
+// send row i = src row idx[i] (row-major, cols doubles per row), i < m
+hipError_t launch_gather_rows(int64_t m, int cols, const int32_t* idx, const double* src, double* send,
+                              hipStream_t s);
 hipError_t launch_gather(int64_t m, const int32_t* idx, const double* x, double* send,
                          hipStream_t s);
 // G_partial[block][a*nv+b] over the block's chunks; then reduced into G

@@ -2119,6 +2119,128 @@ hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// K2w: one-reduce MGS for several GPUs (MGS in its inverse-compact-WY form).  MGS's projections
+// h_l = q_l . w^(l), w^(l+1) = w^(l) - h_l q_l are, by the distributive law K2q uses with a lag
+// of 2, h_l = q_l . w - sum_{m<l} h_m G(l, m) with G(l, m) = q_l . q_m: one pass computes every
+// q_l . w and the newest Gram row G(j, .) (q_j arrived with the previous step), ONE all-reduce
+// carries them, one workgroup forms h in l order (the same correction order as K2q's gatherer),
+// then cgs_update subtracts Q h with the ||w'||^2 partials (the second all-reduce) and K3
+// normalises.  Two reductions per Arnoldi step instead of MGS's j + 2; exact arithmetic is MGS's.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const double* __restrict__ w,
+                                                          const double* __restrict__ Q, int64_t pitch, int nv,
+                                                          double* __restrict__ part) {
+  // rows [0, nv): q_l . w ; rows [nv, 2 nv - 1): q_l . q_{nv-1}, l < nv - 1
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double acc[kCgsPerWave], acg[kCgsPerWave];
+#pragma unroll
+  for (int m = 0; m < kCgsPerWave; ++m) acc[m] = acg[m] = 0.0;
+  const double* Qw = Q + wid * pitch;
+  const double* ql = Q + static_cast<int64_t>(nv - 1) * pitch;
+  const int64_t step = 4 * pitch;
+  const bool vec = aligned16d(w) && aligned16d(Q) && (pitch % 2 == 0);
+  const int64_t n_vec = vec ? (n / kCgsChunk) * kCgsChunk : 0;
+  for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kCgsChunk; e0 < n_vec;
+       e0 += static_cast<int64_t>(gridDim.x) * kCgsChunk) {
+    const int64_t e = e0 + 2 * lane;
+    const double2 wa = *reinterpret_cast<const double2*>(w + e);
+    const double2 wb = *reinterpret_cast<const double2*>(w + e + 128);
+    const double2 la = *reinterpret_cast<const double2*>(ql + e);
+    const double2 lb = *reinterpret_cast<const double2*>(ql + e + 128);
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nv) {
+        const double* qv = Qw + m * step;
+        const double2 qa = *reinterpret_cast<const double2*>(qv + e);
+        const double2 qb = *reinterpret_cast<const double2*>(qv + e + 128);
+        acc[m] += qa.x * wa.x;
+        acc[m] += qa.y * wa.y;
+        acc[m] += qb.x * wb.x;
+        acc[m] += qb.y * wb.y;
+        if (i < nv - 1) {
+          acg[m] += qa.x * la.x;
+          acg[m] += qa.y * la.y;
+          acg[m] += qb.x * lb.x;
+          acg[m] += qb.y * lb.y;
+        }
+      }
+    }
+  }
+  for (int64_t e = n_vec + static_cast<int64_t>(blockIdx.x) * 64 + lane; e < n;
+       e += static_cast<int64_t>(gridDim.x) * 64) {
+    const double we = w[e];
+    const double le = ql[e];
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nv) {
+        const double q = Qw[m * step + e];
+        acc[m] += q * we;
+        if (i < nv - 1) acg[m] += q * le;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < kCgsPerWave; ++m) {
+    const int i = wid + 4 * m;
+    if (i < nv) {
+      const double t = wave_sum(acc[m]);
+      if (lane == 0) part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] = t;
+    }
+    if (i < nv - 1) {
+      const double t = wave_sum(acg[m]);
+      if (lane == 0) part[static_cast<int64_t>(nv + i) * gridDim.x + blockIdx.x] = t;
+    }
+  }
+}
+
+// one workgroup: the 2 nv - 1 dots from their (all-reduced) partials in sum_partials' fixed
+// order, the newest Gram row into G (row-major kCgsMax x kCgsMax, rows < nv - 1 written by the
+// earlier steps of this solve), then h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l
+// order -> coef (device, cgs_update's input) and h_out (the host H column)
+__global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restrict__ part, int n_in, int nv,
+                                                           double* __restrict__ G, double* __restrict__ coef,
+                                                           double* __restrict__ h_out) {
+#pragma clang fp contract(off)
+  __shared__ double s_wave[4];
+  __shared__ double s_d[2 * kCgsMax];
+  for (int r = 0; r < 2 * nv - 1; ++r) {
+    const double t = sum_partials(part + static_cast<int64_t>(r) * n_in, n_in, s_wave);
+    if (threadIdx.x == 0) s_d[r] = t;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* grow = G + static_cast<int64_t>(nv - 1) * kCgsMax;
+    for (int l = 0; l < nv - 1; ++l) grow[l] = s_d[nv + l];
+    double h[kCgsMax];
+    for (int l = 0; l < nv; ++l) {
+      double t = s_d[l];
+      const double* gl = l == nv - 1 ? grow : G + static_cast<int64_t>(l) * kCgsMax;
+      for (int m = 0; m < l; ++m) t -= h[m] * (l == nv - 1 ? s_d[nv + m] : gl[m]);
+      h[l] = t;
+      coef[l] = t;
+      h_out[l] = t;
+    }
+  }
+}
+
+hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
+                           hipStream_t s, const LaunchEv* ev) {
+  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
+  launch_k(icwy_dot_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_icwy_coef(const double* part, int n_in, int nv, double* G, double* coef, double* h_out,
+                            hipStream_t s) {
+  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(icwy_coef_kernel, dim3(1), dim3(kBlock), 0, s, part, n_in, nv, G, coef, h_out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // K4: x = Z[:, :p] y + x0 (solvers.py:287).  For p <= kYArg the coefficients travel in the
 // kernel-argument segment (scalar loads, no H2D copy in front of the launch); otherwise they
 // are copied to LDS from a device buffer.  Each lane streams one (VEC: two) element(s) of every
@@ -2348,6 +2470,29 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(int64_t m, const int32_t
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < m; e += stride)
     send[e] = x[idx[e]];
+}
+
+// rows idx[i] of a row-major (., cols) array -> row i of send (the Ut halo of a constraint
+// reduction on several GPUs): one thread per double
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(int64_t m, int cols, const int32_t* __restrict__ idx,
+                                                             const double* __restrict__ src,
+                                                             double* __restrict__ send) {
+  const int64_t total = m * cols;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < total; e += stride) {
+    const int64_t r = e / cols;
+    const int c = static_cast<int>(e - r * cols);
+    send[e] = src[static_cast<int64_t>(idx[r]) * cols + c];
+  }
+}
+
+hipError_t launch_gather_rows(int64_t m, int cols, const int32_t* idx, const double* src, double* send,
+                              hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  int64_t g = (m * cols + kBlock - 1) / kBlock;
+  if (g > 4 * kRedGrid) g = 4 * kRedGrid;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(g), dim3(kBlock), 0, s, m, cols, idx, src, send);
+  return hipGetLastError();
 }
 
 hipError_t launch_gather(int64_t m, const int32_t* idx, const double* x, double* send,

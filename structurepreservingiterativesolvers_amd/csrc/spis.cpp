@@ -126,6 +126,14 @@ struct spis_context {
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
   double* cgs_c = nullptr;          // c1 [kCgsMax] | c2 [kCgsMax]
+  // several GPUs (SPIS_OPT_DIST_MGS): 1 = MGS's projections in one reduction per Arnoldi step
+  // (K2w, icwy_*), 0 = one MGS step launch + all-reduce per projection
+  int dist_mgs = 1;
+  double* icwy_part = nullptr;      // 2 kCgsMax x kRedGrid partials
+  double* icwy_d = nullptr;         // the 2 nv - 1 reduced dots (+ the norm slot)
+  double* icwy_G = nullptr;         // kCgsMax x kCgsMax Gram rows G(l, m) = q_l . q_m, m < l
+  double* ut_send = nullptr;        // several GPUs: the Ut rows a constraint matrix's halo sends
+  size_t ut_send_len = 0;
   int ell_gram = 3;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy, 3 K7t / K7m, 4 K7m (SPIS_OPT_ELL_GRAM)
   int mgs_chain = 3;                // persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 K2p gathered by workgroup 0, 2 by a dedicated workgroup, 3 K2q pipelined
   int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
@@ -244,6 +252,7 @@ struct spis_workspace {
   double* ydev = nullptr;
   double* Ut = nullptr;  // transposed [Z, x0] for the fused constraint reduction (n x (p+1))
   int Ut_cols = 0;       // its allocated row capacity (32 or 64)
+  int64_t Ut_rows = 0;   // its allocated rows (n, plus a constraint matrix's ghost rows on several GPUs)
   int32_t ext_len = 0;
   std::vector<ConCache> con;
   std::vector<double> y_all;  // k*k host copy of every iteration's y
@@ -460,6 +469,38 @@ static int exchange(spis_context* c, const spis_matrix* M, double* x) {
   return SPIS_OK;
 }
 
+static int allreduce_on(spis_context* c, double* buf, int64_t count, hipStream_t st) {
+  if (!c->comm || count <= 0) return SPIS_OK;
+  NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, st));
+  return SPIS_OK;
+}
+
+// several GPUs: the ghost rows of a row-major (n_rows + n_ghost, cols) array (Ut of a constraint
+// reduction) from their owners, through M's halo plan (one grouped send/recv of whole rows)
+static int exchange_rows(spis_context* c, const spis_matrix* M, double* U, int cols, hipStream_t st) {
+  if (!c->comm || M->nbr.empty()) return SPIS_OK;
+  const size_t need = static_cast<size_t>(std::max<int64_t>(M->n_send, 1)) * cols;
+  if (c->ut_send_len < need) {
+    if (c->ut_send) HIP_TRY(hipFree(c->ut_send));
+    c->ut_send = nullptr;
+    c->ut_send_len = 0;
+    HIP_TRY(hipMalloc(&c->ut_send, sizeof(double) * need));
+    c->ut_send_len = need;
+  }
+  HIP_TRY(launch_gather_rows(M->n_send, cols, M->send_idx, U, c->ut_send, st));
+  NCCL_TRY(ncclGroupStart());
+  for (size_t i = 0; i < M->nbr.size(); ++i) {
+    if (M->scnt[i] > 0)
+      NCCL_TRY(ncclSend(c->ut_send + static_cast<size_t>(M->soff[i]) * cols, static_cast<size_t>(M->scnt[i]) * cols,
+                        ncclDouble, M->nbr[i], c->comm, st));
+    if (M->rcnt[i] > 0)
+      NCCL_TRY(ncclRecv(U + static_cast<size_t>(M->n_rows + M->roff[i]) * cols, static_cast<size_t>(M->rcnt[i]) * cols,
+                        ncclDouble, M->nbr[i], c->comm, st));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return SPIS_OK;
+}
+
 static int ensure_pinned(spis_context* c, size_t len) {
   if (c->pinned_len >= len) return SPIS_OK;
   if (c->pinned) {
@@ -584,6 +625,10 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
+    HIP_TRY(hipMalloc(&c->icwy_part, sizeof(double) * 2 * kCgsMax * kRedGrid));
+    HIP_TRY(hipMalloc(&c->icwy_d, sizeof(double) * (2 * kCgsMax + 8)));
+    HIP_TRY(hipMalloc(&c->icwy_G, sizeof(double) * kCgsMax * kCgsMax));
+    HIP_TRY(hipMemset(c->icwy_G, 0, sizeof(double) * kCgsMax * kCgsMax));
     HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * kChainGranLag));
     HIP_TRY(hipMemset(c->chain_gran, 0, sizeof(unsigned long long) * kChainGranLag));
     HIP_TRY(hipMalloc(&c->chain_gsub, sizeof(double) * kChainGsub));
@@ -654,6 +699,10 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->dscal);
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
+    (void)hipFree(c->icwy_part);
+    (void)hipFree(c->icwy_d);
+    (void)hipFree(c->icwy_G);
+    (void)hipFree(c->ut_send);
     (void)hipFree(c->chain_gran);
     (void)hipFree(c->chain_gsub);
     (void)hipFree(c->gemv_flag);
@@ -740,6 +789,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
+        return SPIS_OK;
+      case SPIS_OPT_DIST_MGS:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "dist_mgs %lld: 0 or 1", (long long)value);
+        c->dist_mgs = static_cast<int>(value);
         return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }
@@ -1706,13 +1759,19 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
                             int p, const double* Z, int64_t pitch, const double* x0, hipStream_t st, double* dst) {
   const int np1 = p + 1;
   const int ut_cols = np1 <= 32 ? 32 : 64;  // Ut is N x np1 row-major: size for this p bucket
-  if (ws->Ut && ws->Ut_cols < ut_cols) {
+  // several GPUs: a constraint matrix's ghost columns read the Ut rows of their owners, received
+  // after the local rows (exchange_rows, per matrix: each has its own halo plan)
+  int64_t ut_rows = std::max<int64_t>(n, 1);
+  for (int ci = 0; ci < m; ++ci)
+    if (c->comm && cons[ci].M != nullptr) ut_rows = std::max<int64_t>(ut_rows, n + cons[ci].M->n_ghost);
+  if (ws->Ut && (ws->Ut_cols < ut_cols || ws->Ut_rows < ut_rows)) {
     HIP_TRY(hipFree(ws->Ut));
     ws->Ut = nullptr;
   }
   if (!ws->Ut) {
-    HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * std::max<int64_t>(n, 1) * ut_cols));
+    HIP_TRY(hipMalloc(&ws->Ut, sizeof(double) * ut_rows * ut_cols));
     ws->Ut_cols = ut_cols;
+    ws->Ut_rows = ut_rows;
   }
   const size_t need = static_cast<size_t>(constraint_gram_partials()) * (np1 * np1 + 4 * np1);
   if (c->cg_part_len < need) {
@@ -1735,7 +1794,8 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   // 4: K7m for every matrix.  Both read Ut in the MFMA column order.
   const int eg = c->ell_gram;
   const bool mfma = np1 <= 32 && eg >= 3;
-  const bool tsym = mfma && eg == 3;
+  // K7t's symmetric pairing needs both (r, c) and (c, r) in one rank's rows: single GPU only
+  const bool tsym = mfma && eg == 3 && !c->comm;
   std::vector<Launch> plan;
   for (int ci = 0; ci < m; ++ci) {
     if (cons[ci].M == nullptr || cons[ci].M->all_zero) continue;
@@ -1763,6 +1823,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     const CsrView mv = cons[L.ci].M->view();
     const int nvv = v_done ? 0 : nv;
     spis_matrix* Mc = cons[L.ci].M;
+    if (c->comm) ST_TRY(exchange_rows(c, Mc, ws->Ut, ut_cols, st));
     if (L.sym) {
       HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, c->cg_G, st));
     } else if (mfma) {
@@ -1774,6 +1835,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
       HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st,
                                      L.ell ? &L.ev : nullptr));
     }
+    ST_TRY(allreduce_on(c, c->cg_G, static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1, st));
     HIP_TRY(hipMemcpyAsync(dst + static_cast<size_t>(L.ci) * np1 * np1, c->cg_G, sizeof(double) * np1 * np1,
                            hipMemcpyDeviceToHost, st));
     if (nvv > 0)
@@ -1786,6 +1848,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
                                           c->cg_G, st));
     else
       HIP_TRY(launch_constraint_gram(n, np1, nullptr, ws->Ut, nv, vlist.data(), c->cg_part, c->cg_G, st));
+    ST_TRY(allreduce_on(c, c->cg_G + np1 * np1, static_cast<int64_t>(nv) * np1, st));
     HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + np1 * np1, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
   }
   return SPIS_OK;
@@ -1830,7 +1893,9 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
 static bool fused_con_ok(const spis_context* c, int p, int m, const spis_constraint_desc* cons) {
   int nlin = 0;
   for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
-  return !c->comm && p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram;
+  // several GPUs: K7m on the local rows, the ghost Ut rows exchanged per matrix, G all-reduced
+  if (c->comm && !(p + 1 <= 32 && c->ell_gram >= 3)) return false;
+  return p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram;
 }
 
 static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
@@ -2170,6 +2235,7 @@ struct Solver {
                    unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr,
                    const double* yx = nullptr, int jx = -1) {
     if (c->cgs2 && j + 1 <= kCgsMax) return arnoldi_post_cgs2(j, xpart, x_out, flag, seq);
+    if (c->comm && c->dist_mgs == 1 && j + 1 <= kCgsMax) return arnoldi_post_icwy(j, xpart, x_out, flag, seq);
     hipStream_t s = c->stream;
     c->prof_iter = j;
     ST_TRY(allreduce(c, c->partA, gs));
@@ -2212,6 +2278,35 @@ struct Solver {
       n_in = gb;
     }
     HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), src, n_in, hcol + j + 1, s, gb, &e_last));
+    return SPIS_OK;
+  }
+
+  // several GPUs, MGS (K2w, kernels.hip): the projections h_l = q_l . w - sum_{m<l} h_m G(l, m)
+  // from one pass and one all-reduce (every q_l . w and the newest Gram row), then w -= Q h with
+  // the ||w'||^2 partials (the second all-reduce) and the normalise.  Each rank reduces its own
+  // partials in a fixed order first, so each all-reduce carries 2 j + 1 doubles (resp. one): the
+  // latency of a few bytes, not of a kRedGrid-long partial array per dot.
+  int arnoldi_post_icwy(int j, const double* xpart, double* x_out, unsigned long long* flag,
+                        const unsigned long long* seq) {
+    hipStream_t s = c->stream;
+    c->prof_iter = j;
+    if (xpart) HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
+    const int nv = j + 1;
+    double* hcol = c->pinned_dev + hoff(j);
+    const int gc = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 63) / 64)));
+    ProfEv pm(c, SPIS_PROF_MGS);
+    const LaunchEv e_first = pm.first(), e_last = pm.last();
+    double* d = c->icwy_d;
+    double* coef = c->cgs_c;
+    HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first));
+    HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
+    ST_TRY(allreduce(c, d, 2 * nv - 1));
+    HIP_TRY(launch_icwy_coef(d, 1, nv, c->icwy_G, coef, hcol, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s));
+    double* nrm = d + 2 * kCgsMax;
+    HIP_TRY(launch_cgs_finalize(c->partB, gc, 1, nrm, nullptr, nullptr, s));
+    ST_TRY(allreduce(c, nrm, 1));
+    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), nrm, 1, hcol + j + 1, s, gb, &e_last));
     return SPIS_OK;
   }
 
@@ -2280,7 +2375,7 @@ struct Solver {
     ++c->gemv_seq;
     HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
     HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
-    return SPIS_OK;
+    return exchange(c, A, xbuf(j));  // (single GPU in L mode: a no-op)
   }
   // U_j's residual partials (from [U_j res | a_{j+2}]) reduced and published without a chain
   int enqueue_finalize(int j) {
@@ -2321,7 +2416,11 @@ struct Solver {
         HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, xbuf(j), s, &le));
       }
     }
-    return exchange(c, A, xbuf(j));
+    // x_j's halo: on the main stream, ordered after the GEMV.  A side-stream GEMV's caller runs
+    // it after the main stream's wait for the GEMV (RCCL calls stay on the main stream: one
+    // order of collectives on every rank); issuing it here, before that wait, sent ghosts of the
+    // buffer's previous contents (round 2: iterate 1's residual read ||b||)
+    return s_gemv ? SPIS_OK : exchange(c, A, xbuf(j));
   }
 
   // U_j's true-residual partials go to device memory (partR).  Single GPU: one workgroup reduces
@@ -2411,6 +2510,7 @@ struct Solver {
         hipEvent_t done = nullptr;
         ST_TRY(update_gemv(j, p, y, c->stream2, &done));
         HIP_TRY(hipStreamWaitEvent(c->stream, done, 0));
+        ST_TRY(exchange(c, A, xbuf(j)));
       } else {
         ST_TRY(update_gemv(j, p, y, c->stream2));
         // cross-stream order through a stream memory write / wait on a device word (~1.5% faster
@@ -2418,6 +2518,7 @@ struct Solver {
         ++c->gemv_seq;
         HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
         HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
+        ST_TRY(exchange(c, A, xbuf(j)));
       }
     } else {
       ST_TRY(update_gemv(j, p, y));

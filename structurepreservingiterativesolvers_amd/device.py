@@ -60,6 +60,7 @@ _OPTIONS = {
     "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
                                         "sell": 6, "xcd_natural": 7}),
     "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
+    "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
 }
 
 

@@ -257,41 +257,116 @@ def swe_fields(M):
     return [6 * M * M, 4 * M * M, 2 * M * M]
 
 
+def lkdv_fields(n):
+    """lkdv's field-major ordering u | v | w (``lkdv/lkdv.py:111,122``, lkdv/assembly.py)."""
+    return [n // 3] * 3
+
+
+def lkdvrk_fields(s, n):
+    """lkdvRK's stage-major ordering (``lkdvRK/lkdvRK.py:171-172``): stage i's block
+    ``zbig[i*dof:(i+1)*dof]``, each field-major u | v | w, so ``3 s`` consecutive stage x field
+    blocks.  Cutting every block into P pieces keeps the couplings of ``A = I_s (x) M_t + dt
+    (A_GL (x) K)`` (``lkdvRK/lkdvRK.py:107-118``) and of the lifted constraints ``kron(P'P, M)``
+    (``lkdvRK/LinearSolver.py:48-49``) between nearest-neighbour ranks: every stage block has the
+    same 1-D band structure, and piece r of stage i couples to pieces r-1 .. r+1 of stage j."""
+    dof = n // s
+    return [dof // 3] * (3 * s)
+
+
+def distribute_constraints(sysd, conlist):
+    """Host class-form constraints ``(M, v, c)`` (reference ordering) -> rank-local device
+    constraints: ``M`` by :meth:`DistributedSystem.matrix` (its own halo plan), ``v`` by
+    :meth:`DistributedSystem.vector`; an all-zero ``M`` (the ``0*A`` mass) or ``v`` is dropped, as
+    ``solvers.cgmres`` does per call."""
+    out = []
+    for con in conlist:
+        M = getattr(con, "M", None)
+        Md = None
+        if M is not None:
+            Ms = sps.csr_matrix(M)
+            if Ms.nnz and np.any(Ms.data):
+                Md = sysd.matrix(Ms)
+        v = getattr(con, "v", None)
+        vd = None
+        if v is not None:
+            va = np.asarray(v, dtype=np.float64).reshape(-1)
+            if np.any(va):
+                vd = sysd.vector(va)
+        out.append(DeviceConstraint(Md, vd, float(np.asarray(getattr(con, "c", 0.0)))))
+    return out
+
+
+def dist_workload(config, P, M_override=None):
+    """The global problem of a SURVEY §8 configuration on P ranks: (A, b, host class constraints,
+    field blocks, scaling, description, normalisation of the reported value).
+
+    c3: swe weak scaling, ~1.0e6 DoF per GPU (global M = 289 sqrt(P)), mass + energy;
+    c5: swe M = 913 (N = 10,002,828) + the synthetic third constraint, strong scaling (restarted);
+    c4: lkdvRK GL(3) M = 16,667 (N = 300,006), the three invariants lifted to (M, v, c), strong;
+    c2: lkdv DG1, ~1.0e5 DoF per GPU (M = 16,667 P), mass + momentum + energy, weak."""
+    if config in ("c3", "c5"):
+        from .swe import LinearSolver as ls
+        from .swe import assembly
+
+        M = M_override or (913 if config == "c5" else int(round(289 * np.sqrt(P))))
+        dic, _ = assembly.linforms(M=M)
+        n = dic["A"].shape[0]
+        cons = ls.constraints(dic, np.zeros(n))
+        desc = f"swe-shaped RT2xDG0 CSR, global N={n:,} DoF (M={M})"
+        if config == "c5":
+            D, c3 = assembly.extra_constraint(n, dic["z0"], seed=2)
+            cons.append(ls._Constraint(D, np.zeros(n), c3))
+            desc += ", mass+energy+synthetic constraints (config C5)"
+        else:
+            desc += ", mass+energy constraints (config C3 per GPU)"
+        return dict(A=dic["A"], b=dic["b"], conlist=cons, fields=swe_fields(M), desc=desc,
+                    scaling="strong" if config == "c5" else "weak", norm=n / 1002252.0)
+    if config == "c4":
+        from .lkdvRK import LinearSolver as ls
+        from .lkdvRK import assembly
+
+        M = M_override or 16667
+        dic, prob = assembly.linforms(M=M, tstages=3)
+        n = dic["A"].shape[0]
+        return dict(A=dic["A"], b=dic["b"], conlist=ls.constraints(dic, prob, lift=True),
+                    fields=lkdvrk_fields(3, n), scaling="strong", norm=1.0,
+                    desc=f"lkdvRK GL(3) block-stage CSR (config C4, M={M}), global N={n:,} DoF, 3 invariants "
+                         "lifted to (M, v, c) form")
+    if config == "c2":
+        from .lkdv import LinearSolver as ls
+        from .lkdv import assembly
+
+        M = M_override or 16667 * P
+        dic, _ = assembly.linforms(M=M)
+        n = dic["A"].shape[0]
+        return dict(A=dic["A"], b=dic["b"], conlist=ls.constraints(dic, np.zeros(n)), fields=lkdv_fields(n),
+                    scaling="weak", norm=n / 100002.0,
+                    desc=f"lkdv DG1 CSR, global N={n:,} DoF (M={M}), mass+momentum+energy (config C2 per GPU)")
+    raise ValueError(f"no multi-GPU workload for config {config!r}")
+
+
 # ------------------------------------------------------------------------------------------------
 # bench.py --gpus N
 # ------------------------------------------------------------------------------------------------
 def bench_main(args, metric):
     from . import solvers
     from .device import DeviceVector
-    from .swe import assembly
 
     comm = Comm()
     P = comm.world
-    c5 = getattr(args, "config", "c3") == "c5"
-    M_base = args.M or 289
-    if c5:  # fixed global problem (strong scaling), restarted, 3 constraints
-        M = args.M or 913
-    else:  # weak scaling: ~1.0e6 DoF per GPU
-        M = int(round(M_base * np.sqrt(P)))
-    dic, _ = assembly.linforms(M=M)
-    A = dic["A"]
+    config = getattr(args, "config", "c3")
+    wl = dist_workload(config, P, args.M)
+    A = wl["A"]
     n_glob = A.shape[0]
-    sysd = DistributedSystem(comm, A, swe_fields(M))
+    sysd = DistributedSystem(comm, A, wl["fields"])
     ctx = comm.ctx
     if getattr(args, "orthog", "mgs") == "cgs2":
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1), "spis_set_option")
-    bd = sysd.vector(dic["b"])
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_DIST_MGS, getattr(args, "dist_mgs", 1)), "spis_set_option")
+    bd = sysd.vector(wl["b"])
     x0d = DeviceVector.from_host(np.zeros(sysd.n_local), ctx=ctx)
-    conlist = [
-        DeviceConstraint(None, sysd.vector(dic["omega"]), -dic["m0"]),
-        DeviceConstraint(sysd.matrix(dic["L"]), None, -dic["e0"]),
-    ]
-    cycles = 1
-    if c5:
-        D, c3 = assembly.extra_constraint(n_glob, dic["z0"], seed=2)
-        conlist.append(DeviceConstraint(sysd.matrix(D), None, c3))
-        cycles = args.cycles
-    del dic
+    conlist = distribute_constraints(sysd, wl["conlist"])
+    cycles = args.cycles if config == "c5" else 1
 
     def solve():
         if cycles > 1:
@@ -317,34 +392,34 @@ def bench_main(args, metric):
     nnz_local = int(sysd.op.csr.nnz)
     S = 12 * nnz_local + 4 * (sysd.n_local + 1) + 16 * sysd.n_local
     spmv_ms = ms[_lib.PROF_SPMV] / max(cnt[_lib.PROF_SPMV], 1)
-    kname = "spmv_rowblock_kernel<kEpiDot> (Arnoldi SpMV, local rows of rank 0)"
+    kname = "spmv_pipe_kernel (Arnoldi SpMV, solvers.py:191; local rows of rank 0)"
     if cnt[_lib.PROF_SPMV_DUAL] > 0:  # fused residual + Arnoldi SpMV: the dominant SpMV launch
         S = 12 * nnz_local + 4 * (sysd.n_local + 1) + 32 * sysd.n_local
         spmv_ms = ms[_lib.PROF_SPMV_DUAL] / cnt[_lib.PROF_SPMV_DUAL]
-        kname = "spmv_dual_kernel (true-residual SpMV of x_j fused with the Arnoldi SpMV of z_{j+2}, rank 0)"
+        kname = ("spmv_pipe_kernel<2048, 4> (true-residual SpMV of x_j, solvers.py:290, fused with the Arnoldi "
+                 "SpMV of z_{j+2}, :191; local rows of rank 0)")
     spmv_gbs = S / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
-    dof_equiv = n_glob / (12 * M_base * M_base)
+    mgs_ms = ms[_lib.PROF_MGS] / max(cnt[_lib.PROF_MGS], 1)
     if comm.rank == 0:
         out = {
             "metric": metric,
-            "value": iters * dof_equiv / elapsed,
+            "value": iters * wl["norm"] / elapsed,
             "unit": "iterations/s",
             "n_gpus": P,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if c5 else "weak",
+            "scaling": wl["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"swe-shaped RT2xDG0 CSR, global N={n_glob:,} DoF (M={M}) row-partitioned over {P} "
-                            f"GPUs (~{n_glob // P:,} DoF/GPU), CGMRES(k={args.k}, tol={args.tol:g})"
-                            + (f" restarted x{cycles}, mass+energy+synthetic constraints (config C5)" if c5 else
-                               ", mass+energy constraints")
-                            + "; value = global iterations x (global DoF / 1,002,252) / s",
-                "config": "c5" if c5 else "c3",
+                "workload": wl["desc"] + f", row-partitioned over {P} GPUs (~{n_glob // P:,} DoF/GPU), "
+                            f"CGMRES(k={args.k}, tol={args.tol:g})" + (f" restarted x{cycles}" if cycles > 1 else "")
+                            + (f"; value = global iterations x {wl['norm']:.4g} (global DoF / the single-GPU "
+                               "config's) / s" if wl["norm"] != 1.0 else "; value = global iterations / s"),
+                "config": config,
                 "orthogonalisation": getattr(args, "orthog", "mgs"),
                 "global_dof": n_glob,
                 "k": args.k,
@@ -362,6 +437,11 @@ def bench_main(args, metric):
                 "algorithmic_bytes_per_launch": S,
                 "avg_launch_us": 1e3 * spmv_ms,
             },
+            "kernels": {"mgs_us_mean": 1e3 * mgs_ms, "spmv_us": 1e3 * spmv_ms},
         }
+        if not args.no_cpu_baseline:  # the reference's CPU path on the same global system
+            import bench as _bench
+
+            out["cpu_baseline"] = _bench.cpu_baseline(wl, wl["conlist"], args.k, args.tol, args.cpu_budget)
         print(json.dumps(out))
     comm.dist.barrier()

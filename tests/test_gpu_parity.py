@@ -967,11 +967,15 @@ def test_full_size_swe_vs_oracle(spis):
     assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
 
 
-def test_distributed_code_path_self_halo(spis):
+@pytest.mark.parametrize("dist_mgs,gram", [("one_reduce", "fused"), ("per_step", "fused"), ("one_reduce", "generic")])
+def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
     """The RCCL data path on one GPU: a 1-rank communicator (fixed-size partial arrays +
     ncclAllReduce) and an operator whose last ~20% columns are declared ghosts received from
-    rank 0 itself (gather + grouped ncclSend/ncclRecv), constraints through the generic
-    per-column halo path.  Must reproduce the single-GPU solve."""
+    rank 0 itself (gather + grouped ncclSend/ncclRecv).  MGS either in its one-reduce form (two
+    all-reduces per Arnoldi step, SPIS_OPT_DIST_MGS 1, the default) or one all-reduce per
+    projection; constraints through K7m on the local rows with the ghost Ut rows exchanged
+    through the matrix's halo plan and G all-reduced (fused), or the generic per-column halo
+    path.  Must reproduce the single-GPU solve."""
     import ctypes as C
 
     from structurepreservingiterativesolvers_amd import _lib, solvers
@@ -990,6 +994,8 @@ def test_distributed_code_path_self_halo(spis):
     uid = (C.c_uint8 * 128)()
     _lib.check(ctx.L.spis_comm_unique_id(uid), "spis_comm_unique_id")
     _lib.check(ctx.L.spis_comm_init(ctx.handle, 1, 0, uid), "spis_comm_init")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_DIST_MGS, 1 if dist_mgs == "one_reduce" else 0), "opt")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GENERIC_GRAM, 1 if gram == "generic" else 0), "opt")
 
     def self_halo(M):
         M = M.tocsr()
