@@ -199,6 +199,9 @@ def main():
                          "pipelined XCD-local walk")
     ap.add_argument("--col16", type=int, default=1, choices=[0, 1, 2],
                     help="16-bit column copy for the pipelined SpMV: 1 beyond the Infinity Cache, 2 always, 0 never")
+    ap.add_argument("--spmv-nt", type=int, default=0, choices=[0, 1, 2],
+                    help="nontemporal matrix stream in the pipelined SpMV (SPIS_OPT_SPMV_NT): 0 never, 1 always, "
+                         "2 beyond the 256 MB Infinity Cache")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
                     help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
@@ -235,6 +238,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_COL16, args.col16), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,

@@ -28,6 +28,7 @@ OPT_EARLY_CON = 9
 OPT_NT_BASIS = 10
 OPT_COL16 = 11
 OPT_DIST_MGS = 12
+OPT_SPMV_NT = 13
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

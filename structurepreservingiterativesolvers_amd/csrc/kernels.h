@@ -58,6 +58,7 @@ struct CsrView {
   const uint16_t* col16 = nullptr;
   const int4* blk_base = nullptr;
   int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
+  bool nt = false;  // K1p / K1dp: the matrix stream (val, col) read with nontemporal loads
   // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
   // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at
   // sl_off[s] + 64 t + l; rows padded to the slice's longest (col = the row, val = 0, skipped
@@ -149,10 +150,9 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
 // q_l . q_{nv-1} (l < nv - 1) -> part rows [0, nv) and [nv, 2 nv - 1), grid columns each
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
                            hipStream_t s, const LaunchEv* ev = nullptr);
-// one workgroup: those dots, Gram row nv - 1 into G (kCgsMax x kCgsMax), h_l = q_l . w -
-// sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
-hipError_t launch_icwy_coef(const double* part, int n_in, int nv, double* G, double* coef, double* h_out,
-                            hipStream_t s);
+// one workgroup: from those 2 nv - 1 dots (reduced, d), Gram row nv - 1 into G (kCgsMax x
+// kCgsMax), h_l = q_l . w - sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
+hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM

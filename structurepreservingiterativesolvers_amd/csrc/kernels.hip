@@ -336,7 +336,10 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
 #pragma unroll
   for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
     const int i = threadIdx.x + u * kBlock;
-    if (C16) {
+    if (C16 && NT) {  // streamed once (beyond the Infinity Cache): keep it for the gathered vectors
+      st.cols[u] = i < st.nnz ? __builtin_nontemporal_load(c16 + st.nz0 + i) : 0;
+      st.vals[u] = i < st.nnz ? __builtin_nontemporal_load(va + st.nz0 + i) : 0.0;
+    } else if (C16) {
       st.cols[u] = i < st.nnz ? c16[st.nz0 + i] : 0;  // raw: decoded at the gathers, so the prefetch
                                                       // stays in flight (0 decodes to a column of the block)
       st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
@@ -727,12 +730,18 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
                             int grid, hipStream_t s, const LaunchEv* ev) {
   dim3 g(grid), b(kBlock);
 #define SPIS_PIPE(M)                                                                                            \
-  if (A.depth == 2)                                                                                             \
+  if (A.depth == 2)                                                                                        \
     launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
+  else if (A.col16 != nullptr && A.nt)                                                                          \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, true, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,         \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
   else if (A.col16 != nullptr)                                                                                  \
     launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,        \
              A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
+  else if (A.nt)                                                                                                \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
+             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);                      \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr)
@@ -2196,29 +2205,32 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
   }
 }
 
-// one workgroup: the 2 nv - 1 dots from their (all-reduced) partials in sum_partials' fixed
-// order, the newest Gram row into G (row-major kCgsMax x kCgsMax, rows < nv - 1 written by the
-// earlier steps of this solve), then h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l
-// order -> coef (device, cgs_update's input) and h_out (the host H column)
-__global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restrict__ part, int n_in, int nv,
+// one workgroup: the 2 nv - 1 dots (already reduced: one value each), the newest Gram row into G
+// (row-major kCgsMax x kCgsMax; rows < nv - 1 were written by the earlier steps of this solve),
+// then h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l order -> coef (device, cgs_update's
+// input) and h_out (the host H column).  The Gram triangle is staged in LDS first: the recurrence
+// is one thread's sequential chain (~nv^2 / 2 dependent FMAs), and read from global memory each
+// operand cost a load latency (icwy 38 us per step at nv ~ 15 in the first version)
+__global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restrict__ d, int nv,
                                                            double* __restrict__ G, double* __restrict__ coef,
                                                            double* __restrict__ h_out) {
 #pragma clang fp contract(off)
-  __shared__ double s_wave[4];
+  __shared__ double s_g[kCgsMax * kCgsMax];
   __shared__ double s_d[2 * kCgsMax];
-  for (int r = 0; r < 2 * nv - 1; ++r) {
-    const double t = sum_partials(part + static_cast<int64_t>(r) * n_in, n_in, s_wave);
-    if (threadIdx.x == 0) s_d[r] = t;
-    __syncthreads();
+  for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = d[i];
+  for (int i = threadIdx.x; i < (nv - 1) * kCgsMax; i += kBlock) s_g[i] = G[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < nv - 1; i += kBlock) {  // the newest row, to LDS and to G
+    s_g[(nv - 1) * kCgsMax + i] = s_d[nv + i];
+    G[static_cast<int64_t>(nv - 1) * kCgsMax + i] = s_d[nv + i];
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double* grow = G + static_cast<int64_t>(nv - 1) * kCgsMax;
-    for (int l = 0; l < nv - 1; ++l) grow[l] = s_d[nv + l];
     double h[kCgsMax];
     for (int l = 0; l < nv; ++l) {
       double t = s_d[l];
-      const double* gl = l == nv - 1 ? grow : G + static_cast<int64_t>(l) * kCgsMax;
-      for (int m = 0; m < l; ++m) t -= h[m] * (l == nv - 1 ? s_d[nv + m] : gl[m]);
+      const double* gl = s_g + l * kCgsMax;
+      for (int m = 0; m < l; ++m) t -= h[m] * gl[m];
       h[l] = t;
       coef[l] = t;
       h_out[l] = t;
@@ -2233,10 +2245,9 @@ hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t 
   return hipGetLastError();
 }
 
-hipError_t launch_icwy_coef(const double* part, int n_in, int nv, double* G, double* coef, double* h_out,
-                            hipStream_t s) {
+hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(icwy_coef_kernel, dim3(1), dim3(kBlock), 0, s, part, n_in, nv, G, coef, h_out);
+  hipLaunchKernelGGL(icwy_coef_kernel, dim3(1), dim3(kBlock), 0, s, d, nv, G, coef, h_out);
   return hipGetLastError();
 }
 

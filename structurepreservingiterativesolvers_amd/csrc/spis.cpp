@@ -143,6 +143,7 @@ struct spis_context {
   int overlap_gemv = 1;
   hipEvent_t ev_gemv = nullptr;
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
+  int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
   // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
@@ -316,6 +317,7 @@ CsrView spis_matrix::dual_view() const {
     return v;
   }
   if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
+  v.nt = ctx->spmv_nt == 1 || (ctx->spmv_nt == 2 && 12.0 * static_cast<double>(nnz) > 256.0 * 1024 * 1024);
   if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
   else if ((mode == 2 || mode == 4) && blk_slab_d != nullptr) {
     v.blk_meta = blk_slab_d;
@@ -449,8 +451,10 @@ static void prof_drain(spis_context* c) {
   c->ev_pending.resize(keep);
 }
 
+// a one-rank communicator's sum is the identity: no collective launch (halo exchanges still run:
+// a one-rank operator may declare ghosts it receives from itself)
 static int allreduce(spis_context* c, double* buf, int64_t count) {
-  if (!c->comm || count <= 0) return SPIS_OK;
+  if (!c->comm || count <= 0 || c->nranks == 1) return SPIS_OK;
   NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
   return SPIS_OK;
 }
@@ -470,7 +474,7 @@ static int exchange(spis_context* c, const spis_matrix* M, double* x) {
 }
 
 static int allreduce_on(spis_context* c, double* buf, int64_t count, hipStream_t st) {
-  if (!c->comm || count <= 0) return SPIS_OK;
+  if (!c->comm || count <= 0 || c->nranks == 1) return SPIS_OK;
   NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, st));
   return SPIS_OK;
 }
@@ -789,6 +793,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_ORTHOG:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
+        return SPIS_OK;
+      case SPIS_OPT_SPMV_NT:
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "spmv_nt %lld: 0, 1 or 2", (long long)value);
+        c->spmv_nt = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_DIST_MGS:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "dist_mgs %lld: 0 or 1", (long long)value);
@@ -2301,7 +2309,7 @@ struct Solver {
     HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first));
     HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
     ST_TRY(allreduce(c, d, 2 * nv - 1));
-    HIP_TRY(launch_icwy_coef(d, 1, nv, c->icwy_G, coef, hcol, s));
+    HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
     HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s));
     double* nrm = d + 2 * kCgsMax;
     HIP_TRY(launch_cgs_finalize(c->partB, gc, 1, nrm, nullptr, nullptr, s));

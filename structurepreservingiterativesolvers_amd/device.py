@@ -61,6 +61,7 @@ _OPTIONS = {
                                         "sell": 6, "xcd_natural": 7}),
     "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
     "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
+    "spmv_nt": (_lib.OPT_SPMV_NT, {False: 0, True: 1, "auto": 2}),
 }
 
 

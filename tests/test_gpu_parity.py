@@ -380,6 +380,49 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
         set_option("ell_gram", "mfma")
 
 
+def test_k7t_waves_walk_many_blocks(spis):
+    """K7t (symmetric constraint matrix, f64 MFMA from the slot table) at p + 1 = 32, where each
+    wave walks ~13 table blocks (swe energy matrix at M = 128: ~27k blocks over the resident
+    waves) through its two-ahead table prefetch (cur / nxt / nx2): against constraint_container's
+    host algebra (solvers.py:33-36) and against K7m on the same inputs.  (Round 2 removed a 32-slot
+    variant that was wrong when waves walked several blocks; this pins the shipping 16-slot walk
+    in that regime.)"""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=128)
+    n = dic["A"].shape[0]
+    rng = np.random.default_rng(11)
+
+    class Con:
+        pass
+
+    con = Con()
+    con.M, con.v, con.c = dic["L"], None, -1.0
+    p = 31
+    Z = rng.normal(size=(n, p))
+    x0 = rng.normal(size=n)
+    Mv = sps.csr_matrix(dic["L"])
+    ref_t2 = 0.5 * Z.T @ (Mv @ Z)
+    ref_t1 = x0 @ (Mv @ Z)
+    ref_t0 = 0.5 * x0 @ (Mv @ x0) + con.c
+    con.v = np.zeros(n)
+    got = {}
+    for mode in ("mfma", "mfma_full"):  # K7t, then K7m for every matrix
+        set_option("ell_gram", mode)
+        try:
+            t = solvers.constraint_container(con, x0, Z)
+        finally:
+            set_option("ell_gram", "mfma")
+        got[mode] = t
+        scale = np.abs(Mv).sum() * np.abs(Z).max() ** 2 * 1e-13
+        np.testing.assert_allclose(t.term2, ref_t2, rtol=1e-11, atol=scale)
+        np.testing.assert_allclose(t.term1, ref_t1, rtol=1e-11, atol=scale)
+        np.testing.assert_allclose(t.term0, ref_t0, rtol=1e-11, atol=scale)
+    np.testing.assert_allclose(got["mfma"].term2, got["mfma_full"].term2, rtol=1e-12, atol=1e-12 * np.abs(ref_t2).max())
+
+
 def test_nontemporal_chain_loads_bit_identical(spis):
     """SPIS_OPT_NT_BASIS changes the cache policy of the MGS chain's basis loads only: the same
     bits with and without it."""

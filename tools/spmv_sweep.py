@@ -22,25 +22,26 @@ A = dic["A"]
 n, nnz = A.shape[0], A.nnz
 ctx = get_context(0)
 print(f"M={M} N={n:,} nnz={nnz:,}", flush=True)
-for mode in modes:
-    for c16 in (0, 2):
-        if mode.endswith("2") and c16:
-            continue  # the two-deep kernel has no 16-bit column variant
-        set_option("spmv_pipe", mode)
-        set_option("col16", {0: False, 2: True}[c16])
-        from structurepreservingiterativesolvers_amd.device import DeviceMatrix
+configs = [(m, nt, c16) for m in modes for nt in (False, True) for c16 in (0, 2)
+           if not (m.endswith("2") and (c16 or nt))]  # the two-deep kernel: no 16-bit / nontemporal variant
+for mode, nt, c16 in configs:
+    set_option("spmv_pipe", mode)
+    set_option("spmv_nt", nt)
+    set_option("col16", {0: False, 2: True}[c16])
+    from structurepreservingiterativesolvers_amd.device import DeviceMatrix
 
-        Ad = DeviceMatrix(ctx, A)  # a fresh upload: the table / copies follow the options
-        cb = 2 if c16 else 4
-        for kind, name in ((0, "arnoldi"), (1, "dual")):
-            byt = (8 + cb) * nnz + 4 * (n + 1) + (16 if kind == 0 else 32) * n
-            res = []
-            for cold in (0, 1):
-                v = C.c_double()
-                _lib.check(ctx.L.spis_spmv_bench(ctx.handle, Ad.handle, kind, cold, 20, C.byref(v)), "bench")
-                res.append(v.value)
-            print(f"{mode:12s} col16={c16} {name:8s} warm {res[0]:8.1f} us {byt / res[0] / 1e3:7.0f} GB/s | "
-                  f"cold {res[1]:8.1f} us {byt / res[1] / 1e3:7.0f} GB/s ({byt / res[1] / 1e3 / 8000:.3f})", flush=True)
-        del Ad
+    Ad = DeviceMatrix(ctx, A)  # a fresh upload: the table / copies follow the options
+    cb = 2 if c16 else 4
+    for kind, name in ((0, "arnoldi"), (1, "dual")):
+        byt = (8 + cb) * nnz + 4 * (n + 1) + (16 if kind == 0 else 32) * n
+        res = []
+        for cold in (0, 1):
+            v = C.c_double()
+            _lib.check(ctx.L.spis_spmv_bench(ctx.handle, Ad.handle, kind, cold, 20, C.byref(v)), "bench")
+            res.append(v.value)
+        print(f"{mode:12s} nt={int(nt)} col16={c16} {name:8s} warm {res[0]:8.1f} us {byt / res[0] / 1e3:7.0f} GB/s | "
+              f"cold {res[1]:8.1f} us {byt / res[1] / 1e3:7.0f} GB/s ({byt / res[1] / 1e3 / 8000:.3f})", flush=True)
+    del Ad
 set_option("spmv_pipe", "auto")
 set_option("col16", "auto")
+set_option("spmv_nt", False)
