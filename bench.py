@@ -300,6 +300,14 @@ def main():
         # the 256 MB Infinity Cache
         pipe = "xcd" if args.config in ("c3", "c5") or 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
     traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" and not c16 else None
+    c5 = args.config == "c5" and args.M in (None, 913)
+    if c5 and pipe == "xcd" and c16 and args.spmv_nt == 0:
+        # profiles/r03_c5_spmv_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the same launches
+        # (tools/r03_pmc_c5.sh over tools/spmv_pmc.py, corrected by tools/pmc_kernels.py)
+        t5 = load_traffic("r03_c5_spmv_traffic.json")
+        want = "spmv_pipe_kernel<2048, 4, false, 1, true>" if fused else "spmv_pipe_kernel<2048, 1, false, 1, true>"
+        rows = [r for r in (t5 or {}).get("kernels", []) if want in r["kernel"]]
+        traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",
              "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)", "stride2": "spmv_pipe2_kernel<2048, 4>",
              "xcd2": "spmv_pipe2_kernel<2048, 4> (XCD-local walk)",

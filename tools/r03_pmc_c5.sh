@@ -4,10 +4,11 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc3
+nt=${1:-0}
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc3/$c -o run -- \
-    python tools/spmv_pmc.py 913 > gpurun_out/pmc3/$c.log 2>&1
-  f=$(find gpurun_out/pmc3/$c -name '*counter_collection.csv' | head -n 1)
-  cp "$f" gpurun_out/pmc3/r03_c5_pmc_$(echo $c | tr A-Z a-z).csv
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc3/${c}_nt$nt -o run -- \
+    python tools/spmv_pmc.py 913 $nt > gpurun_out/pmc3/${c}_nt$nt.log 2>&1
+  f=$(find gpurun_out/pmc3/${c}_nt$nt -name '*counter_collection.csv' | head -n 1)
+  cp "$f" gpurun_out/pmc3/r03_c5_pmc_$(echo $c | tr A-Z a-z)_nt$nt.csv
 done
 echo done
