@@ -145,11 +145,12 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
                           hipStream_t s, const LaunchEv* ev = nullptr);
 hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
-                             bool dot, double* part, int grid, hipStream_t s);
+                             bool dot, double* part, int grid, hipStream_t s, bool nt = false);
 // K2w (multi-GPU MGS, one reduction for the projections): partials of q_l . w (l < nv) and of
 // q_l . q_{nv-1} (l < nv - 1) -> part rows [0, nv) and [nv, 2 nv - 1), grid columns each
+// nt: nontemporal basis loads (the matrix stays Infinity-Cache resident between SpMVs, as K2q's)
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
-                           hipStream_t s, const LaunchEv* ev = nullptr);
+                           hipStream_t s, const LaunchEv* ev = nullptr, bool nt = false);
 // one workgroup: from those 2 nv - 1 dots (reduced, d), Gram row nv - 1 into G (kCgsMax x
 // kCgsMax), h_l = q_l . w - sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
 hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s);
@@ -158,7 +159,7 @@ hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, 
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,
-                       const LaunchEv* ev = nullptr);
+                       const LaunchEv* ev = nullptr, bool nt = false);
 // W[c] = M Z[c] for c < nvec (vectors at stride ldx / ldy)
 hipError_t launch_spmm(const CsrView& A, const double* X, int64_t ldx, int nvec, double* Y,
                        int64_t ldy, hipStream_t s);

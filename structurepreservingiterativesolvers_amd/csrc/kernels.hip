@@ -1975,7 +1975,7 @@ __global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double
   }
 }
 
-template <int DOT>
+template <int DOT, bool NT = false>
 __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* __restrict__ w,
                                                             const double* __restrict__ Q, int64_t pitch, int nv,
                                                             const double* __restrict__ coef,
@@ -2005,8 +2005,8 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     for (int m = 0; m < kCgsPerWave; ++m) {
       if (wid + 4 * m < nv) {
         const double* qv = Qw + m * step;
-        qa[m] = *reinterpret_cast<const double2*>(qv + e);
-        qb[m] = *reinterpret_cast<const double2*>(qv + e + 128);
+        qa[m] = ld_basis(reinterpret_cast<const double2*>(qv + e), NT);
+        qb[m] = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT);
         const double cm = s_c[wid + 4 * m];
         p0 += cm * qa[m].x;
         p1 += cm * qa[m].y;
@@ -2112,10 +2112,12 @@ hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t p
 }
 
 hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
-                             bool dot, double* part, int grid, hipStream_t s) {
+                             bool dot, double* part, int grid, hipStream_t s, bool nt) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
   if (dot)
     hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+  else if (nt)
+    hipLaunchKernelGGL((cgs_update_kernel<0, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
   else
     hipLaunchKernelGGL(cgs_update_kernel<0>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
   return hipGetLastError();
@@ -2136,6 +2138,7 @@ hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, 
 // then cgs_update subtracts Q h with the ||w'||^2 partials (the second all-reduce) and K3
 // normalises.  Two reductions per Arnoldi step instead of MGS's j + 2; exact arithmetic is MGS's.
 // ---------------------------------------------------------------------------------------------
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const double* __restrict__ w,
                                                           const double* __restrict__ Q, int64_t pitch, int nv,
                                                           double* __restrict__ part) {
@@ -2162,8 +2165,8 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
       const int i = wid + 4 * m;
       if (i < nv) {
         const double* qv = Qw + m * step;
-        const double2 qa = *reinterpret_cast<const double2*>(qv + e);
-        const double2 qb = *reinterpret_cast<const double2*>(qv + e + 128);
+        const double2 qa = ld_basis(reinterpret_cast<const double2*>(qv + e), NT);
+        const double2 qb = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT);
         acc[m] += qa.x * wa.x;
         acc[m] += qa.y * wa.y;
         acc[m] += qb.x * wb.x;
@@ -2239,9 +2242,12 @@ __global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restr
 }
 
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
-                           hipStream_t s, const LaunchEv* ev) {
+                           hipStream_t s, const LaunchEv* ev, bool nt) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
-  launch_k(icwy_dot_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+  if (nt)
+    launch_k(icwy_dot_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+  else
+    launch_k(icwy_dot_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
   return hipGetLastError();
 }
 
@@ -2257,7 +2263,7 @@ hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, do
 // are copied to LDS from a device buffer.  Each lane streams one (VEC: two) element(s) of every
 // basis vector; sum in basis order, then + x0 (numpy's ``Z @ yk + x0`` adds x0 afterwards).
 // ---------------------------------------------------------------------------------------------
-template <bool VEC, bool ARG>
+template <bool VEC, bool ARG, bool NT = false>
 __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
                                                       const double* __restrict__ Z, int64_t pitch,
                                                       YArg yarg, const double* __restrict__ ycoef,
@@ -2277,7 +2283,7 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
     for (int64_t q = tid; q < npair; q += stride) {
       double a0 = 0.0, a1 = 0.0;
       for (int i = 0; i < p; ++i) {
-        const double2 z = reinterpret_cast<const double2*>(Z + i * pitch)[q];
+        const double2 z = ld_basis(reinterpret_cast<const double2*>(Z + i * pitch) + q, NT);
         const double c = yc[i];
         a0 += z.x * c;
         a1 += z.y * c;
@@ -2301,7 +2307,7 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
 }
 
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y_host_or_dev,
-                       bool y_on_host, const double* x0, double* x, hipStream_t s, const LaunchEv* ev) {
+                       bool y_on_host, const double* x0, double* x, hipStream_t s, const LaunchEv* ev, bool nt) {
   if (p > kMaxK || p < 1) return hipErrorInvalidValue;
   const bool vec = aligned16(Z) && (pitch % 2 == 0) && aligned16(x0) && aligned16(x);
   int64_t g = (n / (vec ? 2 : 1) + kBlock - 1) / kBlock;
@@ -2313,7 +2319,9 @@ hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const d
   if (arg)
     for (int i = 0; i < p; ++i) ya.v[i] = y_host_or_dev[i];
   const double* yd = arg ? nullptr : y_host_or_dev;
-  if (vec && arg)
+  if (vec && arg && nt)
+    launch_k(gemv_kernel<true, true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+  else if (vec && arg)
     launch_k(gemv_kernel<true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
   else if (vec)
     launch_k(gemv_kernel<true, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);

@@ -2184,6 +2184,12 @@ struct Solver {
   // instead of delaying the dual SpMV that reads x_j.  A constrained LS_j re-enqueues the GEMV
   // with its own y (stream order on the side stream); a stop at j-1 leaves x_j unused (x_j and
   // x_{j-1} live in separate buffers).  Results are identical to the unspeculated path.
+  // basis streams nontemporal when the matrix and the k+1 basis vectors overflow the 256 MB
+  // Infinity Cache (SPIS_OPT_NT_BASIS 2), so re-streaming the basis leaves the matrix resident
+  bool nt_basis_on() const {
+    const double ws_bytes = 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * (k + 1) * static_cast<double>(n);
+    return c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
+  }
   bool lag_chain() const {
     // K2q pads an odd n's last pair: its capacity test counts (n + 1) / 2 pairs, as the launch does
     return c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8;
@@ -2306,11 +2312,12 @@ struct Solver {
     const LaunchEv e_first = pm.first(), e_last = pm.last();
     double* d = c->icwy_d;
     double* coef = c->cgs_c;
-    HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first));
+    const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
+    HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt));
     HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
     ST_TRY(allreduce(c, d, 2 * nv - 1));
     HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
-    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s));
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s, nt));
     double* nrm = d + 2 * kCgsMax;
     HIP_TRY(launch_cgs_finalize(c->partB, gc, 1, nrm, nullptr, nullptr, s));
     ST_TRY(allreduce(c, nrm, 1));
@@ -2416,7 +2423,9 @@ struct Solver {
         *done = le.stop;
       }
       if (p <= kYArg) {
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le));
+        // several GPUs: the GEMV runs every iteration beside the distributed MGS; nontemporal basis
+        // loads keep the matrix resident there (single GPU: the GEMV rides in K2q, FX)
+        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le, c->comm && nt_basis_on()));
       } else {
         double* yh = c->pinned + yoff();
         for (int a = 0; a < p; ++a) yh[a] = y[a];
