@@ -187,7 +187,10 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  *   columns) with nontemporal loads, so streaming a matrix larger than the 256 MB Infinity Cache
  *   does not evict the gathered vectors; 1 = always, 2 = when val/col exceed 256 MB, 0 = never.
  *   Results identical.  Measured at C5 (1.5 GB matrix, standalone, cold): Arnoldi SpMV 404 -> 397
- *   us, dual 497 -> 627 us; off by default. */
+ *   us, dual 497 -> 627 us; off by default.
+ * SPIS_OPT_K7T_SLOTS (default 16): slots per block of K7t's slot table, 16 or 32 (32: twice the
+ *   gathers in flight per lane at 2 waves per SIMD; measured slower at C3, kept for the test that
+ *   walks many 32-slot blocks per wave).  Results equal up to the grouping of the Gram sums. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -201,7 +204,8 @@ enum spis_option {
   SPIS_OPT_NT_BASIS = 10,
   SPIS_OPT_COL16 = 11,
   SPIS_OPT_DIST_MGS = 12,
-  SPIS_OPT_SPMV_NT = 13
+  SPIS_OPT_SPMV_NT = 13,
+  SPIS_OPT_K7T_SLOTS = 14
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

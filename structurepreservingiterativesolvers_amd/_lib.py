@@ -29,6 +29,7 @@ OPT_NT_BASIS = 10
 OPT_COL16 = 11
 OPT_DIST_MGS = 12
 OPT_SPMV_NT = 13
+OPT_K7T_SLOTS = 14
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

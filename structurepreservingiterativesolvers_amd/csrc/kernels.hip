@@ -3625,9 +3625,15 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
   if (blk(L) < kb1) load(blk(L), cur);
   if (blk(L + wpg) < kb1) load(blk(L + wpg), nxt);
   for (; blk(L) < kb1; L += wpg) {
-    const unsigned long long mk = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(cur.mask)) |
-                                  (static_cast<unsigned long long>(__builtin_amdgcn_readfirstlane(
-                                       static_cast<unsigned>(cur.mask >> 32))) << 32);
+    // readfirstlane returns int: widen through unsigned, or a start bit at slot 31 (32-slot
+    // blocks) sign-extends into the slot count (ns = -1: the whole block skipped; the round-2
+    // 32-slot failure, tools/k7t_probe.py)
+    const unsigned long long mk =
+        static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readfirstlane(
+            static_cast<unsigned>(cur.mask)))) |
+        (static_cast<unsigned long long>(static_cast<unsigned>(__builtin_amdgcn_readfirstlane(
+             static_cast<unsigned>(cur.mask >> 32))))
+         << 32);
     const int ns = static_cast<int>(mk >> 32);
     const unsigned starts = static_cast<unsigned>(mk);
     // gathers in straight-line quads (a wave-uniform test per 4 slots): the bpermutes of a quad
@@ -3714,15 +3720,17 @@ static int sym_grid() {
 hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
                                       hipStream_t s) {
   if (np1 > 32) return hipErrorInvalidValue;
-  int grid = 0;
-  if (T.ns != 16) return hipErrorInvalidValue;
-  grid = sym_grid<16>();
+  if (T.ns != 16 && T.ns != 32) return hipErrorInvalidValue;
+  const int grid = T.ns == 16 ? sym_grid<16>() : sym_grid<32>();
   static const int chunk = [] {  // SPIS_K7T_CHUNK: blocks per XCD-local chunk (0: whole-table round robin)
     const char* e = std::getenv("SPIS_K7T_CHUNK");
     const int v = e ? std::atoi(e) : 0;
     return v > 0 ? v : 0;
   }();
-  hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
+  if (T.ns == 16)
+    hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
+  else
+    hipLaunchKernelGGL(constraint_gram_sym_kernel<32>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int np2 = np1 * np1;

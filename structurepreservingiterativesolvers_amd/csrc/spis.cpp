@@ -143,6 +143,7 @@ struct spis_context {
   int overlap_gemv = 1;
   hipEvent_t ev_gemv = nullptr;
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
+  int k7t_slots = 16;               // K7t slot-table width (SPIS_OPT_K7T_SLOTS): 16 or 32
   int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
@@ -801,6 +802,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_DIST_MGS:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "dist_mgs %lld: 0 or 1", (long long)value);
         c->dist_mgs = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_K7T_SLOTS:
+        if (value != 16 && value != 32) return fail(SPIS_ERR_ARG, "k7t_slots %lld: 16 or 32", (long long)value);
+        c->k7t_slots = static_cast<int>(value);
         return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }
@@ -1811,7 +1816,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     if (np1 <= 32 && eg == 2) ST_TRY(ensure_stg(c, cons[ci].M, &L.sv, &L.stg));
     L.ell = !L.stg && np1 <= 32 && (eg == 1 || eg == 2);
     if (L.ell) ST_TRY(ensure_ell(c, cons[ci].M, &L.ev));
-    if (tsym) ST_TRY(ensure_symtab(c, cons[ci].M, 16, &L.tv, &L.sym));
+    if (tsym) ST_TRY(ensure_symtab(c, cons[ci].M, c->k7t_slots, &L.tv, &L.sym));
     plan.push_back(L);
   }
   const size_t voff = static_cast<size_t>(m) * np1 * np1;
@@ -2174,6 +2179,11 @@ struct Solver {
   }
 
   double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
+  // rows the update GEMV computes.  Several GPUs: n + n_ghost.  Every basis vector z_l's ghost
+  // rows hold its owners' values (exchanged before A_l's SpMV) and x0's were exchanged at the
+  // start, so x_j's ghost rows come out bitwise equal to the owners' x_j (same y, same order):
+  // no per-iteration halo exchange of x_j before its residual SpMV
+  int64_t n_gx() const { return (c->comm && !A->nbr.empty()) ? n + A->n_ghost : n; }
 
   // Speculative update (single GPU, K2q chains): K2q's gatherer writes H[:, j] with H[j+1, j]
   // last, behind a system-scope release, so the host can read the column as soon as A_j's chain
@@ -2318,10 +2328,10 @@ struct Solver {
     ST_TRY(allreduce(c, d, 2 * nv - 1));
     HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
     HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s, nt));
-    double* nrm = d + 2 * kCgsMax;
-    HIP_TRY(launch_cgs_finalize(c->partB, gc, 1, nrm, nullptr, nullptr, s));
-    ST_TRY(allreduce(c, nrm, 1));
-    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), nrm, 1, hcol + j + 1, s, gb, &e_last));
+    // ||w'||^2: the gc partials all-reduced element-wise (8 KB, latency-bound like one double) and
+    // summed in fixed order by every normalize workgroup: no finalize launch in between
+    ST_TRY(allreduce(c, c->partB, gc));
+    HIP_TRY(launch_normalize(n, ws->w, Qv(j + 1), c->partB, gc, hcol + j + 1, s, gb, &e_last));
     return SPIS_OK;
   }
 
@@ -2390,7 +2400,7 @@ struct Solver {
     ++c->gemv_seq;
     HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
     HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
-    return exchange(c, A, xbuf(j));  // (single GPU in L mode: a no-op)
+    return SPIS_OK;
   }
   // U_j's residual partials (from [U_j res | a_{j+2}]) reduced and published without a chain
   int enqueue_finalize(int j) {
@@ -2422,22 +2432,19 @@ struct Solver {
         if (le.stop == nullptr) le.stop = c->ev_gemv;
         *done = le.stop;
       }
+      // several GPUs: over the ghost rows too (n_gx), so x_j's halo needs no exchange
       if (p <= kYArg) {
         // several GPUs: the GEMV runs every iteration beside the distributed MGS; nontemporal basis
         // loads keep the matrix resident there (single GPU: the GEMV rides in K2q, FX)
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le, c->comm && nt_basis_on()));
+        HIP_TRY(launch_gemv(n_gx(), p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le, c->comm && nt_basis_on()));
       } else {
         double* yh = c->pinned + yoff();
         for (int a = 0; a < p; ++a) yh[a] = y[a];
         HIP_TRY(hipMemcpyAsync(ws->ydev, yh, sizeof(double) * p, hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_gemv(n, p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, xbuf(j), s, &le));
+        HIP_TRY(launch_gemv(n_gx(), p, ws->Zb, ws->pitch, ws->ydev, false, ws->x0, xbuf(j), s, &le));
       }
     }
-    // x_j's halo: on the main stream, ordered after the GEMV.  A side-stream GEMV's caller runs
-    // it after the main stream's wait for the GEMV (RCCL calls stay on the main stream: one
-    // order of collectives on every rank); issuing it here, before that wait, sent ghosts of the
-    // buffer's previous contents (round 2: iterate 1's residual read ||b||)
-    return s_gemv ? SPIS_OK : exchange(c, A, xbuf(j));
+    return SPIS_OK;
   }
 
   // U_j's true-residual partials go to device memory (partR).  Single GPU: one workgroup reduces
@@ -2527,7 +2534,6 @@ struct Solver {
         hipEvent_t done = nullptr;
         ST_TRY(update_gemv(j, p, y, c->stream2, &done));
         HIP_TRY(hipStreamWaitEvent(c->stream, done, 0));
-        ST_TRY(exchange(c, A, xbuf(j)));
       } else {
         ST_TRY(update_gemv(j, p, y, c->stream2));
         // cross-stream order through a stream memory write / wait on a device word (~1.5% faster
@@ -2535,7 +2541,6 @@ struct Solver {
         ++c->gemv_seq;
         HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
         HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
-        ST_TRY(exchange(c, A, xbuf(j)));
       }
     } else {
       ST_TRY(update_gemv(j, p, y));
@@ -2649,6 +2654,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       HIP_TRY(launch_copy(n, x0, ws->xj, s));
       ST_TRY(exchange(c, A, ws->xj));
       xr0 = ws->xj;
+      // x0's ghost rows for the update GEMV over n_gx() rows
+      if (S.n_gx() > n) HIP_TRY(launch_copy(S.n_gx() - n, ws->xj + n, ws->x0 + n, s));
     }
     HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s));
     ST_TRY(allreduce(c, c->partA, S.gs));

@@ -62,6 +62,7 @@ _OPTIONS = {
     "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
     "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
     "spmv_nt": (_lib.OPT_SPMV_NT, {False: 0, True: 1, "auto": 2}),
+    "k7t_slots": (_lib.OPT_K7T_SLOTS, {16: 16, 32: 32}),
 }
 
 
@@ -97,7 +98,13 @@ def set_option(name, value, ctx=None):
       the device (K8), False by its host ``pre.solve`` through the callback (as the reference
       does), "auto" on the device when the plan's cost model predicts it is faster
       (``DeviceILU.predicted_ms``: shallow level structures; deep dependency chains stay on the
-      host, where a sequential sweep is faster than any level-by-level GPU schedule)."""
+      host, where a sequential sweep is faster than any level-by-level GPU schedule);
+    * ``dist_mgs`` ("one_reduce"): several GPUs, MGS's projections in inverse-compact-WY form
+      (K2w: 2 all-reduces per Arnoldi step; MGS in exact arithmetic, not its rounding), or
+      "per_step" (MGS's j + 2 all-reduces, its rounding);
+    * ``spmv_nt`` (False): nontemporal matrix-stream loads in the pipelined SpMV (True: always;
+      "auto": when values + columns exceed the 256 MB Infinity Cache); results identical;
+    * ``k7t_slots`` (16): K7t slot-table width, 16 or 32 (32 measured slower; kept for tests)."""
     ctx = ctx or get_context()
     if name == "device_ilu":
         if value not in (True, False, "auto"):

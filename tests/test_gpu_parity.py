@@ -380,18 +380,20 @@ def test_constraint_terms_kernels_vs_reference(spis, mode):
         set_option("ell_gram", "mfma")
 
 
-def test_k7t_waves_walk_many_blocks(spis):
+@pytest.mark.parametrize("M,slots", [(128, 16), (128, 32), (289, 16), (289, 32)])
+def test_k7t_waves_walk_many_blocks(spis, M, slots):
     """K7t (symmetric constraint matrix, f64 MFMA from the slot table) at p + 1 = 32, where each
-    wave walks ~13 table blocks (swe energy matrix at M = 128: ~27k blocks over the resident
-    waves) through its two-ahead table prefetch (cur / nxt / nx2): against constraint_container's
-    host algebra (solvers.py:33-36) and against K7m on the same inputs.  (Round 2 removed a 32-slot
-    variant that was wrong when waves walked several blocks; this pins the shipping 16-slot walk
-    in that regime.)"""
+    wave walks many table blocks (swe energy matrix: M = 128 ~13 blocks per wave at 16 slots,
+    M = 289 (C3) ~67) through its two-ahead table prefetch (cur / nxt / nx2): against
+    constraint_container's host algebra (solvers.py:33-36) and against K7m on the same inputs.
+    Round 2 removed a 32-slot variant that was wrong at C3 when waves walked several blocks (its
+    code was never committed); the shipping kernel is a template on the slot count, so the same
+    walk is checked here at 32 slots (SPIS_OPT_K7T_SLOTS) as well as at the default 16."""
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.device import set_option
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
 
-    dic, _ = sa.linforms(M=128)
+    dic, _ = sa.linforms(M=M)
     n = dic["A"].shape[0]
     rng = np.random.default_rng(11)
 
@@ -411,10 +413,12 @@ def test_k7t_waves_walk_many_blocks(spis):
     got = {}
     for mode in ("mfma", "mfma_full"):  # K7t, then K7m for every matrix
         set_option("ell_gram", mode)
+        set_option("k7t_slots", slots)
         try:
             t = solvers.constraint_container(con, x0, Z)
         finally:
             set_option("ell_gram", "mfma")
+            set_option("k7t_slots", 16)
         got[mode] = t
         scale = np.abs(Mv).sum() * np.abs(Z).max() ** 2 * 1e-13
         np.testing.assert_allclose(t.term2, ref_t2, rtol=1e-11, atol=scale)
