@@ -2211,13 +2211,16 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
 // one workgroup: the 2 nv - 1 dots (already reduced: one value each), the newest Gram row into G
 // (row-major kCgsMax x kCgsMax; rows < nv - 1 were written by the earlier steps of this solve),
 // then h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l order -> coef (device, cgs_update's
-// input) and h_out (the host H column).  The Gram triangle is staged in LDS first: the recurrence
-// is one thread's sequential chain (~nv^2 / 2 dependent FMAs), and read from global memory each
-// operand cost a load latency (icwy 38 us per step at nv ~ 15 in the first version)
+// input) and h_out (the host H column).  The Gram triangle is staged in LDS, and the forward
+// substitution runs column by column on one wave: lane i holds t_i and, once h_l = t_l is
+// broadcast, subtracts h_l G(i, l) — for every i the same subtractions in the same m order as the
+// row-by-row recurrence, so the same bits.  (Thread 0 running the recurrence with h[] in private
+// memory took 17 us per step: the dynamically indexed array lived in scratch.)
 __global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restrict__ d, int nv,
                                                            double* __restrict__ G, double* __restrict__ coef,
                                                            double* __restrict__ h_out) {
 #pragma clang fp contract(off)
+  static_assert(kCgsMax <= 64, "one lane per coefficient");
   __shared__ double s_g[kCgsMax * kCgsMax];
   __shared__ double s_d[2 * kCgsMax];
   for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = d[i];
@@ -2228,15 +2231,16 @@ __global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restr
     G[static_cast<int64_t>(nv - 1) * kCgsMax + i] = s_d[nv + i];
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double h[kCgsMax];
-    for (int l = 0; l < nv; ++l) {
-      double t = s_d[l];
-      const double* gl = s_g + l * kCgsMax;
-      for (int m = 0; m < l; ++m) t -= h[m] * gl[m];
-      h[l] = t;
-      coef[l] = t;
-      h_out[l] = t;
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    double t = i < nv ? s_d[i] : 0.0;
+    for (int l = 0; l + 1 < nv; ++l) {
+      const double hl = __shfl(t, l, 64);  // h_l: t_l is final once columns 0 .. l-1 are applied
+      if (i > l && i < nv) t -= hl * s_g[i * kCgsMax + l];
+    }
+    if (i < nv) {
+      coef[i] = t;
+      h_out[i] = t;
     }
   }
 }

@@ -177,7 +177,16 @@ class Comm:
         import torch.distributed as dist
 
         if not dist.is_initialized():
-            dist.init_process_group("gloo", init_method="env://")
+            if "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+                # a plain `python` process (no launcher): a one-rank group on a free local port
+                import socket
+
+                with socket.socket() as s:
+                    s.bind(("127.0.0.1", 0))
+                    port = s.getsockname()[1]
+                dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+            else:
+                dist.init_process_group("gloo", init_method="env://")
         self.dist = dist
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
@@ -363,6 +372,11 @@ def bench_main(args, metric):
     if getattr(args, "orthog", "mgs") == "cgs2":
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_DIST_MGS, getattr(args, "dist_mgs", 1)), "spis_set_option")
+    if hasattr(args, "gemv_sync"):  # bench.py's shared solver flags
+        ov = 0 if args.no_overlap else args.gemv_sync
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, ov), "spis_set_option")
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
     bd = sysd.vector(wl["b"])
     x0d = DeviceVector.from_host(np.zeros(sysd.n_local), ctx=ctx)
     conlist = distribute_constraints(sysd, wl["conlist"])
