@@ -144,8 +144,12 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 // reduces vector i's partials into c[i] and, with h_out, writes add[i] + c[i] there.
 hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
                           hipStream_t s, const LaunchEv* ev = nullptr);
+// px > 0 (dot = false): the same pass also writes xo = Q[:, :px] yx + x0 over rows [0, n_gx) (yx on
+// the host, px <= kYArg; rows >= n are ghost rows, whose basis entries the halo exchange filled)
 hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
-                             bool dot, double* part, int grid, hipStream_t s, bool nt = false);
+                             bool dot, double* part, int grid, hipStream_t s, bool nt = false, int px = 0,
+                             const double* yx = nullptr, const double* x0 = nullptr, double* xo = nullptr,
+                             int64_t n_gx = 0);
 // K2w (multi-GPU MGS, one reduction for the projections): partials of q_l . w (l < nv) and of
 // q_l . q_{nv-1} (l < nv - 1) -> part rows [0, nv) and [nv, 2 nv - 1), grid columns each
 // nt: nontemporal basis loads (the matrix stays Infinity-Cache resident between SpMVs, as K2q's)

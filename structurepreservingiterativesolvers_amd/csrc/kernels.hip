@@ -1975,13 +1975,22 @@ __global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double
   }
 }
 
-template <int DOT, bool NT = false>
+// FX (several GPUs, L mode; DOT = 0): the same pass also forms U_{px-1}'s iterate
+// x = Z[:, :px] y + x0 (Z = Q, px <= nv) from the basis values it already holds: each wave sums
+// its vectors' y_l q_l (l = wid, wid + 4, ... with fma, in that order), the four wave sums combine
+// through LDS in wave order, then + x0; rows [n, n_gx) (x's ghost rows, from the basis vectors'
+// ghost entries) by the same arithmetic one row per thread, so a rank's ghost copy of x equals its
+// owner's bitwise and x needs no halo exchange
+template <int DOT, bool NT = false, bool FX = false>
 __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* __restrict__ w,
                                                             const double* __restrict__ Q, int64_t pitch, int nv,
                                                             const double* __restrict__ coef,
-                                                            double* __restrict__ part) {
+                                                            double* __restrict__ part, int px, YArg yx,
+                                                            const double* __restrict__ x0, double* __restrict__ xo,
+                                                            int64_t n_gx) {
   __shared__ double s_c[kCgsMax];
   __shared__ double s_sum[4][4][64];  // [wave][element slot][lane]
+  __shared__ double s_x[FX ? 4 : 1][4][64];
   __shared__ double s_wave[4];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1992,7 +2001,7 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
   for (int m = 0; m < kCgsPerWave; ++m) acc[m] = 0.0;
   const double* Qw = Q + wid * pitch;
   const int64_t step = 4 * pitch;
-  const bool vec = aligned16d(w) && aligned16d(Q) && (pitch % 2 == 0);
+  const bool vec = aligned16d(w) && aligned16d(Q) && (pitch % 2 == 0) && (!FX || (aligned16d(x0) && aligned16d(xo)));
   const int64_t n_vec = vec ? (n / kCgsChunk) * kCgsChunk : 0;
   // w' = w - Q c: each wave sums its vectors' share (basis order within the wave), the 4 shares
   // combine in a fixed order through LDS (every wave gets the same w'); wave 0 stores it
@@ -2001,6 +2010,7 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     const int64_t e = e0 + 2 * lane;
     double2 qa[kCgsPerWave], qb[kCgsPerWave];
     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
 #pragma unroll
     for (int m = 0; m < kCgsPerWave; ++m) {
       if (wid + 4 * m < nv) {
@@ -2012,6 +2022,13 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
         p1 += cm * qa[m].y;
         p2 += cm * qb[m].x;
         p3 += cm * qb[m].y;
+        if (FX && wid + 4 * m < px) {
+          const double ym = yx.v[wid + 4 * m];
+          g0 = fma(ym, qa[m].x, g0);
+          g1 = fma(ym, qa[m].y, g1);
+          g2 = fma(ym, qb[m].x, g2);
+          g3 = fma(ym, qb[m].y, g3);
+        }
       } else {
         qa[m] = make_double2(0.0, 0.0);
         qb[m] = make_double2(0.0, 0.0);
@@ -2023,6 +2040,12 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     s_sum[wid][1][lane] = p1;
     s_sum[wid][2][lane] = p2;
     s_sum[wid][3][lane] = p3;
+    if (FX) {
+      s_x[wid][0][lane] = g0;
+      s_x[wid][1][lane] = g1;
+      s_x[wid][2][lane] = g2;
+      s_x[wid][3][lane] = g3;
+    }
     __syncthreads();
     double t[4];
 #pragma unroll
@@ -2035,6 +2058,16 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     if (wid == 0) {
       *reinterpret_cast<double2*>(w + e) = make_double2(t[0], t[1]);
       *reinterpret_cast<double2*>(w + e + 128) = make_double2(t[2], t[3]);
+    }
+    if (FX && wid == 1) {
+      double xs[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
+      const double2 ba = *reinterpret_cast<const double2*>(x0 + e);
+      const double2 bb = *reinterpret_cast<const double2*>(x0 + e + 128);
+      *reinterpret_cast<double2*>(xo + e) = make_double2(xs[0] + ba.x, xs[1] + ba.y);
+      *reinterpret_cast<double2*>(xo + e + 128) = make_double2(xs[2] + bb.x, xs[3] + bb.y);
     }
     if (DOT) {
 #pragma unroll
@@ -2057,17 +2090,21 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     const int64_t e = e0 + lane;
     const bool ok = e < n;
     double q[kCgsPerWave];
-    double ps = 0.0;
+    double ps = 0.0, gs = 0.0;
 #pragma unroll
     for (int m = 0; m < kCgsPerWave; ++m) {
       q[m] = (ok && wid + 4 * m < nv) ? Qw[m * step + e] : 0.0;
       if (wid + 4 * m < nv) ps += s_c[wid + 4 * m] * q[m];
+      if (FX && wid + 4 * m < px) gs = fma(yx.v[wid + 4 * m], q[m], gs);
     }
     const double we = ok ? w[e] : 0.0;
     s_sum[wid][0][lane] = ps;
+    if (FX) s_x[wid][0][lane] = gs;
     __syncthreads();
     const double t = we - (((s_sum[0][0][lane] + s_sum[1][0][lane]) + s_sum[2][0][lane]) + s_sum[3][0][lane]);
     if (wid == 0 && ok) w[e] = t;
+    if (FX && wid == 1 && ok)
+      xo[e] = (((s_x[0][0][lane] + s_x[1][0][lane]) + s_x[2][0][lane]) + s_x[3][0][lane]) + x0[e];
     if (DOT) {
 #pragma unroll
       for (int m = 0; m < kCgsPerWave; ++m) acc[m] += q[m] * t;
@@ -2075,6 +2112,19 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
       acc[0] += t * t;
     }
     __syncthreads();
+  }
+  if (FX) {  // x's ghost rows: the four wave sums in wave order, each over its vectors in order
+    for (int64_t e = n + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n_gx;
+         e += static_cast<int64_t>(gridDim.x) * kBlock) {
+      double sw[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        double g = 0.0;
+        for (int l = v; l < px; l += 4) g = fma(yx.v[l], Q[static_cast<int64_t>(l) * pitch + e], g);
+        sw[v] = g;
+      }
+      xo[e] = (((sw[0] + sw[1]) + sw[2]) + sw[3]) + x0[e];
+    }
   }
   if (DOT) {
 #pragma unroll
@@ -2112,14 +2162,31 @@ hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t p
 }
 
 hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
-                             bool dot, double* part, int grid, hipStream_t s, bool nt) {
+                             bool dot, double* part, int grid, hipStream_t s, bool nt, int px, const double* yx,
+                             const double* x0, double* xo, int64_t n_gx) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
+  YArg ya;
+  const bool fx = px > 0;
+  if (fx) {
+    if (dot || px > nv || px > kYArg || yx == nullptr || x0 == nullptr || xo == nullptr || n_gx < n)
+      return hipErrorInvalidValue;
+    for (int i = 0; i < px; ++i) ya.v[i] = yx[i];
+  }
   if (dot)
-    hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+    hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
+                       x0, xo, n_gx);
+  else if (fx && nt)
+    hipLaunchKernelGGL((cgs_update_kernel<0, true, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
+                       part, px, ya, x0, xo, n_gx);
+  else if (fx)
+    hipLaunchKernelGGL((cgs_update_kernel<0, false, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
+                       part, px, ya, x0, xo, n_gx);
   else if (nt)
-    hipLaunchKernelGGL((cgs_update_kernel<0, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+    hipLaunchKernelGGL((cgs_update_kernel<0, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part,
+                       0, ya, x0, xo, n_gx);
   else
-    hipLaunchKernelGGL(cgs_update_kernel<0>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part);
+    hipLaunchKernelGGL(cgs_update_kernel<0>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
+                       x0, xo, n_gx);
   return hipGetLastError();
 }
 

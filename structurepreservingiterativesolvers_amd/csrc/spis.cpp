@@ -2202,8 +2202,13 @@ struct Solver {
   }
   bool lag_chain() const {
     // K2q pads an odd n's last pair: its capacity test counts (n + 1) / 2 pairs, as the launch does
-    return c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8;
+    return (c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8) ||
+           icwy_lag();
   }
+  // several GPUs: L mode on the one-reduce MGS (K2w) — every step of the solve takes it (k <=
+  // kCgsMax), its coefficient kernel and normalise publish H[:, j] to pinned memory (the
+  // normalise's system-scope store of H[j+1, j] last), and its update pass carries U_{j-1}'s GEMV
+  bool icwy_lag() const { return c->comm && c->dist_mgs == 1 && !c->cgs2 && k <= kCgsMax; }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
   void arm_hcol(int j) {  // before A_j's chain is enqueued
     *reinterpret_cast<volatile uint64_t*>(c->pinned + hoff(j) + j + 1) = kHSentinel;
@@ -2259,7 +2264,7 @@ struct Solver {
                    unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr,
                    const double* yx = nullptr, int jx = -1) {
     if (c->cgs2 && j + 1 <= kCgsMax) return arnoldi_post_cgs2(j, xpart, x_out, flag, seq);
-    if (c->comm && c->dist_mgs == 1 && j + 1 <= kCgsMax) return arnoldi_post_icwy(j, xpart, x_out, flag, seq);
+    if (c->comm && c->dist_mgs == 1 && j + 1 <= kCgsMax) return arnoldi_post_icwy(j, xpart, x_out, flag, seq, yx, jx);
     hipStream_t s = c->stream;
     c->prof_iter = j;
     ST_TRY(allreduce(c, c->partA, gs));
@@ -2311,10 +2316,14 @@ struct Solver {
   // partials in a fixed order first, so each all-reduce carries 2 j + 1 doubles (resp. one): the
   // latency of a few bytes, not of a kRedGrid-long partial array per dot.
   int arnoldi_post_icwy(int j, const double* xpart, double* x_out, unsigned long long* flag,
-                        const unsigned long long* seq) {
+                        const unsigned long long* seq, const double* yx = nullptr, int jx = -1) {
     hipStream_t s = c->stream;
     c->prof_iter = j;
-    if (xpart) HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
+    if (icwy_lag()) arm_hcol(j);
+    if (xpart) {  // U_{j-2}'s residual (L mode): partials all-reduced, then reduced and published
+      ST_TRY(allreduce(c, const_cast<double*>(xpart), gs));
+      HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
+    }
     const int nv = j + 1;
     double* hcol = c->pinned_dev + hoff(j);
     const int gc = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 63) / 64)));
@@ -2327,7 +2336,11 @@ struct Solver {
     HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
     ST_TRY(allreduce(c, d, 2 * nv - 1));
     HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
-    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s, nt));
+    // L mode: U_jx's GEMV in the same pass (x_jx = Z y + x0 over the local and ghost rows)
+    const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
+    if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
+    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s, nt, px, yx, ws->x0,
+                              px > 0 ? xbuf(jx) : nullptr, n_gx()));
     // ||w'||^2: the gc partials all-reduced element-wise (8 KB, latency-bound like one double) and
     // summed in fixed order by every normalize workgroup: no finalize launch in between
     ST_TRY(allreduce(c, c->partB, gc));
@@ -2404,6 +2417,7 @@ struct Solver {
   }
   // U_j's residual partials (from [U_j res | a_{j+2}]) reduced and published without a chain
   int enqueue_finalize(int j) {
+    ST_TRY(allreduce(c, c->partR, gs));
     HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
     return SPIS_OK;
   }
@@ -2415,6 +2429,7 @@ struct Solver {
       HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, xbuf(j), nullptr, b, c->partR, gs, c->stream, &le));
     }
     next_seq(j);
+    ST_TRY(allreduce(c, c->partR, gs));
     HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
     return SPIS_OK;
   }
