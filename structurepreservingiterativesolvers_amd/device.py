@@ -43,6 +43,11 @@ class Context:
         """Destroy the context; device objects still alive become inert (their finalizers
         see the closed context and do nothing)."""
         if self.handle:
+            for (cid, _), ptrs in list(_POOL.items()):
+                if cid == id(self):
+                    for p in ptrs:
+                        self.L.spis_free(self.handle, C.c_void_p(p))
+                    ptrs.clear()
             self.L.spis_context_destroy(self.handle)
             self.handle = None
 
@@ -168,12 +173,47 @@ class DeviceBuffer:
         return out
 
 
+# recycled allocations of solver outputs (DeviceVector.scratch): a solve's result vector is
+# dropped by the time the next solve asks for one, and hipMalloc + the zeroing memset cost
+# ~20-60 us per solve call (C3: ~2% of a solve).  Reuse is stream-ordered: every libspis
+# operation of a context runs on its one stream.
+_POOL: dict = {}
+_POOL_MAX = 4
+
+
+def _pool_release(ctx, n, ptr):
+    if not ctx.handle:
+        return
+    lst = _POOL.setdefault((id(ctx), n), [])
+    if len(lst) < _POOL_MAX:
+        lst.append(ptr)
+    else:
+        ctx.L.spis_free(ctx.handle, C.c_void_p(ptr))
+
+
 class DeviceVector(DeviceBuffer):
     """An fp64 vector resident in HBM (length ``n``, room for ``capacity``)."""
 
     def __init__(self, ctx: Context, n: int, capacity: int | None = None):
         super().__init__(ctx, n if capacity is None else max(n, capacity))
         self.n_valid = int(n)
+
+    @classmethod
+    def scratch(cls, ctx: Context, n: int):
+        """A length-``n`` vector with unspecified contents, from the context's pool of released
+        ones when there is one (for outputs a kernel overwrites whole)."""
+        n = int(n)
+        lst = _POOL.get((id(ctx), n))
+        obj = cls.__new__(cls)
+        obj.ctx, obj.n, obj.n_valid = ctx, n, n
+        if lst:
+            obj.ptr = lst.pop()
+        else:
+            p = C.c_void_p()
+            _lib.check(ctx.L.spis_malloc(ctx.handle, 8 * max(n, 1), C.byref(p)), "spis_malloc")
+            obj.ptr = p.value
+        obj._fin = weakref.finalize(obj, _pool_release, ctx, n, obj.ptr)
+        return obj
 
     @classmethod
     def from_host(cls, arr, ctx=None, capacity=None):

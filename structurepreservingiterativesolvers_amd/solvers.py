@@ -33,6 +33,7 @@ from __future__ import annotations
 import collections.abc
 import ctypes as C
 import logging
+import threading
 import warnings
 
 import numpy as np
@@ -375,6 +376,32 @@ def _as_slsqp(cc):
 # ------------------------------------------------------------------------------------------------
 # the call
 # ------------------------------------------------------------------------------------------------
+_OUT = threading.local()
+_NO_CONLS = _lib.CONLS_FN()  # the null callback (class-form or no constraints)
+
+
+def _out_buffers(k):
+    """(float buffer: res | y | stamps, int32 buffer: branch | events | msg, SolveOut pointing
+    at them) for CGMRES(k), built once per thread and k: building the ctypes pointers costs
+    more per call than the copies of the results do."""
+    cache = getattr(_OUT, "bufs", None)
+    if cache is None:
+        cache = _OUT.bufs = {}
+    hit = cache.get(k)
+    if hit is None:
+        fbuf = np.zeros(k + 1 + k * k + 4 * k + 2)
+        ibuf = np.zeros(3 * k, dtype=np.int32)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        fa, ia = fbuf.ctypes.data, ibuf.ctypes.data
+        out = _lib.SolveOut(
+            steps=0, n_res=0, res_host=C.cast(fa, dp), y_host=C.cast(fa + 8 * (k + 1), dp),
+            branch_host=C.cast(ia, ip), events_host=C.cast(ia + 4 * k, ip), msg_host=C.cast(ia + 8 * k, ip),
+            stamps_host=C.cast(fa + 8 * (k + 1 + k * k), dp), x_final_dev=None,
+        )
+        hit = cache[k] = (fbuf, ibuf, out)
+    return hit
+
+
 def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     # a device matrix carries its context (distributed rank / communicator); else the default one
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
@@ -392,7 +419,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     pre_mat, pre_fn, pre_ilu = _precond_setup(pre, n, ctx, keep)
     conlist = list(conlist)
     descs = None
-    conls = _lib.CONLS_FN()
+    conls = _NO_CONLS
     if conlist:
         kinds = ["class" if hasattr(c, "__dict__") else "dict" if type(c) is dict else "bad" for c in conlist]
         if all(kd == "class" for kd in kinds):
@@ -411,19 +438,11 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
         n_constraints=len(conlist), constraints=descs, pre_matrix=pre_mat, pre_fn=pre_fn, pre_user=None, pre_ilu=pre_ilu,
         conls_fn=conls, conls_user=None,
     )
-    res = np.zeros(k + 1)
-    ys = np.zeros(k * k)
-    br = np.zeros(k, dtype=np.int32)
-    ev = np.zeros(k, dtype=np.int32)
-    msg = np.zeros(k, dtype=np.int32)
-    stamps = np.zeros(4 * k + 2)
-    xf = DeviceVector(ctx, n)
-    out = _lib.SolveOut(
-        steps=0, n_res=0, res_host=res.ctypes.data_as(C.POINTER(C.c_double)),
-        y_host=ys.ctypes.data_as(C.POINTER(C.c_double)), branch_host=br.ctypes.data_as(C.POINTER(C.c_int32)),
-        events_host=ev.ctypes.data_as(C.POINTER(C.c_int32)), msg_host=msg.ctypes.data_as(C.POINTER(C.c_int32)),
-        stamps_host=stamps.ctypes.data_as(C.POINTER(C.c_double)), x_final_dev=xf.ptr,
-    )
+    fbuf, ibuf, out = _out_buffers(k)
+    fbuf.fill(0.0)
+    ibuf.fill(0)
+    xf = DeviceVector.scratch(ctx, n)  # overwritten whole by the solve (x[-1], or x0 on breakdown)
+    out.steps, out.n_res, out.x_final_dev = 0, 0, xf.ptr
     ws = C.c_void_p()
     status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
                               C.byref(out), C.byref(ws))
@@ -431,6 +450,9 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
         if isinstance(item, list) and item:
             raise item[0]
     _lib.check(status, "spis_solve")
+    # the per-thread output buffers are reused by the next call: the results are copies
+    res, ys, stamps = fbuf[:k + 1].copy(), fbuf[k + 1:k + 1 + k * k].copy(), fbuf[k + 1 + k * k:].copy()
+    br, ev, msg = ibuf[:k].copy(), ibuf[k:2 * k].copy(), ibuf[2 * k:].copy()
     n_iter = out.n_res - 1
     final = xf if device_io else xf.numpy()
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
