@@ -56,11 +56,17 @@ def mgs_chain_bytes(n, k, chain):
       K2p (chain 1-2, N/2 <= 2^19): 8 N (j + 3);
       K2b (chain >= 2 beyond): 16 N (j + 1) + 16 N (q_i and q_{i+1} streamed per MGS step, w
           read once, q_{j+1} written);
+      one-reduce two-pass MGS (chain 4, and chain 3 beyond K2q): 8 N (j + 2) for the dots (w,
+          q_0 .. q_j) + 8 N (j + 3) for the update (q_0 .. q_j and w read, w written) + 16 N for
+          the update GEMV it carries from j >= 1 + 16 N for the normalise;
       per-step launches (chain 0): 32 N (j + 1) + 16 N (y, q_i, q_{i+1} read, y written; the
           normalise reads y, writes q)."""
     tot = 0.0
+    k2q = (n + 1) // 2 <= 255 * 512 * 4
     for j in range(k):
-        if chain == 3 and (n + 1) // 2 <= 255 * 512 * 4:
+        if chain == 4 or (chain == 3 and not k2q):
+            b = 8 * n * (j + 2) + 8 * n * (j + 3) + (16 * n if j >= 1 else 0) + 16 * n
+        elif chain == 3:
             b = 8 * n * (j + 3) + (16 * n if j >= 1 else 0)
         elif chain >= 1 and n // 2 <= 256 * 256 * 8 and not (chain >= 2 and n // 2 > 255 * 256 * 8):
             b = 8 * n * (j + 3)
@@ -184,9 +190,10 @@ def main():
     ap.add_argument("--gemv-sync", type=int, default=1, choices=[1, 2],
                     help="how the dual SpMV waits for the side-stream GEMV (SPIS_OPT_OVERLAP_GEMV): "
                          "1 stream write/wait on a device word, 2 the GEMV launch's completion event")
-    ap.add_argument("--chain", type=int, default=3, choices=[0, 1, 2, 3],
+    ap.add_argument("--chain", type=int, default=3, choices=[0, 1, 2, 3, 4],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
-                         "workgroup 0, 2 with a dedicated gathering workgroup, 3 pipelined (dots one step early)")
+                         "workgroup 0, 2 with a dedicated gathering workgroup, 3 pipelined (dots one step early), "
+                         "4 one-reduce two-pass MGS carrying the update GEMV")
     ap.add_argument("--nt-basis", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
     ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],

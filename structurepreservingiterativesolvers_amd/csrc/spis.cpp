@@ -768,7 +768,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->ell_gram = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN:
-        if (value < 0 || value > 3) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0, 1, 2 or 3", (long long)value);
+        if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0 .. 4", (long long)value);
         c->mgs_chain = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_OVERLAP_GEMV:
@@ -2200,15 +2200,19 @@ struct Solver {
     const double ws_bytes = 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * (k + 1) * static_cast<double>(n);
     return c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
   }
-  bool lag_chain() const {
-    // K2q pads an odd n's last pair: its capacity test counts (n + 1) / 2 pairs, as the launch does
-    return (c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8) ||
-           icwy_lag();
-  }
+  bool lag_chain() const { return (c->mgs_chain == 3 && !fixed_grid(c) && !c->cgs2 && k2q_fits()) || icwy_lag(); }
+  // K2q pads an odd n's last pair: its capacity test counts (n + 1) / 2 pairs, as the launch does
+  bool k2q_fits() const { return ((n + 1) >> 1) <= (kChainMaxWG - 1) * int64_t(kBlock) * 8; }
   // several GPUs: L mode on the one-reduce MGS (K2w) — every step of the solve takes it (k <=
   // kCgsMax), its coefficient kernel and normalise publish H[:, j] to pinned memory (the
   // normalise's system-scope store of H[j+1, j] last), and its update pass carries U_{j-1}'s GEMV
-  bool icwy_lag() const { return c->comm && c->dist_mgs == 1 && !c->cgs2 && k <= kCgsMax; }
+  bool icwy_lag() const { return icwy_on() && !c->cgs2 && k <= kCgsMax; }
+  // K2w: several GPUs (SPIS_OPT_DIST_MGS 1), or one GPU with SPIS_OPT_MGS_CHAIN 4, or 3 beyond
+  // K2q's capacity: two passes over the basis per step, the second carrying the update GEMV, in
+  // place of K2b + a separate GEMV pass (C5: 826 -> 902 it/s; FX does not fit K2b's registers)
+  bool icwy_on() const {
+    return c->comm ? c->dist_mgs == 1 : (c->mgs_chain == 4 || (c->mgs_chain == 3 && !c->cgs2 && !k2q_fits()));
+  }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
   void arm_hcol(int j) {  // before A_j's chain is enqueued
     *reinterpret_cast<volatile uint64_t*>(c->pinned + hoff(j) + j + 1) = kHSentinel;
@@ -2264,7 +2268,7 @@ struct Solver {
                    unsigned long long* flag = nullptr, const unsigned long long* seq = nullptr,
                    const double* yx = nullptr, int jx = -1) {
     if (c->cgs2 && j + 1 <= kCgsMax) return arnoldi_post_cgs2(j, xpart, x_out, flag, seq);
-    if (c->comm && c->dist_mgs == 1 && j + 1 <= kCgsMax) return arnoldi_post_icwy(j, xpart, x_out, flag, seq, yx, jx);
+    if (icwy_on() && j + 1 <= kCgsMax) return arnoldi_post_icwy(j, xpart, x_out, flag, seq, yx, jx);
     hipStream_t s = c->stream;
     c->prof_iter = j;
     ST_TRY(allreduce(c, c->partA, gs));

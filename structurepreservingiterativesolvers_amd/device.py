@@ -58,7 +58,8 @@ _OPTIONS = {
     "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
     "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}),
-    "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 3, "gather0": 1, "aggregator": 2, "pipelined": 3}),
+    "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 3, "gather0": 1, "aggregator": 2, "pipelined": 3,
+                                       "one_reduce": 4}),
     "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
     "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False

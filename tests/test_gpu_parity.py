@@ -246,9 +246,10 @@ def _run_package(spis, case):
     return solvers.cgmres(case.A, case.b, x0, m["k"], tol=m["tol"], conlist=case.conlist(), pre=pre, **kw)
 
 
-@pytest.fixture(params=["aggregator", "pipelined"])
+@pytest.fixture(params=["aggregator", "pipelined", "one_reduce"])
 def chain_mode(request, spis):
-    """The pipelined MGS chain (the default, SPIS_OPT_MGS_CHAIN = 3) and the plain one (2)."""
+    """The pipelined MGS chain (the default, SPIS_OPT_MGS_CHAIN = 3), the plain one (2), and the
+    one-reduce two-pass MGS with the fused update GEMV (4: the several-GPU kernels on one GPU)."""
     from structurepreservingiterativesolvers_amd.device import set_option
 
     set_option("mgs_chain", request.param)
@@ -945,7 +946,16 @@ def test_full_size_swe_c5_restarted_properties(spis):
         sol = _slsqp(func, y0, jac, cl, 1e-24)
         assert max(f["fun"](sol.x) for f in cl) <= 1e-12, c  # the reference keeps the step
         yd = xs.y[k - 1]
-        assert func(yd) <= func(sol.x) * (1 + 1e-10), (c, func(yd), func(sol.x))
+        # the device stops each constraint 8 eps x its rounding scale inside the feasible side (so
+        # that the reference's signed checker, solvers.py:14-18,267, passes on the computed
+        # value); that margin may cost the objective up to sum |lambda_i| x 16 eps x scale_i
+        eps = np.finfo(float).eps
+        gf = jac(yd)
+        G = np.stack([b + 2 * (yd @ cc) for _, b, cc in terms], 1)
+        lam = np.linalg.lstsq(G, -gf, rcond=None)[0]
+        scale = [abs(a) + np.abs(b) @ np.abs(yd) + np.abs(yd) @ np.abs(cc) @ np.abs(yd) for a, b, cc in terms]
+        margin = sum(abs(li) * 16 * eps * si for li, si in zip(lam, scale))
+        assert func(yd) <= func(sol.x) * (1 + 1e-10) + margin, (c, func(yd), func(sol.x), margin)
         assert np.linalg.norm(yd - sol.x) <= 1e-6 * np.linalg.norm(sol.x), c
         xs.release()
     _assert_invariants(cons, x)
@@ -1092,9 +1102,9 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
     b = rng.standard_normal(n)
     k = 12
     runs = []
-    # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 3: pipelined (K2q; K2b
-    # beyond 2^20); 0: per-step launches
-    modes = (1, 1, 2, 2, 3, 3, 0) if n <= 2_000_001 else (2, 2, 3, 3, 0)
+    # 1: gathered by workgroup 0; 2: by a dedicated gathering workgroup; 3: pipelined (K2q; the
+    # one-reduce MGS beyond its capacity); 4: one-reduce two-pass MGS; 0: per-step launches
+    modes = (1, 1, 2, 2, 3, 3, 4, 4, 0) if n <= 2_000_001 else (2, 2, 3, 3, 4, 4, 0)
     for chain in modes:
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
         try:
