@@ -147,7 +147,11 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  *   so results differ from the per-step launches at roundoff level.  3 = the pipelined chain:
  *   MGS's projections and updates, each dot product evaluated one step early by the distributive
  *   law (h_{i+1} = q_{i+1}.w^{(i)} - h_i q_{i+1}.q_i), so two exchanges overlap; roundoff differs
- *   from MGS's (N <= 2^20 - 4096; mode 2's K2b beyond).
+ *   from MGS's (N <= 2^20 - 4096; beyond, mode 4).  4 = the one-reduce two-pass MGS (the
+ *   several-GPU K2w: every q_l.w and the newest Gram row in one pass, the projections by the
+ *   distributive law, then the update pass, which also forms the previous iteration's update
+ *   GEMV); MGS in exact arithmetic, not its rounding; k <= 32.  Mode 3 takes it beyond K2q's
+ *   capacity, where it replaces K2b + a separate GEMV pass (C5: 826 -> 921 it/s).
  * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
  *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
  *   The dual SpMV waits for it through a stream write / wait on a device word (1) or through the

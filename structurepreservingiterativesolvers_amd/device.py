@@ -88,8 +88,10 @@ def set_option(name, value, ctx=None):
     * ``mgs_chain`` (True = "pipelined"): each Arnoldi step's MGS chain + normalise as one persistent
       launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
       ("gather0"); "pipelined": each dot product one MGS step early by the distributive law
-      (h_{i+1} = q_{i+1}.w^(i) - h_i q_{i+1}.q_i), two exchanges in flight (not MGS's rounding);
-      False = one launch per MGS step;
+      (h_{i+1} = q_{i+1}.w^(i) - h_i q_{i+1}.q_i), two exchanges in flight (not MGS's rounding),
+      and beyond its capacity (N > ~1.04M) the one-reduce MGS; "one_reduce": two passes per
+      step (every q_l.w and the newest Gram row, then the update carrying the previous
+      iteration's GEMV), k <= 32; False = one launch per MGS step;
     * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
     * ``nt_basis`` ("auto"): the MGS chain's basis loads are nontemporal when the matrix and the
       basis exceed the 256 MB Infinity Cache (True: always; False: never), results identical;
