@@ -402,7 +402,18 @@ def _out_buffers(k):
     return hit
 
 
+_CHECKPOINTS = None  # tools/host_overhead.py: a list to collect perf_counter() stamps of _run's phases
+
+
+def _cp():
+    if _CHECKPOINTS is not None:
+        import time
+
+        _CHECKPOINTS.append(time.perf_counter())
+
+
 def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
+    _cp()
     # a device matrix carries its context (distributed rank / communicator); else the default one
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
     Ad = device_matrix(A, ctx=ctx)
@@ -438,14 +449,17 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
         n_constraints=len(conlist), constraints=descs, pre_matrix=pre_mat, pre_fn=pre_fn, pre_user=None, pre_ilu=pre_ilu,
         conls_fn=conls, conls_user=None,
     )
+    _cp()
     fbuf, ibuf, out = _out_buffers(k)
     fbuf.fill(0.0)
     ibuf.fill(0)
     xf = DeviceVector.scratch(ctx, n)  # overwritten whole by the solve (x[-1], or x0 on breakdown)
     out.steps, out.n_res, out.x_final_dev = 0, 0, xf.ptr
     ws = C.c_void_p()
+    _cp()
     status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
                               C.byref(out), C.byref(ws))
+    _cp()
     for item in keep:  # a Python exception inside a callback is re-raised as itself
         if isinstance(item, list) and item:
             raise item[0]
@@ -459,6 +473,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)
     xs.beta = float(res[0])  # ||r0||: with hessenberg(p), the exact LS problem of every step
     xs.stamps = stamps  # host clock: per-iteration / constraint-step stamps, [4k] call start, [4k+1] end
+    _cp()
     return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
                 stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)
 

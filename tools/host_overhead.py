@@ -106,3 +106,19 @@ print("events of a C3 solve:", xs0.events, flush=True)
 import warnings  # noqa: E402
 
 tm("warnings.warn (repeat)", lambda: warnings.warn("Iteration 29 failed with message 'x'", RuntimeWarning))
+
+# _run's phases: [entry, before the output buffers, before spis_solve, after it, before return]
+solvers._CHECKPOINTS = cps = []
+marks = []
+for _ in range(reps):
+    t = time.perf_counter()
+    _, d = solve()
+    marks.append((t, time.perf_counter()))
+solvers._CHECKPOINTS = None
+ph = np.array(cps).reshape(reps, 5)
+m = np.array(marks)
+print("cgmres entry -> _run entry %.1f us" % (1e6 * np.mean(ph[:, 0] - m[:, 0])))
+for i, name in enumerate(["setup (matrix, vectors, constraints, opts)", "buffers + scratch", "spis_solve",
+                          "results + IterateList"]):
+    print("%-44s %.1f us" % (name, 1e6 * np.mean(ph[:, i + 1] - ph[:, i])))
+print("_run return -> cgmres return + assignment %.1f us" % (1e6 * np.mean(m[:, 1] - ph[:, 4])), flush=True)
