@@ -307,6 +307,13 @@ def main():
         # the 256 MB Infinity Cache
         pipe = "xcd" if args.config in ("c3", "c5") or 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
     traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" and not c16 else None
+    if args.config in ("c2", "c4") and args.M is None and pipe == "xcd" and not c16 and args.spmv_nt == 0:
+        # profiles/r03_{c2,c4}_spmv_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the same launches
+        # standalone, back to back (tools/r03_pmc_c2c4.sh over tools/spmv_pmc.py)
+        tt = load_traffic(f"r03_{args.config}_spmv_traffic.json")
+        want = "spmv_pipe_kernel<2048, 4, false, 1, false>" if fused else "spmv_pipe_kernel<2048, 1, false, 1, false>"
+        rows = [r for r in (tt or {}).get("kernels", []) if want in r["kernel"]]
+        traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
     c5 = args.config == "c5" and args.M in (None, 913)
     if c5 and pipe == "xcd" and c16 and args.spmv_nt == 0:
         # profiles/r03_c5_spmv_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the same launches
