@@ -455,7 +455,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
     const int r = cur.r0 + threadIdx.x;
     if (r < cur.r1) {
       double s1 = 0.0, s2 = 0.0;
-      for (int t = cur.rs; t < cur.re; ++t) {
+      // LDS reads in flight in groups, then the adds in row order (the sum is still left to right)
+      int t = cur.rs;
+      for (; t + 8 <= cur.re; t += 8) {
+        if constexpr (DUAL) {
+          double2 pp[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) pp[u] = s_p[t + u + ((t + u) >> 4)];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            s1 += pp[u].x;
+            s2 += pp[u].y;
+          }
+        } else {
+          double pp[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) pp[u] = s_p[t + u + ((t + u) >> 4)];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s1 += pp[u];
+        }
+      }
+      for (; t + 4 <= cur.re; t += 4) {
+        if constexpr (DUAL) {
+          const double2 p0 = s_p[t + (t >> 4)], p1 = s_p[t + 1 + ((t + 1) >> 4)];
+          const double2 p2 = s_p[t + 2 + ((t + 2) >> 4)], p3 = s_p[t + 3 + ((t + 3) >> 4)];
+          s1 += p0.x;
+          s2 += p0.y;
+          s1 += p1.x;
+          s2 += p1.y;
+          s1 += p2.x;
+          s2 += p2.y;
+          s1 += p3.x;
+          s2 += p3.y;
+        } else {
+          const double p0 = s_p[t + (t >> 4)], p1 = s_p[t + 1 + ((t + 1) >> 4)];
+          const double p2 = s_p[t + 2 + ((t + 2) >> 4)], p3 = s_p[t + 3 + ((t + 3) >> 4)];
+          s1 += p0;
+          s1 += p1;
+          s1 += p2;
+          s1 += p3;
+        }
+      }
+      for (; t < cur.re; ++t) {
         if constexpr (DUAL) {
           const double2 pp = s_p[t + (t >> 4)];
           s1 += pp.x;
