@@ -3751,15 +3751,24 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
     // gathers in straight-line quads (a wave-uniform test per 4 slots): the bpermutes of a quad
     // go out together, then its loads; slots past ns hold (row 0, value 0) in the table
     double2 gt[NS];
+    // the block's column indices in groups of GB bpermutes (one LDS wait per group), then the
+    // gathers of the group's quads that hold slots.  32 slots: groups of 8 (166 -> 143 us at C3);
+    // 16 slots: quads (groups of 8 measured 127 vs 124 us)
+    constexpr int GB = NS >= 32 ? 8 : 4;
 #pragma unroll
-    for (int t4 = 0; t4 < NS; t4 += 4) {
-      if (t4 < ns) {
-        int c[4];
+    for (int tg = 0; tg < NS; tg += GB) {
+      if (tg < ns) {
+        int c[GB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          c[u] = __shfl(cur.col[(t4 + u) >> 4], (g << 4) + ((t4 + u) & 15), 64);
+        for (int u = 0; u < GB; ++u)
+          c[u] = __shfl(cur.col[(tg + u) >> 4], (g << 4) + ((tg + u) & 15), 64);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) gt[t4 + u] = U2[static_cast<int64_t>(c[u]) * 16 + li];
+        for (int q = 0; q < GB; q += 4) {
+          if (q == 0 || tg + q < ns) {
+#pragma unroll
+            for (int u = q; u < q + 4; ++u) gt[tg + u] = U2[static_cast<int64_t>(c[u]) * 16 + li];
+          }
+        }
       }
     }
     Ent nx2;
