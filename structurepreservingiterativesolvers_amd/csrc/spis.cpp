@@ -869,6 +869,7 @@ extern "C" int spis_spmv_bench(spis_context* c, spis_matrix* A, int32_t kind, in
       for (double* d : {x, z, bb, q0}) HIP_TRY(hipMemcpy(d, h.data(), sizeof(double) * pn, hipMemcpyHostToDevice));
     }
     if (cold) HIP_TRY(hipMemsetAsync(fl, 0, sizeof(double) * big, c->stream));
+    if (c->spmv_pipe == 6) ST_TRY(ensure_sell(c, A));  // K1s's copy, as spis_solve builds it
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
