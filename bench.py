@@ -196,6 +196,8 @@ def main():
                          "4 one-reduce two-pass MGS carrying the update GEMV")
     ap.add_argument("--nt-basis", type=int, default=2, choices=[0, 1, 2],
                     help="MGS chain basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
+    ap.add_argument("--lag-mode", type=int, default=1, choices=[0, 1],
+                    help="L-mode schedule (SPIS_OPT_LAG_MODE): 1 where the MGS kernel supports it, 0 never")
     ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],
                     help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
                          "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
@@ -246,6 +248,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_COL16, args.col16), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_LAG_MODE, args.lag_mode), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,

@@ -194,7 +194,10 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  *   us, dual 497 -> 627 us; off by default.
  * SPIS_OPT_K7T_SLOTS (default 16): slots per block of K7t's slot table, 16 or 32 (32: twice the
  *   gathers in flight per lane at 2 waves per SIMD; measured slower at C3, kept for the test that
- *   walks many 32-slot blocks per wave).  Results equal up to the grouping of the Gram sums. */
+ *   walks many 32-slot blocks per wave).  Results equal up to the grouping of the Gram sums.
+ * SPIS_OPT_LAG_MODE (default 1): the L-mode schedule (each Arnoldi step's MGS enqueued once the
+ *   host holds the previous H column, carrying the previous update GEMV) where the MGS kernel
+ *   supports it; 0 = the plain pipelined order (the GEMV as its own launch).  Same arithmetic. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -209,7 +212,8 @@ enum spis_option {
   SPIS_OPT_COL16 = 11,
   SPIS_OPT_DIST_MGS = 12,
   SPIS_OPT_SPMV_NT = 13,
-  SPIS_OPT_K7T_SLOTS = 14
+  SPIS_OPT_K7T_SLOTS = 14,
+  SPIS_OPT_LAG_MODE = 15
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -30,6 +30,7 @@ OPT_COL16 = 11
 OPT_DIST_MGS = 12
 OPT_SPMV_NT = 13
 OPT_K7T_SLOTS = 14
+OPT_LAG_MODE = 15
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

@@ -144,6 +144,7 @@ struct spis_context {
   hipEvent_t ev_gemv = nullptr;
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
   int k7t_slots = 16;               // K7t slot-table width (SPIS_OPT_K7T_SLOTS): 16 or 32
+  int lag_mode = 1;                 // SPIS_OPT_LAG_MODE: 1 = L mode where it applies, 0 = never
   int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
@@ -802,6 +803,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_DIST_MGS:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "dist_mgs %lld: 0 or 1", (long long)value);
         c->dist_mgs = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_LAG_MODE:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "lag_mode %lld: 0 or 1", (long long)value);
+        c->lag_mode = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_K7T_SLOTS:
         if (value != 16 && value != 32) return fail(SPIS_ERR_ARG, "k7t_slots %lld: 16 or 32", (long long)value);
@@ -2685,7 +2690,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
     // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
     // L mode: the solver loop below (lag_chain: K2q chains publish H[:, j] to the host themselves)
-    const bool L = S.lag_chain() && c->fuse_spmv && !S.graphable();
+    const bool L = S.lag_chain() && c->fuse_spmv && !S.graphable() && c->lag_mode == 1;
     if (stamps) stamps[0] = now_s();
     ST_TRY(S.enqueue_arnoldi(0));
     if (!L) HIP_TRY(hipEventRecord(c->ev_arn, s));  // L mode waits for H[:, 0] itself

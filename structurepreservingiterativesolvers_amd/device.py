@@ -69,6 +69,7 @@ _OPTIONS = {
     "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
     "spmv_nt": (_lib.OPT_SPMV_NT, {False: 0, True: 1, "auto": 2}),
     "k7t_slots": (_lib.OPT_K7T_SLOTS, {16: 16, 32: 32}),
+    "lag_mode": (_lib.OPT_LAG_MODE, None),
 }
 
 
@@ -112,7 +113,9 @@ def set_option(name, value, ctx=None):
       "per_step" (MGS's j + 2 all-reduces, its rounding);
     * ``spmv_nt`` (False): nontemporal matrix-stream loads in the pipelined SpMV (True: always;
       "auto": when values + columns exceed the 256 MB Infinity Cache); results identical;
-    * ``k7t_slots`` (16): K7t slot-table width, 16 or 32 (32 measured slower; kept for tests)."""
+    * ``k7t_slots`` (16): K7t slot-table width, 16 or 32 (32 measured slower; kept for tests);
+    * ``lag_mode`` (True): the L-mode schedule (MGS enqueued after the host holds the previous H
+      column, carrying the update GEMV); False: the plain pipelined order."""
     ctx = ctx or get_context()
     if name == "device_ilu":
         if value not in (True, False, "auto"):
