@@ -211,6 +211,11 @@ def main():
     ap.add_argument("--spmv-nt", type=int, default=0, choices=[0, 1, 2],
                     help="nontemporal matrix stream in the pipelined SpMV (SPIS_OPT_SPMV_NT): 0 never, 1 always, "
                          "2 beyond the 256 MB Infinity Cache")
+    ap.add_argument("--spmv-w4", type=int, default=0, choices=[0, 1],
+                    help="pipelined SpMV at 4 waves per SIMD (SPIS_OPT_SPMV_W4)")
+    ap.add_argument("--slab-key", type=int, default=1, choices=[0, 1],
+                    help="SpMV row blocks of a slab by position (SPIS_OPT_SLAB_KEY, at upload): 1 groups side by "
+                         "side, 0 group after group")
     ap.add_argument("--orthog", default="mgs", choices=["mgs", "cgs2"],
                     help="mgs = the reference's MGS (the BASELINE line); cgs2 = the opt-in low-sync option")
     ap.add_argument("--prof-period", type=int, default=10,
@@ -231,6 +236,7 @@ def main():
     A = wl["A"]
     n = A.shape[0]
     ctx = get_context(0)
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SLAB_KEY, args.slab_key), "spis_set_option")
     device_matrix(A, ctx=ctx)
     bd = DeviceVector.from_host(wl["b"], ctx=ctx)
     x0 = np.zeros(n)
@@ -249,6 +255,7 @@ def main():
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_COL16, args.col16), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_LAG_MODE, args.lag_mode), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_W4, args.spmv_w4), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
                "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
@@ -319,10 +326,13 @@ def main():
         traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
     c5 = args.config == "c5" and args.M in (None, 913)
     if c5 and pipe == "xcd" and c16 and args.spmv_nt == 0:
-        # profiles/r03_c5_spmv_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the same launches
-        # (tools/r03_pmc_c5.sh over tools/spmv_pmc.py, corrected by tools/pmc_kernels.py)
-        t5 = load_traffic("r03_c5_spmv_traffic.json")
-        want = "spmv_pipe_kernel<2048, 4, false, 1, true>" if fused else "spmv_pipe_kernel<2048, 1, false, 1, true>"
+        # profiles/r03_c5_spmv_traffic[_key1].json: FETCH_SIZE / WRITE_SIZE passes of the same
+        # launches (tools/r03_pmc_c5.sh, tools/r03_slabkey.sh over tools/spmv_pmc.py, corrected by
+        # tools/pmc_kernels.py), on the table in slab order with / without the slab key
+        t5 = load_traffic("r03_c5_spmv_traffic_key1.json" if args.slab_key else "r03_c5_spmv_traffic.json")
+        tmpl = "true, true>" if args.spmv_w4 else "1, true>"
+        want = (f"spmv_pipe_kernel<2048, 4, false, {'4, ' if args.spmv_w4 else ''}{tmpl}" if fused else
+                f"spmv_pipe_kernel<2048, 1, false, {'4, ' if args.spmv_w4 else ''}{tmpl}")
         rows = [r for r in (t5 or {}).get("kernels", []) if want in r["kernel"]]
         traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",

@@ -197,7 +197,16 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  *   walks many 32-slot blocks per wave).  Results equal up to the grouping of the Gram sums.
  * SPIS_OPT_LAG_MODE (default 1): the L-mode schedule (each Arnoldi step's MGS enqueued once the
  *   host holds the previous H column, carrying the previous update GEMV) where the MGS kernel
- *   supports it; 0 = the plain pipelined order (the GEMV as its own launch).  Same arithmetic. */
+ *   supports it; 0 = the plain pipelined order (the GEMV as its own launch).  Same arithmetic.
+ * SPIS_OPT_SLAB_KEY (default 1): read at spis_matrix_create.  1 = within a slab the row blocks
+ *   follow their rows' mean position in the slab's dominant DoF group (slab_order.h), so the
+ *   slab's DoF groups are walked side by side and each XCD gathers an x line about once; 0 = the
+ *   groups one after another inside a slab (round 2's order).  Rows bit-identical; reduction
+ *   partials grouped differently (roundoff).
+ * SPIS_OPT_SPMV_W4 (default 0): the pipelined SpMV (one-deep, not nontemporal) in its 4-waves-per-
+ *   SIMD form: matrix stream and gathers through buffer descriptors, the next block's values
+ *   loaded once the current products are in LDS, partial sums in LDS (<= 128 VGPRs, 4 workgroups
+ *   per CU instead of 3).  Rows bit-identical; partials grouped per workgroup (roundoff). */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -213,7 +222,9 @@ enum spis_option {
   SPIS_OPT_DIST_MGS = 12,
   SPIS_OPT_SPMV_NT = 13,
   SPIS_OPT_K7T_SLOTS = 14,
-  SPIS_OPT_LAG_MODE = 15
+  SPIS_OPT_LAG_MODE = 15,
+  SPIS_OPT_SLAB_KEY = 16,
+  SPIS_OPT_SPMV_W4 = 17
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -31,6 +31,8 @@ OPT_DIST_MGS = 12
 OPT_SPMV_NT = 13
 OPT_K7T_SLOTS = 14
 OPT_LAG_MODE = 15
+OPT_SLAB_KEY = 16
+OPT_SPMV_W4 = 17
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

@@ -59,6 +59,10 @@ struct CsrView {
   const int4* blk_base = nullptr;
   int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
   bool nt = false;  // K1p / K1dp: the matrix stream (val, col) read with nontemporal loads
+  // K1p / K1dp at 4 waves per SIMD (4 workgroups per CU instead of 3): buffer-descriptor matrix
+  // stream and gathers, the next block's values loaded after the current products are in LDS
+  // (SPIS_OPT_SPMV_W4; one-deep, not nontemporal)
+  bool w4 = false;
   // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
   // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at
   // sl_off[s] + 64 t + l; rows padded to the slice's longest (col = the row, val = 0, skipped

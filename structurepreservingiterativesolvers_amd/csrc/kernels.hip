@@ -1,10 +1,11 @@
 // kernels.hip — gfx950 (MI355X, CDNA4) kernels of the CGMRES/FGMRES inner loop.
 //
-// Everything here is HBM-bandwidth bound fp64 work (SpMV ~0.17 flop/B, BLAS-1
-// <= 0.125 flop/B), so no MFMA: the design levers are coalesced 8/16-B-per-lane
-// streams, LDS staging of the irregular SpMV products, enough waves in flight
-// (256-thread workgroups, grid-stride), and deterministic reductions whose
-// partials never leave the device.
+// The SpMV, MGS chain, norms and GEMV are HBM-bandwidth bound fp64 work (SpMV
+// ~0.17 flop/B, BLAS-1 <= 0.125 flop/B): their levers are coalesced 8/16-B-per-lane
+// streams, LDS staging of the irregular SpMV products, enough waves in flight, and
+// deterministic reductions whose partials never leave the device.  The one place
+// with matrix-shaped work, the constraint Gram U^T M U of the terminal projection
+// (K7t / K7m, the default), runs on f64 MFMA (v_mfma_f64_16x16x4).  See DESIGN.md §3.
 //
 // Reference call sites (solvers.py): SpMV :191 / :167 / :290, MGS :193-195,
 // norm + normalise :196-198, GEMV :287, constraint Gram :33-36.
@@ -106,6 +107,21 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double buf_ld1(__amdgpu_buffer_rsrc_t r, int voff) {
   const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
   return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x));
+}
+
+// the same with the element's distance in the scalar offset (K1p's matrix stream: one lane offset
+// for all of a block's loads, the block's start in the descriptor's base)
+__device__ __forceinline__ double buf_ld1s(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x));
+}
+// a descriptor over [p, p + 2^31 B) with a wave-uniform base (callers index it with valid offsets)
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const T* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t u = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a >> 32)))) << 32) |
+                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu)));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), 0, 0x7fffffff, 0x00020000);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -313,7 +329,18 @@ __device__ __forceinline__ int col16_decode(unsigned v, int b0, int b1, int b2, 
 
 // block lb of the table (entries lb * ms, lb * ms + 1: ms = 1 consecutive starts, 2 (start, end)
 // pairs); C16: the columns from the 16-bit copy and the block's bases base[lb]
-template <int CAP, int MODE, bool NT = false, bool C16 = false>
+// BUF stage: the values only (LATEV: issued once the current block's products are in LDS, so the
+// next block's values are not live in registers across the current block's gathers)
+template <int CAP>
+__device__ __forceinline__ void pipe_load_vals(PipeStage<CAP>& st, const double* __restrict__ va) {
+  if (st.nnz > CAP) return;
+  const __amdgpu_buffer_rsrc_t rv = span_rsrc(va + st.nz0);
+#pragma unroll
+  for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
+    st.vals[u] = threadIdx.x + u * kBlock < st.nnz ? buf_ld1s(rv, threadIdx.x * 8, u * kBlock * 8) : 0.0;
+}
+
+template <int CAP, int MODE, bool NT = false, bool C16 = false, bool BUF = false, bool VALS = true>
 __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int lb, int ms,
                                           const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                           const uint16_t* __restrict__ c16, const int4* __restrict__ base,
@@ -333,6 +360,27 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
   st.nz0 = m0.y;
   st.nnz = m1.y - m0.y;
   if (st.nnz > CAP) return;  // long row: read directly by the workgroup-wide path
+  if constexpr (BUF && !NT) {
+    // buffer descriptors based at the block's first nonzero: every load of the block shares the
+    // lane offset, its distance u * kBlock elements rides in the scalar offset (no 64-bit address
+    // registers per element, which is what kept the stage at 3 waves per SIMD)
+    if constexpr (C16) {
+      const __amdgpu_buffer_rsrc_t rc = span_rsrc(c16 + st.nz0);
+#pragma unroll
+      for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
+        st.cols[u] = threadIdx.x + u * kBlock < st.nnz
+                         ? static_cast<int>(__builtin_amdgcn_raw_buffer_load_b16(rc, threadIdx.x * 2, u * kBlock * 2, 0))
+                         : 0;
+    } else {
+      const __amdgpu_buffer_rsrc_t rc = span_rsrc(ci + st.nz0);
+#pragma unroll
+      for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
+        st.cols[u] = threadIdx.x + u * kBlock < st.nnz
+                         ? static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(rc, threadIdx.x * 4, u * kBlock * 4, 0))
+                         : 0;
+    }
+    if constexpr (VALS) pipe_load_vals<CAP>(st, va);
+  } else {
 #pragma unroll
   for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
     const int i = threadIdx.x + u * kBlock;
@@ -350,6 +398,7 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
       st.cols[u] = i < st.nnz ? ci[st.nz0 + i] : 0;
       st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
     }
+  }
   }
   const int r = st.r0 + threadIdx.x;
   if (r < st.r1) {
@@ -379,8 +428,10 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 // x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
 // x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
-template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16 ? 3 : 8))) void spmv_pipe_kernel(
+// BUF: the matrix stream and the gathers through buffer descriptors (32-bit lane offsets), which
+// frees the registers for WPE = 4 waves per SIMD (4 workgroups per CU instead of 3)
+template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE > 3 ? WPE : (C16 ? 3 : 8)))) void spmv_pipe_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
@@ -388,18 +439,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
     double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
   constexpr bool DUAL = MODE == 4;
   constexpr int kPer = PipeStage<CAP>::kPer;
+  constexpr bool LATEV = BUF && !NT && WPE > 3;  // 4 waves per SIMD: the next values loaded late
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
   // of 16 entries (swe's edge rows) would otherwise put a wave's lanes 256 B apart, all in one
   // LDS bank group; the pad staggers them
   __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
   __shared__ double s_wave[4];
+  // LATEV: each thread's partial sums live in its own LDS slot between blocks (in registers they
+  // were spilled, and a scratch reload waits for every load issued before it: the prefetch)
+  __shared__ double2 s_pt[LATEV ? kBlock : 1];
   double pt1 = 0.0, pt2 = 0.0;
+  if (LATEV) s_pt[threadIdx.x] = make_double2(0.0, 0.0);
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
   const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
-  PipeStage<CAP> cur;
-  if (b0 < b1) pipe_load<CAP, MODE, NT, C16>(cur, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
-  for (int blk = b0; blk < b1; blk += bs) {
+  const __amdgpu_buffer_rsrc_t rx1 = span_rsrc(x1);
+  const __amdgpu_buffer_rsrc_t rx2 = span_rsrc(DUAL ? x2 : x1);
+  // one block: cur's products and row sums, nxt (block nb) loaded meanwhile.  The loop below
+  // alternates two stages (no stage copy at the back edge: the copy's register moves spilled)
+  auto step = [&](PipeStage<CAP>& cur, PipeStage<CAP>& nxt, int blk) __attribute__((always_inline)) {
     const int nb = blk + bs;
     if (cur.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
       double s1 = 0.0, s2 = 0.0;
@@ -415,6 +473,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
       }
       if (threadIdx.x == 0) {
         const int r0 = cur.r0;
+        if (LATEV) {
+          pt1 = s_pt[0].x;
+          pt2 = s_pt[0].y;
+        }
         if (DUAL) {
           const double t = s1 - aux1[r0];
           pt1 += t * t;
@@ -425,9 +487,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
         if (MODE == kEpiDot) { y1[r0] = s1; pt1 += aux1[r0] * s1; }
         if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
         if (MODE == kEpiR0) { const double t = aux1[r0] - s1; y1[r0] = t; pt1 += t * t; }
+        if (LATEV) s_pt[0] = make_double2(pt1, pt2);
       }
-      if (nb < b1) pipe_load<CAP, MODE, NT, C16>(cur, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
-      continue;
+      nxt.nnz = 0;
+      if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+      return;
     }
     // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
     // include the prefetch, and the prefetch is in flight through the LDS phase below
@@ -435,29 +499,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
-      g1[u] = x1[c];
-      if (DUAL) g2[u] = x2[c];
+      if constexpr (BUF) {
+        g1[u] = buf_ld1(rx1, c * 8);
+        if (DUAL) g2[u] = buf_ld1(rx2, c * 8);
+      } else {
+        g1[u] = x1[c];
+        if (DUAL) g2[u] = x2[c];
+      }
     }
-    PipeStage<CAP> nxt;
     nxt.nnz = 0;
-    if (nb < b1) pipe_load<CAP, MODE, NT, C16>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+    if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, !LATEV>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+    // entry i = tid + u kBlock sits at i + i/16 = (tid + tid/16) + u (kBlock + kBlock/16): one base
+    // register and an immediate offset per u (the compiler's own form of i + i/16 kept 8 addresses
+    // live, which spilled at 4 waves per SIMD)
+    const int pbase = threadIdx.x + (threadIdx.x >> 4);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int i = threadIdx.x + u * kBlock;
       if (i < cur.nnz) {
         if constexpr (DUAL)
-          s_p[i + (i >> 4)] = make_double2(cur.vals[u] * g1[u], cur.vals[u] * g2[u]);
+          s_p[pbase + u * (kBlock + kBlock / 16)] = make_double2(cur.vals[u] * g1[u], cur.vals[u] * g2[u]);
         else
-          s_p[i + (i >> 4)] = cur.vals[u] * g1[u];
+          s_p[pbase + u * (kBlock + kBlock / 16)] = cur.vals[u] * g1[u];
       }
     }
     __syncthreads();
+    if (LATEV && nb < b1) pipe_load_vals<CAP>(nxt, va);
     const int r = cur.r0 + threadIdx.x;
     if (r < cur.r1) {
       double s1 = 0.0, s2 = 0.0;
       // LDS reads in flight in groups, then the adds in row order (the sum is still left to right)
       int t = cur.rs;
-      for (; t + 8 <= cur.re; t += 8) {
+      for (; WPE < 4 && t + 8 <= cur.re; t += 8) {  // (at 4 waves per SIMD the group of 8 spills)
         if constexpr (DUAL) {
           double2 pp[8];
 #pragma unroll
@@ -505,6 +578,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
           s1 += s_p[t + (t >> 4)];
         }
       }
+      if (LATEV) {
+        pt1 = s_pt[threadIdx.x].x;
+        pt2 = s_pt[threadIdx.x].y;
+      }
       if (DUAL) {
         const double t = s1 - cur.a1;
         pt1 += t * t;
@@ -515,9 +592,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, C16
       if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
       if (MODE == kEpiResNorm) { const double t = s1 - cur.a1; pt1 += t * t; }
       if (MODE == kEpiR0) { const double t = cur.a1 - s1; y1[r] = t; pt1 += t * t; }
+      if (LATEV) s_pt[threadIdx.x] = make_double2(pt1, pt2);
     }
     __syncthreads();
-    cur = nxt;
+  };
+  PipeStage<CAP> sa, sb;
+  if (b0 < b1) pipe_load<CAP, MODE, NT, C16, BUF>(sa, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
+  for (int blk = b0; blk < b1; blk += 2 * bs) {
+    step(sa, sb, blk);
+    if (blk + bs >= b1) break;
+    step(sb, sa, blk + bs);
+  }
+  if (LATEV) {
+    pt1 = s_pt[threadIdx.x].x;
+    pt2 = s_pt[threadIdx.x].y;
   }
   if (MODE != kEpiPlain) {
     const double tot1 = block_sum(pt1, s_wave);
@@ -774,6 +862,12 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   if (A.depth == 2)                                                                                        \
     launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
+  else if (A.w4 && A.col16 != nullptr)                                                                          \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
+  else if (A.w4)                                                                                                \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, false, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);            \
   else if (A.col16 != nullptr && A.nt)                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,         \
              A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
@@ -822,10 +916,13 @@ static int resident_grid(F kernel) {
   return t < 8 ? 8 : (t > kSpmvGrid ? kSpmvGrid : t);
 }
 
-static int pipe_grid_max(int depth, bool c16) {
+static int pipe_grid_max(int depth, bool c16, bool w4) {
   static const int g1 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
   static const int g1c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 1, true>);
   static const int g2 = resident_grid(spmv_pipe2_kernel<kPipeCap, 4>);
+  static const int g4 = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 4, false, true>);
+  static const int g4c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 4, true, true>);
+  if (w4 && depth == 1) return c16 ? g4c : g4;
   return depth == 2 ? g2 : c16 ? g1c : g1;
 }
 
@@ -839,7 +936,7 @@ int spmv_grid(const CsrView& A, bool fixed) {
     if (g > 8) g &= ~7;
     return g < 1 ? 1 : g;
   }
-  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth, A.col16 != nullptr) : kSpmvGrid;
+  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth, A.col16 != nullptr, A.w4) : kSpmvGrid;
   int g = A.n_blk < cap ? A.n_blk : cap;
   if (A.blk_meta != nullptr && g > 8) g &= ~7;  // the XCD-local walk deals workgroups 8 at a time
   return g < 1 ? 1 : g;

@@ -10,12 +10,18 @@ extern "C" {
 
 // blk[nb1] = row-block boundaries; pairs_out[4 (nb1 - 1)] = (row start, nz start, row end, nz end)
 // per block in slab order.  Returns 1 when reordered, 0 when the natural order stands.
-int slab_order_blocks(int64_t n, const int32_t* rp, const int32_t* ci, const int32_t* blk, int64_t nb1,
-                      int32_t* pairs_out) {
+// keyed = 1: blocks of one slab by their rows' mean position (slab key, SPIS_OPT_SLAB_KEY)
+int slab_order_blocks_keyed(int64_t n, const int32_t* rp, const int32_t* ci, const int32_t* blk, int64_t nb1,
+                            int32_t* pairs_out, int32_t keyed) {
   std::vector<int32_t> b(blk, blk + nb1), pairs;
-  if (!spis::build_slab_order(n, rp, ci, b, pairs)) return 0;
+  if (!spis::build_slab_order(n, rp, ci, b, pairs, keyed != 0)) return 0;
   for (size_t i = 0; i < pairs.size(); ++i) pairs_out[i] = pairs[i];
   return 1;
+}
+
+int slab_order_blocks(int64_t n, const int32_t* rp, const int32_t* ci, const int32_t* blk, int64_t nb1,
+                      int32_t* pairs_out) {
+  return slab_order_blocks_keyed(n, rp, ci, blk, nb1, pairs_out, 0);
 }
 
 // col16_out[nnz], bases_out[4 (nb1 - 1)]: the 16-bit column copy (col16.h); 1 = built, 0 = a block

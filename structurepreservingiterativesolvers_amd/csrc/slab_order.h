@@ -20,12 +20,18 @@ namespace spis {
 // sum bit-identical); only which workgroup adds a row into its partial dot products changes.
 // Square matrices only (a column is a row); false when the order would equal the contiguous one.
 constexpr int kSlabLabels = 64;
-// the rows' slab labels (one propagation pass over the matrix's pattern); false if too small
-inline bool slab_labels(int64_t n, const int32_t* rp, const int32_t* ci, std::vector<uint8_t>& lab) {
+// the rows' slab labels (one propagation pass over the matrix's pattern); false if too small.
+// key (optional): each row's position inside its slab, the mean index of its columns that carry
+// its label (the row's own index when none do).  The dominant DoF group's numbering is then the
+// common coordinate of every group in the slab: an swe interior-RT or rho row gets the position of
+// its cell's edges (slab key, build_slab_order).
+inline bool slab_labels(int64_t n, const int32_t* rp, const int32_t* ci, std::vector<uint8_t>& lab,
+                        std::vector<double>* key = nullptr) {
   const int64_t nnz = rp[n];
   if (n < 1 || nnz < 1) return false;
   std::vector<uint8_t> lab0(n);
   lab.assign(n, 0);
+  if (key) key->assign(n, 0.0);
   for (int64_t r = 0; r < n; ++r)
     lab0[r] = static_cast<uint8_t>(std::min<int64_t>(kSlabLabels - 1, static_cast<int64_t>(rp[r]) * kSlabLabels / nnz));
   int cnt[kSlabLabels];
@@ -36,28 +42,53 @@ inline bool slab_labels(int64_t n, const int32_t* rp, const int32_t* ci, std::ve
     for (int l = 0; l < kSlabLabels; ++l)
       if (cnt[l] > cnt[best]) best = l;
     lab[r] = static_cast<uint8_t>(best);
+    if (key) {
+      double s = 0.0;
+      int m = 0;
+      for (int32_t i = rp[r]; i < rp[r + 1]; ++i)
+        if (lab0[ci[i]] == best) {
+          s += ci[i];
+          ++m;
+        }
+      (*key)[r] = m > 0 ? s / m : static_cast<double>(r);
+    }
   }
   return true;
 }
 
-// a stable order of items by label; false when it is the natural one
-inline bool slab_sort(const std::vector<uint8_t>& item_lab, std::vector<int64_t>& order) {
+// a stable order of items by label (then by key within a label, when given); false when it is
+// the natural one
+inline bool slab_sort(const std::vector<uint8_t>& item_lab, std::vector<int64_t>& order,
+                      const std::vector<double>* item_key = nullptr) {
   const int64_t m = static_cast<int64_t>(item_lab.size());
-  bool moved = false;
-  for (int64_t i = 1; i < m && !moved; ++i) moved = item_lab[i] < item_lab[i - 1];
-  if (!moved) return false;
   order.resize(m);
   for (int64_t i = 0; i < m; ++i) order[i] = i;
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return item_lab[a] < item_lab[b]; });
-  return true;
+  if (item_key) {
+    const std::vector<double>& k = *item_key;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return item_lab[a] != item_lab[b] ? item_lab[a] < item_lab[b] : k[a] < k[b];
+    });
+  } else {
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return item_lab[a] < item_lab[b]; });
+  }
+  for (int64_t i = 0; i < m; ++i)
+    if (order[i] != i) return true;
+  return false;
 }
 
-// the row blocks blk in slab order of the rows' labels lab
+// the row blocks blk in slab order of the rows' labels lab; with key (slab_labels' row positions)
+// the blocks of one slab follow their rows' mean position, so the slab's DoF groups are walked
+// side by side instead of one group after another.  Each XCD's workgroups take its eighth's blocks
+// round-robin, about 100 consecutive blocks at a time, and at C5 a slab holds ~1,500 blocks: in
+// group order a slab's interior and rho blocks re-gather the x lines its edge blocks gathered
+// ~1,000 blocks earlier, long after the XCD's 4 MB L2 has turned over.
 inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab, const std::vector<int32_t>& blk,
-                             std::vector<int32_t>& pairs, std::vector<int64_t>* order_out = nullptr) {
+                             std::vector<int32_t>& pairs, std::vector<int64_t>* order_out = nullptr,
+                             const std::vector<double>* key = nullptr) {
   const int64_t nb = static_cast<int64_t>(blk.size()) - 1;
   if (nb < 16) return false;
   std::vector<uint8_t> blab(nb);
+  std::vector<double> bkey(key ? nb : 0);
   int cnt[kSlabLabels];
   for (int64_t b = 0; b < nb; ++b) {  // a block: the label most of its rows carry
     std::fill(cnt, cnt + kSlabLabels, 0);
@@ -66,9 +97,15 @@ inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab,
     for (int l = 1; l < kSlabLabels; ++l)
       if (cnt[l] > cnt[best]) best = l;
     blab[b] = static_cast<uint8_t>(best);
+    if (key) {  // the mean position of the block's rows that carry its label
+      double s = 0.0;
+      for (int32_t r = blk[b]; r < blk[b + 1]; ++r)
+        if (lab[r] == best) s += (*key)[r];
+      bkey[b] = cnt[best] > 0 ? s / cnt[best] : static_cast<double>(blk[b]);
+    }
   }
   std::vector<int64_t> order;
-  if (!slab_sort(blab, order)) return false;
+  if (!slab_sort(blab, order, key ? &bkey : nullptr)) return false;
   pairs.resize(4 * nb);  // per block (row start, nz start, row end, nz end): the kernels' int2 pairs
   for (int64_t i = 0; i < nb; ++i) {
     const int64_t b = order[i];
@@ -82,9 +119,11 @@ inline bool build_slab_order(const int32_t* rp, const std::vector<uint8_t>& lab,
 }
 
 inline bool build_slab_order(int64_t n, const int32_t* rp, const int32_t* ci, const std::vector<int32_t>& blk,
-                             std::vector<int32_t>& pairs) {
+                             std::vector<int32_t>& pairs, bool keyed = false) {
   std::vector<uint8_t> lab;
-  return static_cast<int64_t>(blk.size()) > 16 && slab_labels(n, rp, ci, lab) && build_slab_order(rp, lab, blk, pairs);
+  std::vector<double> key;
+  return static_cast<int64_t>(blk.size()) > 16 && slab_labels(n, rp, ci, lab, keyed ? &key : nullptr) &&
+         build_slab_order(rp, lab, blk, pairs, nullptr, keyed ? &key : nullptr);
 }
 
 }  // namespace spis

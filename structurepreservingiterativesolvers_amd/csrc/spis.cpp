@@ -145,6 +145,8 @@ struct spis_context {
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
   int k7t_slots = 16;               // K7t slot-table width (SPIS_OPT_K7T_SLOTS): 16 or 32
   int lag_mode = 1;                 // SPIS_OPT_LAG_MODE: 1 = L mode where it applies, 0 = never
+  int slab_key = 1;                 // SPIS_OPT_SLAB_KEY: slab order's blocks by position within a slab (at upload)
+  int spmv_w4 = 0;                  // SPIS_OPT_SPMV_W4: the pipelined SpMV at 4 waves per SIMD (buffer-descriptor form)
   int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
@@ -320,6 +322,7 @@ CsrView spis_matrix::dual_view() const {
   }
   if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   v.nt = ctx->spmv_nt == 1 || (ctx->spmv_nt == 2 && 12.0 * static_cast<double>(nnz) > 256.0 * 1024 * 1024);
+  v.w4 = ctx->spmv_w4 == 1 && !v.nt && n_cols + n_ghost < (int64_t{1} << 28);  // 32-bit byte offsets
   if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
   else if ((mode == 2 || mode == 4) && blk_slab_d != nullptr) {
     v.blk_meta = blk_slab_d;
@@ -808,6 +811,14 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "lag_mode %lld: 0 or 1", (long long)value);
         c->lag_mode = static_cast<int>(value);
         return SPIS_OK;
+      case SPIS_OPT_SPMV_W4:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "spmv_w4 %lld: 0 or 1", (long long)value);
+        c->spmv_w4 = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_SLAB_KEY:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "slab_key %lld: 0 or 1", (long long)value);
+        c->slab_key = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_K7T_SLOTS:
         if (value != 16 && value != 32) return fail(SPIS_ERR_ARG, "k7t_slots %lld: 16 or 32", (long long)value);
         c->k7t_slots = static_cast<int>(value);
@@ -1038,8 +1049,10 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
       std::vector<int32_t> pairs;
       std::vector<int64_t> order;
       std::vector<uint8_t> lab;
-      if (n_ghost == 0 && static_cast<int64_t>(blk.size()) > 16 && slab_labels(n_rows, indptr, indices, lab) &&
-          build_slab_order(indptr, lab, blk, pairs, &order)) {
+      std::vector<double> key;
+      std::vector<double>* kp = c->slab_key ? &key : nullptr;
+      if (n_ghost == 0 && static_cast<int64_t>(blk.size()) > 16 && slab_labels(n_rows, indptr, indices, lab, kp) &&
+          build_slab_order(indptr, lab, blk, pairs, &order, kp)) {
         HIP_TRY(hipMalloc(&M->blk_slab_d, sizeof(int32_t) * pairs.size()));
         HIP_TRY(hipMemcpy(M->blk_slab_d, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice));
       }

@@ -70,6 +70,8 @@ _OPTIONS = {
     "spmv_nt": (_lib.OPT_SPMV_NT, {False: 0, True: 1, "auto": 2}),
     "k7t_slots": (_lib.OPT_K7T_SLOTS, {16: 16, 32: 32}),
     "lag_mode": (_lib.OPT_LAG_MODE, None),
+    "slab_key": (_lib.OPT_SLAB_KEY, None),
+    "spmv_w4": (_lib.OPT_SPMV_W4, None),
 }
 
 
@@ -115,7 +117,10 @@ def set_option(name, value, ctx=None):
       "auto": when values + columns exceed the 256 MB Infinity Cache); results identical;
     * ``k7t_slots`` (16): K7t slot-table width, 16 or 32 (32 measured slower; kept for tests);
     * ``lag_mode`` (True): the L-mode schedule (MGS enqueued after the host holds the previous H
-      column, carrying the update GEMV); False: the plain pipelined order."""
+      column, carrying the update GEMV); False: the plain pipelined order;
+    * ``slab_key`` (True): matrices uploaded afterwards order the row blocks of a slab by their
+      rows' position, so a slab's DoF groups are walked side by side (False: group after group);
+    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form."""
     ctx = ctx or get_context()
     if name == "device_ilu":
         if value not in (True, False, "auto"):

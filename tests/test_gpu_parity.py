@@ -96,6 +96,38 @@ def test_spmv_bit_exact_vs_scipy(spis, pipe):
         set_option("spmv_pipe", "auto")
 
 
+@pytest.mark.parametrize("col16", [False, True])
+@pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd_natural"])
+def test_spmv_w4_bit_exact_vs_scipy(spis, pipe, col16):
+    """SPIS_OPT_SPMV_W4: the pipelined SpMV's 4-waves-per-SIMD form (buffer-descriptor matrix
+    stream and gathers, late value loads, partial sums in LDS), on 32- and 16-bit columns: rows
+    bit-exact vs SciPy, the residual-norm epilogue to 1e-12, long rows 1e-12."""
+    from structurepreservingiterativesolvers_amd import primitives as P
+    from structurepreservingiterativesolvers_amd.device import set_option
+
+    rng = np.random.default_rng(7)
+    set_option("spmv_pipe", pipe)
+    set_option("col16", col16)
+    set_option("spmv_w4", True)
+    try:
+        for name, A in _matrices().items():
+            x = rng.normal(size=A.shape[1])
+            y = P.spmv(A, x)
+            yref = A @ x
+            long_rows = np.flatnonzero(np.diff(A.indptr) > 1024)
+            mask = np.ones(A.shape[0], dtype=bool)
+            mask[long_rows] = False
+            assert np.array_equal(y[mask], yref[mask]), name
+            if long_rows.size:
+                np.testing.assert_allclose(y[long_rows], yref[long_rows], rtol=1e-12)
+            r = P.residual_norm(A, x, yref + 1e-3)
+            np.testing.assert_allclose(r, np.linalg.norm(A @ x - (yref + 1e-3)), rtol=1e-12)
+    finally:
+        set_option("spmv_pipe", "auto")
+        set_option("col16", "auto")
+        set_option("spmv_w4", False)
+
+
 @pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd_natural"])
 def test_spmv_col16_bit_exact_vs_scipy(spis, pipe):
     """The pipelined SpMV on the 16-bit column copy (SPIS_OPT_COL16 = 2: forced at any size; by
@@ -161,10 +193,16 @@ def test_spmv_pipe_modes_solver_agree(spis):
             set_option("spmv_pipe", pipe)
             x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
             runs[pipe] = (x, np.asarray(d["res"]), d["steps"], d["x"].trace)
+        set_option("spmv_w4", True)  # the 4-waves-per-SIMD form of the default kernels
+        for pipe in ("xcd", "stride"):
+            set_option("spmv_pipe", pipe)
+            x, d = solvers.cgmres(A, b, np.zeros_like(b), 25, tol=1e-19, conlist=cons)
+            runs[pipe + "_w4"] = (x, np.asarray(d["res"]), d["steps"], d["x"].trace)
     finally:
         set_option("spmv_pipe", "auto")
+        set_option("spmv_w4", False)
     x0, r0, s0, t0 = runs["off"]
-    for pipe in ("stride", "xcd", "stride2", "xcd2", "sell", "xcd_natural"):
+    for pipe in ("stride", "xcd", "stride2", "xcd2", "sell", "xcd_natural", "xcd_w4", "stride_w4"):
         x, r, st, tr = runs[pipe]
         assert st == s0 and tr == t0, pipe
         assert np.linalg.norm(x - x0) <= 1e-9 * np.linalg.norm(x0), pipe

@@ -75,6 +75,53 @@ def test_swe_slab_order(host):
     assert before > 3.0 and after < 0.6 * before, (before, after)  # C3 (M=289): 3.0 -> 1.14
 
 
+def _refetched_lines(A, spans, dist):
+    """Lines of x fetched per eighth when a line whose previous use in that eighth lies more than
+    dist blocks back is fetched again (an XCD's L2 over its round-robin walk), / total lines."""
+    rp, ci = A.indptr, A.indices
+    nb = len(spans)
+    fetched = 0
+    for g in range(8):
+        sel = spans[nb * g // 8: nb * (g + 1) // 8]
+        lines = [np.unique(ci[rp[r0]:rp[r1]] // 16) for r0, r1 in sel]
+        pos = np.concatenate([np.full(ln.size, p) for p, ln in enumerate(lines)])
+        lines = np.concatenate(lines)
+        o = np.lexsort((pos, lines))
+        pos, lines = pos[o], lines[o]
+        first = np.ones(lines.size, dtype=bool)
+        first[1:] = lines[1:] != lines[:-1]
+        fetched += first.sum() + ((~first) & (np.diff(pos, prepend=0) > dist)).sum()
+    return fetched / ((A.shape[1] + 15) // 16)
+
+
+def test_swe_slab_key_walks_groups_side_by_side(host):
+    """SPIS_OPT_SLAB_KEY: inside a slab the blocks follow their rows' position, so an x line's
+    uses by the slab's edge, interior and rho blocks lie close together in the walk.  M = 240 with
+    16-row blocks has C5's proportions (a slab ~6 times the reuse distance, which spans two mesh
+    rows): group after group each line is fetched 1.53 times per eighth, side by side 1.05."""
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    A = sa.linforms(M=240)[0]["A"].tocsr()
+    blk = _blocks(A, rows=16)
+    host.slab_order_blocks_keyed.argtypes = [C.c_int64, PI, PI, PI, C.c_int64, PI, C.c_int32]
+    host.slab_order_blocks_keyed.restype = C.c_int
+    spans = {}
+    for key in (0, 1):
+        rp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+        ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+        out = np.zeros(4 * (len(blk) - 1), dtype=np.int32)
+        assert host.slab_order_blocks_keyed(A.shape[0], rp.ctypes.data_as(PI), ci.ctypes.data_as(PI),
+                                            blk.ctypes.data_as(PI), len(blk), out.ctypes.data_as(PI), key) == 1
+        pairs = out.reshape(-1, 4)
+        np.testing.assert_array_equal(pairs[:, 1], A.indptr[pairs[:, 0]])
+        spans[key] = pairs[:, [0, 2]]
+    natural = sorted(map(tuple, np.stack([blk[:-1], blk[1:]], axis=1)))
+    assert sorted(map(tuple, spans[1])) == natural  # a permutation of the blocks
+    grouped, keyed = _refetched_lines(A, spans[0], 360), _refetched_lines(A, spans[1], 360)
+    assert keyed < 1.1 and grouped > 1.3 * keyed, (grouped, keyed)
+    assert _lines_per_eighth(A, spans[1]) <= _lines_per_eighth(A, spans[0])
+
+
 def test_banded_keeps_natural_order(host):
     n = 20000
     A = sps.diags([np.ones(n - 1), 2 * np.ones(n), np.ones(n - 1)], [-1, 0, 1], format="csr")

@@ -3,7 +3,7 @@ Arnoldi SpMV and fused dual SpMV launches on a bench configuration's matrix, sta
 solver's default kernel choice (spis_spmv_bench), so that the per-launch HBM traffic of both
 SpMVs is measured:
 
-    rocprofv3 --pmc FETCH_SIZE --output-format csv -d DIR -o run -- python tools/spmv_pmc.py [CFG] [nt] [cold]
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d DIR -o run -- python tools/spmv_pmc.py [CFG] [nt] [cold] [key]
 
 CFG: c5 (default: swe M = 913, 1.25 GB of 16-bit-column matrix stream, where the matrix never
 stays resident), c2 or c4 (lkdv / lkdvRK: the matrix fits the Infinity Cache, as in the solver),
@@ -29,9 +29,11 @@ if cfg.isdigit():
 else:
     wl = bench.build_workload(argparse.Namespace(config=cfg, M=None, cycles=1))
 cold = int(sys.argv[3]) if len(sys.argv) > 3 else (1 if cfg == "c5" else 0)
+key = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # SPIS_OPT_SLAB_KEY at upload
 print(f"assembled {cfg}: N={wl['A'].shape[0]:,} nnz={wl['A'].nnz:,}", flush=True)
 ctx = get_context(0)
 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, nt), "spis_set_option")
+_lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SLAB_KEY, key), "spis_set_option")
 Ad = device_matrix(wl["A"], ctx=ctx)
 for kind, name in ((0, "arnoldi"), (1, "dual")):
     v = C.c_double()
