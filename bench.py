@@ -26,6 +26,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -277,6 +278,11 @@ def main():
 
     _lib.check(L.spis_profile_enable(ctx.handle, args.prof_period), "spis_profile_enable")
     ctx.synchronize()
+    # the set-up's objects (assembled matrices, oracle imports) leave the collector's generations,
+    # so a full collection inside the timed loop does not walk them (one run's host time between
+    # solves read 302 instead of 48 us)
+    gc.collect()
+    gc.freeze()
     t0 = time.perf_counter()
     iters = 0
     outside = 0.0  # host time per solve outside spis_solve (Python wrapper, result objects)
