@@ -30,8 +30,8 @@ class problem:
     """Mirror of ``lkdv/lkdv.py:15-37``."""
 
     def __init__(self, N, M, degree, space="DG"):
-        if degree != 1 or space != "DG":
-            raise NotImplementedError("synthetic lkdv assembly supports DG1 only")
+        if int(degree) < 1 or space != "DG":
+            raise NotImplementedError("synthetic lkdv assembly supports DG(q), q >= 1")
         self.mlength = 40
         self.degree = degree
         self.dim = 3
@@ -77,6 +77,77 @@ def dg1_operators(M, length):
     return Mass, G, Gpat, cdofs
 
 
+def _lagrange(q):
+    """Equispaced Lagrange basis of degree q on [0, 1] (nodes include both ends, so a facet value
+    is one dof of each cell, as in DG(1)): the monomial coefficients C, phi_j = sum_k C[k, j] x^k."""
+    nodes = np.linspace(0.0, 1.0, q + 1)
+    return np.linalg.inv(np.vander(nodes, q + 1, increasing=True))
+
+
+def _basis(C, x, deriv=False):
+    """phi_j(x) (or phi_j'(x)) for every j, as (q + 1, len(x))."""
+    q = C.shape[0] - 1
+    if deriv:
+        P = np.zeros((len(x), q + 1))
+        for k in range(1, q + 1):
+            P[:, k] = k * x ** (k - 1)
+    else:
+        P = np.vander(x, q + 1, increasing=True)
+    return (P @ C).T
+
+
+def _gauss01(npts):
+    xg, wg = np.polynomial.legendre.leggauss(npts)
+    return 0.5 * (xg + 1.0), 0.5 * wg
+
+
+def dg_operators(M, length, q=1):
+    """DG(q) mass and ``g`` on a periodic interval (exact Gauss quadrature): (Mass, G, Gpat,
+    cdofs).  q = 1 is :func:`dg1_operators` itself (the golden fixtures were made from it)."""
+    if q == 1:
+        return dg1_operators(M, length)
+    h = length / M
+    nl = q + 1
+    n = nl * M
+    cells = np.arange(M)
+    cdofs = nl * cells[:, None] + np.arange(nl)[None, :]
+    C = _lagrange(q)
+    xg, wg = _gauss01(q + 1)  # exact for the degree-2q mass and degree-(2q-1) volume integrands
+    phi, dphi = _basis(C, xg), _basis(C, xg, deriv=True)
+    mass_e = h * (phi * wg) @ phi.T
+    vol_e = (phi * wg) @ dphi.T  # [i, j] = int phi_j' phi_i dx (h cancels)
+    Mass = Triplets(n, n).add_blocks(cdofs, cdofs, np.broadcast_to(mass_e, (M, nl, nl))).csr()
+    t = Triplets(n, n).add_blocks(cdofs, cdofs, np.broadcast_to(vol_e, (M, nl, nl)))
+    # facet between L = cell - 1 (its last dof: u_L(1)) and R = cell (its first dof: u_R(0)):
+    # -(u_L(1) - u_R(0)) * (v_L(1) + v_R(0)) / 2, local order (L_0 .. L_q, R_0 .. R_q)
+    left = (cells - 1) % M
+    fdofs = np.concatenate([cdofs[left], cdofs], axis=1)
+    fac = np.zeros((2 * nl, 2 * nl))
+    for test in (q, q + 1):
+        fac[test, q] += -0.5
+        fac[test, q + 1] += +0.5
+    t.add_blocks(fdofs, fdofs, np.broadcast_to(fac, (M, 2 * nl, 2 * nl)))
+    G = t.csr()
+    Gpat = Triplets(n, n).add_blocks(fdofs, fdofs, np.zeros((M, 2 * nl, 2 * nl))).csr()
+    return Mass, G, Gpat, cdofs
+
+
+def project_dg(f, M, length, q=1):
+    """L2 projection of ``f`` into DG(q) (q + 2 Gauss points per cell); q = 1 is
+    :func:`project_dg1`."""
+    if q == 1:
+        return project_dg1(f, M, length)
+    h = length / M
+    C = _lagrange(q)
+    xg, wg = _gauss01(q + 2)
+    x0 = np.arange(M)[:, None] * h
+    fq = f(x0 + xg[None, :] * h)  # (M, npts)
+    phi = _basis(C, xg)  # (q + 1, npts)
+    rhs = h * (fq * wg) @ phi.T  # (M, q + 1)
+    mass_e = h * (_basis(C, _gauss01(q + 1)[0]) * _gauss01(q + 1)[1]) @ _basis(C, _gauss01(q + 1)[0]).T
+    return np.linalg.solve(mass_e, rhs.T).T.reshape(-1)
+
+
 def project_dg1(f, M, length):
     """L2 projection of ``f`` into DG(1) (2-point Gauss per cell; the DG mass
     matrix is block-diagonal so this is exact for the quadrature)."""
@@ -91,8 +162,12 @@ def project_dg1(f, M, length):
     return (rhs @ minv.T).reshape(-1)
 
 
-def solve_mass(Mass, rhs):
-    """Mass^{-1} rhs for the block-diagonal DG(1) mass (2x2 blocks)."""
+def solve_mass(Mass, rhs, q=1):
+    """Mass^{-1} rhs for the block-diagonal DG(q) mass ((q + 1) x (q + 1) blocks)."""
+    if q != 1:
+        nl = q + 1
+        blk = Mass[:nl, :nl].toarray()  # uniform mesh: every cell's block is the same
+        return np.linalg.solve(blk, np.asarray(rhs).reshape(-1, nl).T).T.reshape(-1)
     d = Mass.diagonal()
     off = np.asarray(Mass[np.arange(0, Mass.shape[0], 2), np.arange(1, Mass.shape[0], 2)]).ravel()
     a, bb = d[0::2], d[1::2]
@@ -106,13 +181,14 @@ def solve_mass(Mass, rhs):
 
 def linforms(N=100, M=50, degree=1, T=1, space="DG", zinit=None):
     prob = problem(N=N, M=M, degree=degree, space=space)
-    Mass, G, Gpat, _ = dg1_operators(M, prob.mlength)
-    nf = 2 * M
+    q = int(degree)
+    Mass, G, Gpat, _ = dg_operators(M, prob.mlength, q)
+    nf = (q + 1) * M
     n = 3 * nf
     off = [0, nf, 2 * nf]
     if zinit is None:
-        u0 = project_dg1(lambda x: prob.exact(x, 0.0), M, prob.mlength)
-        w0 = solve_mass(Mass, G @ u0)  # gfuncproject, lkdv/lkdv.py:62-69,79
+        u0 = project_dg(lambda x: prob.exact(x, 0.0), M, prob.mlength, q)
+        w0 = solve_mass(Mass, G @ u0, q)  # gfuncproject, lkdv/lkdv.py:62-69,79
     else:
         zinit = np.asarray(zinit, dtype=np.float64)
         u0, w0 = zinit[:nf].copy(), zinit[2 * nf:].copy()

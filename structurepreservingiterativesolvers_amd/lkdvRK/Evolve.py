@@ -5,9 +5,9 @@ the exact travelling wave is recorded (``:80-81``, ``lkdvRK/lkdvRK.py:223-240``)
 
 ``pre`` defaults to the reference's host ``spilu(A, drop_tol=1e-4, fill_factor=10)`` (``:48-49``),
 built once (the stage operator is the same every step); ``pre=None`` runs unpreconditioned,
-and any object ``solvers.cgmres`` accepts as ``pre`` is passed through.  ``degree`` defaults to 1
-(the reference's default is 3): the synthetic assembly here is DG(1) only
-(``lkdvRK/assembly.py``)."""
+and any object ``solvers.cgmres`` accepts as ``pre`` is passed through.  ``degree`` defaults to 3
+as in the reference (``:19``); the synthetic assembly is DG(q) with an equispaced Lagrange basis
+(``lkdv/assembly.py`` ``dg_operators``), SURVEY §8 config C4 is its q = 1 case."""
 import numpy as np
 import scipy.sparse.linalg as spsla
 
@@ -20,18 +20,20 @@ _SPILU = object()
 
 def compute_error(forms, prob, zbig, t):
     """``lkdvRK/lkdvRK.py:223-240``: L2 norm of ``I(u_exact(t)) - u1`` with the exact solution
-    interpolated at the DG(1) nodes (cell end points, dof 2c at ``c h``, 2c+1 at ``(c+1) h``)."""
+    interpolated at the DG(q) nodes (dof (q+1) c + i at ``(c + i/q) h``; q = 1: the cell end
+    points)."""
     nf = forms["_step"]["nf"]
     Mass = forms["_step"]["Mass"]
     z1 = asm.z1calc(prob, zbig, forms["z0"])
-    M = nf // 2
+    q = int(prob.degree)
+    M = nf // (q + 1)
     h = prob.mlength / M
-    xn = np.stack([np.arange(M) * h, (np.arange(M) + 1) * h], axis=1).reshape(-1)
+    xn = ((np.arange(M)[:, None] + np.arange(q + 1)[None, :] / q) * h).reshape(-1)
     e = prob.exact(xn, t) - z1[:nf]
     return float(np.sqrt(e @ (Mass @ e)))
 
 
-def evolve(N=10, M=50, degree=1, tstages=2, T=1, k=50, tol=1e-6, contol=10, solver=ls.cgmresWrapper,
+def evolve(N=10, M=50, degree=3, tstages=2, T=1, k=50, tol=1e-6, contol=10, solver=ls.cgmresWrapper,
            pre=_SPILU):
     forms, prob = asm.linforms(N=N, M=M, degree=degree, tstages=tstages, T=T)
     if pre is _SPILU:

@@ -24,7 +24,7 @@ import copy
 import numpy as np
 
 from .._assembly import Triplets, embed_blocks, with_pattern
-from ..lkdv.assembly import dg1_operators, project_dg1, solve_mass
+from ..lkdv.assembly import dg_operators, project_dg, solve_mass
 
 
 def gauss_legendre(s):
@@ -58,8 +58,8 @@ class problem:
     """Mirror of ``lkdvRK/lkdvRK.py:16-46``."""
 
     def __init__(self, N, M, degree, tstages, space="DG", T=1):
-        if degree != 1 or space != "DG":
-            raise NotImplementedError("synthetic lkdvRK assembly supports DG1 only")
+        if int(degree) < 1 or space != "DG":
+            raise NotImplementedError("synthetic lkdvRK assembly supports DG(q), q >= 1")
         self.mlength = 40
         self.degree = degree
         self.tstages = tstages
@@ -81,16 +81,17 @@ class problem:
 
 def linforms(N=100, M=50, degree=1, tstages=2, T=10, t=0.0, zinit=None):
     prob = problem(N=N, M=M, T=T, degree=degree, tstages=tstages)
-    Mass, G, Gpat, _ = dg1_operators(M, prob.mlength)
-    nf = 2 * M
+    q = int(degree)
+    Mass, G, Gpat, _ = dg_operators(M, prob.mlength, q)
+    nf = (q + 1) * M
     dof = 3 * nf
     s = prob.ns
     n = s * dof
     off3 = [0, nf, 2 * nf]
     if zinit is None:
-        u0 = project_dg1(lambda x: prob.exact(x, t), M, prob.mlength)
-        w0 = solve_mass(Mass, G @ u0)  # w_finder, lkdvRK/lkdvRK.py:75-82
-        v0 = solve_mass(Mass, Mass @ u0 + G @ w0)  # v_finder, :64-73
+        u0 = project_dg(lambda x: prob.exact(x, t), M, prob.mlength, q)
+        w0 = solve_mass(Mass, G @ u0, q)  # w_finder, lkdvRK/lkdvRK.py:75-82
+        v0 = solve_mass(Mass, Mass @ u0 + G @ w0, q)  # v_finder, :64-73
     else:
         zinit = np.asarray(zinit, dtype=np.float64)
         u0, v0, w0 = zinit[:nf].copy(), zinit[nf:2 * nf].copy(), zinit[2 * nf:].copy()

@@ -1,0 +1,67 @@
+"""DG(q) operators of the synthetic lkdv / lkdvRK assembly (lkdv/assembly.py ``dg_operators``), on
+CPU.  The reference's lkdvRK driver defaults to degree 3 (``lkdvRK/Evolve.py:19``) and
+``lkdvRK/lkdvRK.py:48`` takes ``degree``.  Firedrake is absent, so these are exact element
+algebra checks, not a comparison with Firedrake's matrices (parity unpinned for q > 1):
+q = 1 is the round-1 DG(1) assembly bit for bit (the golden fixtures were made from it); for
+every q the mass integrates to the domain length, ``g`` annihilates constants and is skew on
+the periodic mesh (central flux), and Mass^-1 G u converges to u' under refinement."""
+import numpy as np
+import pytest
+
+from structurepreservingiterativesolvers_amd.lkdv import assembly as la
+from structurepreservingiterativesolvers_amd.lkdvRK import assembly as ra
+
+
+def test_degree1_is_the_dg1_assembly():
+    M, G, Gp, c = la.dg_operators(37, 40.0, 1)
+    M1, G1, Gp1, c1 = la.dg1_operators(37, 40.0)
+    for a, b in ((M, M1), (G, G1), (Gp, Gp1)):
+        assert (a != b).nnz == 0
+    f = lambda x: np.sin(x) + 2  # noqa: E731
+    assert np.array_equal(la.project_dg(f, 37, 40.0, 1), la.project_dg1(f, 37, 40.0))
+
+
+@pytest.mark.parametrize("q", [1, 2, 3, 4])
+def test_dgq_operator_identities(q):
+    L = 40.0
+    Mq, Gq, Gp, cdofs = la.dg_operators(25, L, q)
+    n = Mq.shape[0]
+    assert n == 25 * (q + 1) and cdofs.shape == (25, q + 1)
+    one = np.ones(n)
+    assert one @ Mq @ one == pytest.approx(L, rel=1e-13)
+    assert np.abs(Gq @ one).max() < 1e-13
+    rng = np.random.default_rng(q)
+    x, y = rng.normal(size=n), rng.normal(size=n)
+    assert abs(x @ Gq @ y + y @ Gq @ x) < 1e-12 * np.linalg.norm(x) * np.linalg.norm(y) * n
+    pat = Gp.copy()
+    pat.data[:] = 1.0
+    nzG = (abs(Gq) > 0).astype(float)
+    assert (nzG - nzG.multiply(pat)).count_nonzero() == 0  # G inside its facet pattern
+    # block-diagonal mass solve
+    r = rng.normal(size=n)
+    np.testing.assert_allclose(Mq @ la.solve_mass(Mq, r, q), r, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("q,rate", [(1, 1.0), (2, 3.0), (3, 3.0)])
+def test_dgq_derivative_converges(q, rate):
+    L = 40.0
+    errs = []
+    for M in (20, 40, 80):
+        Mq, Gq, _, _ = la.dg_operators(M, L, q)
+        u = la.project_dg(lambda x: np.sin(2 * np.pi * x / L), M, L, q)
+        du = la.solve_mass(Mq, Gq @ u, q)
+        ex = la.project_dg(lambda x: 2 * np.pi / L * np.cos(2 * np.pi * x / L), M, L, q)
+        e = du - ex
+        errs.append(np.sqrt(e @ Mq @ e))
+    rates = np.log2(np.array(errs[:-1]) / np.array(errs[1:]))
+    assert np.all(rates > rate - 0.1), rates
+
+
+def test_lkdv_and_lkdvrk_forms_at_degree3():
+    d, prob = la.linforms(M=30, degree=3)
+    nf = 4 * 30
+    assert d["A"].shape == (3 * nf, 3 * nf) and d["_step"]["nf"] == nf
+    dr, pr = ra.linforms(M=30, degree=3, tstages=2)
+    assert dr["A"].shape == (2 * 3 * nf, 2 * 3 * nf)
+    # the stage system at the initial state: mass omega . u0 as the DG(3) integral of u0
+    assert dr["m0"] == pytest.approx(float(dr["omega"][:nf] @ dr["z0"][:nf]))

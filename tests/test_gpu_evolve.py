@@ -129,9 +129,9 @@ def test_lkdvrk_evolve_spilu_vs_oracle_driver(spis, upload_counter):
     from structurepreservingiterativesolvers_amd.lkdvRK import Evolve, LinearSolver as ls, assembly as asm
 
     N, M, s, k, tol = 4, 50, 2, 40, 1e-8
-    out = Evolve.evolve(N=N, M=M, tstages=s, T=1, k=k, tol=tol)
+    out = Evolve.evolve(N=N, M=M, degree=1, tstages=s, T=1, k=k, tol=tol)
     assert upload_counter.inserts <= 4, upload_counter.inserts  # A, lifted zero / P'MP / P'KP
-    forms, prob = asm.linforms(N=N, M=M, tstages=s, T=1)
+    forms, prob = asm.linforms(N=N, M=M, degree=1, tstages=s, T=1)
     pre = spsla.spilu(forms["A"].tocsc(), drop_tol=1e-4, fill_factor=10)
     x_init = np.tile(forms["z0"], prob.ns)
     n_cmp = _per_step(
@@ -151,3 +151,32 @@ def test_lkdvrk_evolve_spilu_vs_oracle_driver(spis, upload_counter):
     scale = max(abs(forms["m0"]), abs(forms["mo0"]), abs(forms["e0"]))
     for key in ("dm", "dmo", "de"):
         assert out[key].max() <= 1e-9 * scale, (key, out[key])
+
+
+def test_lkdvrk_evolve_default_degree3_vs_oracle_driver(spis):
+    """The reference driver's default DG degree (``lkdvRK/Evolve.py:19``: degree = 3, DG(q)
+    assembly with an equispaced Lagrange basis): each step's stage solve matches the oracle from
+    the same state, and the u-error uses the DG(3) nodes."""
+    import scipy.sparse.linalg as spsla
+
+    from oracle import cgmres_port as port
+    from structurepreservingiterativesolvers_amd.lkdvRK import Evolve, LinearSolver as ls, assembly as asm
+
+    N, M, s, k, tol = 3, 30, 2, 60, 1e-8
+    out = Evolve.evolve(N=N, M=M, tstages=s, T=1, k=k, tol=tol)
+    forms, prob = asm.linforms(N=N, M=M, degree=3, tstages=s, T=1)
+    assert forms["A"].shape[0] == s * 3 * 4 * M
+    pre = spsla.spilu(forms["A"].tocsc(), drop_tol=1e-4, fill_factor=10)
+    x_init = np.tile(forms["z0"], prob.ns)
+    n_cmp = _per_step(
+        out, forms, N, asm.step_forms,
+        lambda f, x: port.cgmres(f["A"], f["b"], x_init if x is None else x, k, tol=tol, contol=10,
+                                 conlist=ls.constraints(f, prob), pre=pre),
+        lambda f, x: asm.z1calc(prob, x, f["z0"]), 1e-8, rtol_failed=1e-8)
+    assert n_cmp == N
+    nf = forms["_step"]["nf"]
+    h = prob.mlength / M
+    xn = ((np.arange(M)[:, None] + np.arange(4)[None, :] / 3) * h).reshape(-1)
+    for i in range(1, N + 1):
+        e = prob.exact(xn, out["time"][i]) - out["sol"][i][:nf]
+        assert out["err"][i] == pytest.approx(np.sqrt(e @ (forms["_step"]["Mass"] @ e)), rel=1e-12)
