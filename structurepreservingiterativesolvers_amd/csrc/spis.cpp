@@ -91,6 +91,10 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // ------------------------------------------------------------------------------------------------
 // objects
 // ------------------------------------------------------------------------------------------------
+// icwy_d layout: the one-reduce MGS's 2 nv - 1 dots (nv <= kCgsMax), slack, then partR (the true
+// residual partials), so that one all-reduce on several GPUs carries both
+constexpr int kIcwyROff = 2 * kCgsMax + 8;
+
 struct spis_context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -130,7 +134,7 @@ struct spis_context {
   // (K2w, icwy_*), 0 = one MGS step launch + all-reduce per projection
   int dist_mgs = 1;
   double* icwy_part = nullptr;      // 2 kCgsMax x kRedGrid partials
-  double* icwy_d = nullptr;         // the 2 nv - 1 reduced dots (+ the norm slot)
+  double* icwy_d = nullptr;         // the 2 nv - 1 reduced dots, then (at kIcwyROff) partR
   double* icwy_G = nullptr;         // kCgsMax x kCgsMax Gram rows G(l, m) = q_l . q_m, m < l
   double* ut_send = nullptr;        // several GPUs: the Ut rows a constraint matrix's halo sends
   size_t ut_send_len = 0;
@@ -630,12 +634,15 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     const int np = std::max(kSpmvGrid, kRedGrid);
     HIP_TRY(hipMalloc(&c->partA, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
-    HIP_TRY(hipMalloc(&c->partR, sizeof(double) * np));
+    // partR lives behind the one-reduce MGS's dot vector (icwy_d): on several GPUs the residual
+    // partials then ride in the same all-reduce as the dots (arnoldi_post_icwy)
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
     HIP_TRY(hipMalloc(&c->cgs_part, sizeof(double) * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
     HIP_TRY(hipMalloc(&c->icwy_part, sizeof(double) * 2 * kCgsMax * kRedGrid));
-    HIP_TRY(hipMalloc(&c->icwy_d, sizeof(double) * (2 * kCgsMax + 8)));
+    HIP_TRY(hipMalloc(&c->icwy_d, sizeof(double) * (kIcwyROff + np)));
+    HIP_TRY(hipMemset(c->icwy_d, 0, sizeof(double) * (kIcwyROff + np)));
+    c->partR = c->icwy_d + kIcwyROff;
     HIP_TRY(hipMalloc(&c->icwy_G, sizeof(double) * kCgsMax * kCgsMax));
     HIP_TRY(hipMemset(c->icwy_G, 0, sizeof(double) * kCgsMax * kCgsMax));
     HIP_TRY(hipMalloc(&c->chain_gran, sizeof(unsigned long long) * kChainGranLag));
@@ -704,7 +711,6 @@ extern "C" int spis_context_destroy(spis_context* c) {
     for (auto& kv : c->live_blocks) (void)hipFree(kv.first);
     (void)hipFree(c->partA);
     (void)hipFree(c->partB);
-    (void)hipFree(c->partR);
     (void)hipFree(c->dscal);
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
@@ -2343,7 +2349,12 @@ struct Solver {
     hipStream_t s = c->stream;
     c->prof_iter = j;
     if (icwy_lag()) arm_hcol(j);
-    if (xpart) {  // U_{j-2}'s residual (L mode): partials all-reduced, then reduced and published
+    // U_{j-2}'s residual (L mode): partials all-reduced, then reduced and published.  On several
+    // GPUs partR sits right behind the dot vector d, so one all-reduce carries both (3 collectives
+    // per Arnoldi step instead of 4); the residual is then published after the dot pass
+    // (one rank takes the same order, the all-reduce being the identity: the self-halo test covers it)
+    const bool merged = xpart != nullptr && xpart == c->partR && c->comm != nullptr;
+    if (xpart && !merged) {
       ST_TRY(allreduce(c, const_cast<double*>(xpart), gs));
       HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
     }
@@ -2357,7 +2368,12 @@ struct Solver {
     const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
     HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt));
     HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
-    ST_TRY(allreduce(c, d, 2 * nv - 1));
+    if (merged) {
+      ST_TRY(allreduce(c, d, kIcwyROff + gs));  // [d | slack | partR]
+      HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
+    } else {
+      ST_TRY(allreduce(c, d, 2 * nv - 1));
+    }
     HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
     // L mode: U_jx's GEMV in the same pass (x_jx = Z y + x0 over the local and ghost rows)
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
