@@ -620,6 +620,98 @@ int main(int argc, char** argv) {
     printf("%-44s %8.2f us  %7.0f GB/s  (%.0f%% of 8 TB/s)\n", name, us, bytes / (us * 1e-6) / 1e9,
            100.0 * bytes / (us * 1e-6) / 8e12);
   };
+  if (argc > 2 && std::string(argv[2]) == "cap4k") {
+    // the dual on 2,048- vs 4,096-nnz row blocks (<= 256 rows each), both in slab order with the
+    // slab key, 32-bit columns, resident grids; warm and cold; rows compared
+    double *dx2, *dw, *dw2, *db, *pa, *pb;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&dw2, 8 * pitch));
+    CK(hipMalloc(&db, 8 * pitch));
+    CK(hipMalloc(&pa, 8 * 16384));
+    CK(hipMalloc(&pb, 8 * 16384));
+    std::vector<double> h2(pitch);
+    for (int64_t i = 0; i < pitch; ++i) h2[i] = i < n ? 1e-3 * ((i * 104729) % 997) - 0.4 : 0.0;
+    CK(hipMemcpy(dx2, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    std::vector<uint8_t> lab;
+    std::vector<double> key;
+    if (!slab_labels(n, rp.data(), ci.data(), lab, &key)) return 1;
+    auto table = [&](int cap, int& nb_out) {
+      std::vector<int32_t> blk, pairs;
+      blocks(n, rp.data(), cap + 256, 256, cap, blk);
+      nb_out = static_cast<int>(blk.size()) - 1;
+      if (!build_slab_order(rp.data(), lab, blk, pairs, nullptr, &key)) {
+        printf("no slab order\n");
+        exit(1);
+      }
+      int2* d;
+      CK(hipMalloc(&d, 4 * pairs.size()));
+      CK(hipMemcpy(d, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice));
+      return d;
+    };
+    int nb2 = 0, nb4 = 0;
+    int2* t2 = table(2048, nb2);
+    int2* t4 = table(4096, nb4);
+    const int64_t big = int64_t(1) << 26;
+    double* bx;
+    CK(hipMalloc(&bx, 8 * big));
+    CK(hipMemset(bx, 0, 8 * big));
+    const int g2 = resident_grid(spmv_pipe_kernel<2048, 4>);
+    const int g4 = resident_grid(spmv_pipe_kernel<4096, 4, false, 2>);
+    printf("blocks %d / %d, resident grids %d / %d\n", nb2, nb4, g2, g4);
+    auto run = [&](const char* name, auto&& launch) {
+      for (int cold = 0; cold < 2; ++cold) {
+        double tot = 0;
+        const int reps = 20;
+        for (int r = 0; r < reps + 3; ++r) {
+          if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                                       reinterpret_cast<const double2*>(bx), pb + 8192);
+          launch();
+          CK(hipEventSynchronize(e1));
+          float ms_;
+          CK(hipEventElapsedTime(&ms_, e0, e1));
+          if (r >= 3) tot += ms_;
+        }
+        const double us = 1e3 * tot / reps;
+        printf("%s %-36s %8.2f us  %7.0f GB/s  (%.3f of 8 TB/s)\n", cold ? "COLD" : "WARM", name, us,
+               SD / (us * 1e-6) / 1e9, SD / (us * 1e-6) / 8e12);
+        fflush(stdout);
+      }
+    };
+    char nm[96];
+    for (int g : {g2, g2 * 4 / 3 / 8 * 8}) {
+      snprintf(nm, sizeof nm, "cap 2048 grid %d", g);
+      run(nm, [&] {
+        hipExtLaunchKernelGGL((spmv_pipe_kernel<2048, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva, t2,
+                              nb2, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr,
+                              (const int4*)nullptr);
+      });
+    }
+    for (int g : {g4, 512}) {
+      snprintf(nm, sizeof nm, "cap 4096 WPE2 grid %d", g);
+      run(nm, [&] {
+        hipExtLaunchKernelGGL((spmv_pipe_kernel<4096, 4, false, 2>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci,
+                              dva, t4, nb4, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb,
+                              (const uint16_t*)nullptr, (const int4*)nullptr);
+      });
+      snprintf(nm, sizeof nm, "cap 4096 WPE2 BUF grid %d", g);
+      run(nm, [&] {
+        hipExtLaunchKernelGGL((spmv_pipe_kernel<4096, 4, false, 2, false, true>), dim3(g), dim3(kBlock), 0, s, e0, e1,
+                              0, drp, dci, dva, t4, nb4, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb,
+                              (const uint16_t*)nullptr, (const int4*)nullptr);
+      });
+    }
+    std::vector<double> w1(n), w2(n);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(w2.data(), dw2, 8 * n, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+    printf("cap 4096 vs 2048, dual rows: %lld differ\n", (long long)bad);
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "slab") {
     // the solver's dual (kPipeCap table) in natural vs slab block order, resident grid vs more
     // workgroups, nontemporal matrix loads; warm (back to back: the matrix Infinity-Cache
