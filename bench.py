@@ -212,6 +212,8 @@ def main():
     ap.add_argument("--spmv-nt", type=int, default=0, choices=[0, 1, 2],
                     help="nontemporal matrix stream in the pipelined SpMV (SPIS_OPT_SPMV_NT): 0 never, 1 always, "
                          "2 beyond the 256 MB Infinity Cache")
+    ap.add_argument("--c16-tm", type=int, default=0, choices=[0, 1],
+                    help="thread-major 16-bit column copy (SPIS_OPT_C16_TM, at upload)")
     ap.add_argument("--spmv-w4", type=int, default=0, choices=[0, 1],
                     help="pipelined SpMV at 4 waves per SIMD (SPIS_OPT_SPMV_W4)")
     ap.add_argument("--slab-key", type=int, default=1, choices=[0, 1],
@@ -238,6 +240,7 @@ def main():
     n = A.shape[0]
     ctx = get_context(0)
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SLAB_KEY, args.slab_key), "spis_set_option")
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_C16_TM, args.c16_tm), "spis_set_option")
     device_matrix(A, ctx=ctx)
     bd = DeviceVector.from_host(wl["b"], ctx=ctx)
     x0 = np.zeros(n)

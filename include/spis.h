@@ -206,7 +206,11 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  * SPIS_OPT_SPMV_W4 (default 0): the pipelined SpMV (one-deep, not nontemporal) in its 4-waves-per-
  *   SIMD form: matrix stream and gathers through buffer descriptors, the next block's values
  *   loaded once the current products are in LDS, partial sums in LDS (<= 128 VGPRs, 4 workgroups
- *   per CU instead of 3).  Rows bit-identical; partials grouped per workgroup (roundoff). */
+ *   per CU instead of 3).  Rows bit-identical; partials grouped per workgroup (roundoff).
+ * SPIS_OPT_C16_TM (default 0): read at spis_matrix_create.  1 = the 16-bit column copy is also
+ *   kept thread-major per slab-order block (each thread's 8 columns contiguous: one 16-B load
+ *   instead of 8 two-byte loads per block); used by the slab-ordered pipelined SpMV on 16-bit
+ *   columns.  Same columns, same arithmetic: bit-identical. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
   SPIS_OPT_GENERIC_GRAM = 2,
@@ -224,7 +228,8 @@ enum spis_option {
   SPIS_OPT_K7T_SLOTS = 14,
   SPIS_OPT_LAG_MODE = 15,
   SPIS_OPT_SLAB_KEY = 16,
-  SPIS_OPT_SPMV_W4 = 17
+  SPIS_OPT_SPMV_W4 = 17,
+  SPIS_OPT_C16_TM = 18
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

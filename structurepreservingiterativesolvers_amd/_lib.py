@@ -33,6 +33,7 @@ OPT_K7T_SLOTS = 14
 OPT_LAG_MODE = 15
 OPT_SLAB_KEY = 16
 OPT_SPMV_W4 = 17
+OPT_C16_TM = 18
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",

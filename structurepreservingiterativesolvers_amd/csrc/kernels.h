@@ -63,6 +63,9 @@ struct CsrView {
   // stream and gathers, the next block's values loaded after the current products are in LDS
   // (SPIS_OPT_SPMV_W4; one-deep, not nontemporal)
   bool w4 = false;
+  // C16 columns thread-major per block (col16.h build_col16_tm; col16 then points at that copy, in
+  // the table's block order): one 16-B column load per thread and block (SPIS_OPT_C16_TM)
+  bool c16tm = false;
   // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
   // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at
   // sl_off[s] + 64 t + l; rows padded to the slice's longest (col = the row, val = 0, skipped

@@ -340,7 +340,7 @@ __device__ __forceinline__ void pipe_load_vals(PipeStage<CAP>& st, const double*
     st.vals[u] = threadIdx.x + u * kBlock < st.nnz ? buf_ld1s(rv, threadIdx.x * 8, u * kBlock * 8) : 0.0;
 }
 
-template <int CAP, int MODE, bool NT = false, bool C16 = false, bool BUF = false, bool VALS = true>
+template <int CAP, int MODE, bool NT = false, bool C16 = false, bool BUF = false, bool VALS = true, bool TM = false>
 __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int lb, int ms,
                                           const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                           const uint16_t* __restrict__ c16, const int4* __restrict__ base,
@@ -360,7 +360,25 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
   st.nz0 = m0.y;
   st.nnz = m1.y - m0.y;
   if (st.nnz > CAP) return;  // long row: read directly by the workgroup-wide path
-  if constexpr (BUF && !NT) {
+  if constexpr (TM && C16 && !NT && !BUF) {
+    // thread-major copy: this thread's kPer 16-bit columns in one 16-B load (no long rows here:
+    // the host builds the copy only for matrices without them)
+    static_assert(PipeStage<CAP>::kPer == 8, "one 16-B load = 8 columns");
+    const uint4 v = *reinterpret_cast<const uint4*>(c16 + static_cast<int64_t>(lb) * CAP + threadIdx.x * 8);
+    st.cols[0] = static_cast<int>(v.x & 0xffffu);
+    st.cols[1] = static_cast<int>(v.x >> 16);
+    st.cols[2] = static_cast<int>(v.y & 0xffffu);
+    st.cols[3] = static_cast<int>(v.y >> 16);
+    st.cols[4] = static_cast<int>(v.z & 0xffffu);
+    st.cols[5] = static_cast<int>(v.z >> 16);
+    st.cols[6] = static_cast<int>(v.w & 0xffffu);
+    st.cols[7] = static_cast<int>(v.w >> 16);
+#pragma unroll
+    for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
+    }
+  } else if constexpr (BUF && !NT) {
     // buffer descriptors based at the block's first nonzero: every load of the block shares the
     // lane offset, its distance u * kBlock elements rides in the scalar offset (no 64-bit address
     // registers per element, which is what kept the stage at 3 waves per SIMD)
@@ -430,7 +448,7 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
 // BUF: the matrix stream and the gathers through buffer descriptors (32-bit lane offsets), which
 // frees the registers for WPE = 4 waves per SIMD (4 workgroups per CU instead of 3)
-template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false>
+template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false, bool TM = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE > 3 ? WPE : (C16 ? 3 : 8)))) void spmv_pipe_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
@@ -490,7 +508,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
         if (LATEV) s_pt[0] = make_double2(pt1, pt2);
       }
       nxt.nnz = 0;
-      if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+      if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, true, TM>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
       return;
     }
     // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
@@ -508,7 +526,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
       }
     }
     nxt.nnz = 0;
-    if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, !LATEV>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+    if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, !LATEV, TM>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
     // entry i = tid + u kBlock sits at i + i/16 = (tid + tid/16) + u (kBlock + kBlock/16): one base
     // register and an immediate offset per u (the compiler's own form of i + i/16 kept 8 addresses
     // live, which spilled at 4 waves per SIMD)
@@ -597,7 +615,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
     __syncthreads();
   };
   PipeStage<CAP> sa, sb;
-  if (b0 < b1) pipe_load<CAP, MODE, NT, C16, BUF>(sa, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE, NT, C16, BUF, true, TM>(sa, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += 2 * bs) {
     step(sa, sb, blk);
     if (blk + bs >= b1) break;
@@ -862,6 +880,9 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   if (A.depth == 2)                                                                                        \
     launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
+  else if (A.c16tm && A.col16 != nullptr && !A.nt && !A.w4)                                                     \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true, false, true>, g, b, 0, s, ev, A.indptr, A.indices,      \
+             A.vals, A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base); \
   else if (A.w4 && A.col16 != nullptr)                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
              A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \

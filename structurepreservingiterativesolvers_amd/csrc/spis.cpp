@@ -151,6 +151,7 @@ struct spis_context {
   int lag_mode = 1;                 // SPIS_OPT_LAG_MODE: 1 = L mode where it applies, 0 = never
   int slab_key = 1;                 // SPIS_OPT_SLAB_KEY: slab order's blocks by position within a slab (at upload)
   int spmv_w4 = 0;                  // SPIS_OPT_SPMV_W4: the pipelined SpMV at 4 waves per SIMD (buffer-descriptor form)
+  int c16tm = 0;                    // SPIS_OPT_C16_TM: thread-major 16-bit column copy (built at upload)
   int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
   hipStream_t stream2 = nullptr;
@@ -201,6 +202,7 @@ struct spis_matrix {
   uint16_t* col16_d = nullptr;   // C16 copy of the columns (col16.h), or null
   int4* base_nat_d = nullptr;     // its per-block bases, natural block order
   int4* base_slab_d = nullptr;    // the same in slab order
+  uint16_t* col16t_slab_d = nullptr;  // the 16-bit columns thread-major per slab-order block (SPIS_OPT_C16_TM)
   // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
   int32_t* ell_col = nullptr;
   double* ell_val = nullptr;
@@ -336,6 +338,10 @@ CsrView spis_matrix::dual_view() const {
     if (v.depth == 1 && use_col16()) {
       v.col16 = col16_d;
       v.blk_base = base_slab_d;
+      if (col16t_slab_d != nullptr && ctx->c16tm) {
+        v.col16 = col16t_slab_d;
+        v.c16tm = true;
+      }
     }
     return v;
   }
@@ -817,6 +823,10 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "lag_mode %lld: 0 or 1", (long long)value);
         c->lag_mode = static_cast<int>(value);
         return SPIS_OK;
+      case SPIS_OPT_C16_TM:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "c16_tm %lld: 0 or 1", (long long)value);
+        c->c16tm = static_cast<int>(value);
+        return SPIS_OK;
       case SPIS_OPT_SPMV_W4:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "spmv_w4 %lld: 0 or 1", (long long)value);
         c->spmv_w4 = static_cast<int>(value);
@@ -1077,6 +1087,17 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
                       bs.begin() + kCol16Bases * i);
           HIP_TRY(hipMalloc(&M->base_slab_d, sizeof(int32_t) * bs.size()));
           HIP_TRY(hipMemcpy(M->base_slab_d, bs.data(), sizeof(int32_t) * bs.size(), hipMemcpyHostToDevice));
+          if (c->c16tm && M->n_long == 0) {  // thread-major copy in slab order (no long-row block)
+            std::vector<int32_t> rng(2 * order.size());
+            for (size_t i = 0; i < order.size(); ++i) {
+              rng[2 * i] = pairs[4 * i + 1];
+              rng[2 * i + 1] = pairs[4 * i + 3];
+            }
+            std::vector<uint16_t> tm;
+            build_col16_tm(c16, rng, kPipeCap, kBlock, tm);
+            HIP_TRY(hipMalloc(&M->col16t_slab_d, sizeof(uint16_t) * tm.size()));
+            HIP_TRY(hipMemcpy(M->col16t_slab_d, tm.data(), sizeof(uint16_t) * tm.size(), hipMemcpyHostToDevice));
+          }
         }
       }
     }
@@ -1131,6 +1152,7 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->col16_d);
     (void)hipFree(M->base_nat_d);
     (void)hipFree(M->base_slab_d);
+    (void)hipFree(M->col16t_slab_d);
     (void)hipFree(M->blk_slab_d);
     if (M->ell_col) (void)hipFree(M->ell_col);
     if (M->ell_val) (void)hipFree(M->ell_val);

@@ -72,6 +72,7 @@ _OPTIONS = {
     "lag_mode": (_lib.OPT_LAG_MODE, None),
     "slab_key": (_lib.OPT_SLAB_KEY, None),
     "spmv_w4": (_lib.OPT_SPMV_W4, None),
+    "c16_tm": (_lib.OPT_C16_TM, None),
 }
 
 
@@ -120,7 +121,9 @@ def set_option(name, value, ctx=None):
       column, carrying the update GEMV); False: the plain pipelined order;
     * ``slab_key`` (True): matrices uploaded afterwards order the row blocks of a slab by their
       rows' position, so a slab's DoF groups are walked side by side (False: group after group);
-    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form."""
+    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form;
+    * ``c16_tm`` (False): matrices uploaded afterwards also keep their 16-bit columns thread-major
+      per slab-order block (one 16-B column load per thread and block); bit-identical."""
     ctx = ctx or get_context()
     if name == "device_ilu":
         if value not in (True, False, "auto"):

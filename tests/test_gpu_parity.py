@@ -128,6 +128,37 @@ def test_spmv_w4_bit_exact_vs_scipy(spis, pipe, col16):
         set_option("spmv_w4", False)
 
 
+def test_spmv_c16_thread_major_bit_exact_vs_scipy(spis):
+    """SPIS_OPT_C16_TM: the slab-ordered pipelined SpMV reading its 16-bit columns from the
+    thread-major copy (one 16-B load per thread and block) is bit-exact vs SciPy, and the solver's
+    iterates are bitwise those of the plain 16-bit copy (same columns, same arithmetic)."""
+    from structurepreservingiterativesolvers_amd import primitives as P
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    rng = np.random.default_rng(11)
+    dic, _ = sa.linforms(M=30)
+    cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+    outs = []
+    set_option("col16", True)
+    try:
+        for tm in (False, True):
+            set_option("c16_tm", tm)
+            A = dic["A"].copy()  # a new object: uploaded again under the option
+            x = rng.normal(size=A.shape[1]) if not outs else outs[0][0]
+            y = P.spmv(A, x)
+            assert np.array_equal(y, A @ x)
+            xs, d = solvers.cgmres(A, dic["b"], np.zeros_like(dic["b"]), 25, tol=1e-19, conlist=cons)
+            outs.append((x, xs, np.asarray(d["res"]), d["x"].trace))
+    finally:
+        set_option("c16_tm", False)
+        set_option("col16", "auto")
+    assert np.array_equal(outs[0][1], outs[1][1]) and np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
 @pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd_natural"])
 def test_spmv_col16_bit_exact_vs_scipy(spis, pipe):
     """The pipelined SpMV on the 16-bit column copy (SPIS_OPT_COL16 = 2: forced at any size; by
