@@ -214,8 +214,9 @@ def main():
                          "2 beyond the 256 MB Infinity Cache")
     ap.add_argument("--c16-tm", type=int, default=0, choices=[0, 1],
                     help="thread-major 16-bit column copy (SPIS_OPT_C16_TM, at upload)")
-    ap.add_argument("--spmv-w4", type=int, default=0, choices=[0, 1],
-                    help="pipelined SpMV at 4 waves per SIMD (SPIS_OPT_SPMV_W4)")
+    ap.add_argument("--spmv-w4", type=int, default=0, choices=[0, 1, 2],
+                    help="pipelined SpMV at 4 waves per SIMD (1) or its buffer-descriptor form at 3 (2) "
+                         "(SPIS_OPT_SPMV_W4)")
     ap.add_argument("--slab-key", type=int, default=1, choices=[0, 1],
                     help="SpMV row blocks of a slab by position (SPIS_OPT_SLAB_KEY, at upload): 1 groups side by "
                          "side, 0 group after group")

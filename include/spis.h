@@ -206,7 +206,8 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  * SPIS_OPT_SPMV_W4 (default 0): the pipelined SpMV (one-deep, not nontemporal) in its 4-waves-per-
  *   SIMD form: matrix stream and gathers through buffer descriptors, the next block's values
  *   loaded once the current products are in LDS, partial sums in LDS (<= 128 VGPRs, 4 workgroups
- *   per CU instead of 3).  Rows bit-identical; partials grouped per workgroup (roundoff).
+ *   per CU instead of 3); 2 = the buffer-descriptor form at 3 waves per SIMD.  Rows
+ *   bit-identical; partials grouped per workgroup (roundoff).
  * SPIS_OPT_C16_TM (default 0): read at spis_matrix_create.  1 = the 16-bit column copy is also
  *   kept thread-major per slab-order block (each thread's 8 columns contiguous: one 16-B load
  *   instead of 8 two-byte loads per block); used by the slab-ordered pipelined SpMV on 16-bit

@@ -63,6 +63,7 @@ struct CsrView {
   // stream and gathers, the next block's values loaded after the current products are in LDS
   // (SPIS_OPT_SPMV_W4; one-deep, not nontemporal)
   bool w4 = false;
+  bool buf = false;  // the buffer-descriptor form at the default 3 waves per SIMD (SPIS_OPT_SPMV_W4 = 2)
   // C16 columns thread-major per block (col16.h build_col16_tm; col16 then points at that copy, in
   // the table's block order): one 16-B column load per thread and block (SPIS_OPT_C16_TM)
   bool c16tm = false;

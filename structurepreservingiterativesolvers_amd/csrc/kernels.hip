@@ -883,6 +883,12 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   else if (A.c16tm && A.col16 != nullptr && !A.nt && !A.w4)                                                     \
     launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true, false, true>, g, b, 0, s, ev, A.indptr, A.indices,      \
              A.vals, A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base); \
+  else if (A.buf && A.col16 != nullptr && !A.nt)                                                                \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
+  else if (A.buf && !A.nt)                                                                                      \
+    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, false, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, \
+             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);            \
   else if (A.w4 && A.col16 != nullptr)                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
              A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \

@@ -329,6 +329,7 @@ CsrView spis_matrix::dual_view() const {
   if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
   v.nt = ctx->spmv_nt == 1 || (ctx->spmv_nt == 2 && 12.0 * static_cast<double>(nnz) > 256.0 * 1024 * 1024);
   v.w4 = ctx->spmv_w4 == 1 && !v.nt && n_cols + n_ghost < (int64_t{1} << 28);  // 32-bit byte offsets
+  v.buf = ctx->spmv_w4 == 2 && !v.nt && n_cols + n_ghost < (int64_t{1} << 28);
   if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
   else if ((mode == 2 || mode == 4) && blk_slab_d != nullptr) {
     v.blk_meta = blk_slab_d;
@@ -828,7 +829,7 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         c->c16tm = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SPMV_W4:
-        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "spmv_w4 %lld: 0 or 1", (long long)value);
+        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "spmv_w4 %lld: 0, 1 or 2", (long long)value);
         c->spmv_w4 = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_SLAB_KEY:

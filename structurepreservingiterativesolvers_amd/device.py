@@ -71,7 +71,7 @@ _OPTIONS = {
     "k7t_slots": (_lib.OPT_K7T_SLOTS, {16: 16, 32: 32}),
     "lag_mode": (_lib.OPT_LAG_MODE, None),
     "slab_key": (_lib.OPT_SLAB_KEY, None),
-    "spmv_w4": (_lib.OPT_SPMV_W4, None),
+    "spmv_w4": (_lib.OPT_SPMV_W4, {False: 0, True: 1, "buf": 2, 2: 2}),
     "c16_tm": (_lib.OPT_C16_TM, None),
 }
 
@@ -121,7 +121,8 @@ def set_option(name, value, ctx=None):
       column, carrying the update GEMV); False: the plain pipelined order;
     * ``slab_key`` (True): matrices uploaded afterwards order the row blocks of a slab by their
       rows' position, so a slab's DoF groups are walked side by side (False: group after group);
-    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form;
+    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form
+      (True), or the buffer-descriptor form at the default 3 waves per SIMD ("buf");
     * ``c16_tm`` (False): matrices uploaded afterwards also keep their 16-bit columns thread-major
       per slab-order block (one 16-B column load per thread and block); bit-identical."""
     ctx = ctx or get_context()

@@ -96,9 +96,10 @@ def test_spmv_bit_exact_vs_scipy(spis, pipe):
         set_option("spmv_pipe", "auto")
 
 
+@pytest.mark.parametrize("form", [True, "buf"])
 @pytest.mark.parametrize("col16", [False, True])
 @pytest.mark.parametrize("pipe", ["xcd", "stride", "xcd_natural"])
-def test_spmv_w4_bit_exact_vs_scipy(spis, pipe, col16):
+def test_spmv_w4_bit_exact_vs_scipy(spis, pipe, col16, form):
     """SPIS_OPT_SPMV_W4: the pipelined SpMV's 4-waves-per-SIMD form (buffer-descriptor matrix
     stream and gathers, late value loads, partial sums in LDS), on 32- and 16-bit columns: rows
     bit-exact vs SciPy, the residual-norm epilogue to 1e-12, long rows 1e-12."""
@@ -108,7 +109,7 @@ def test_spmv_w4_bit_exact_vs_scipy(spis, pipe, col16):
     rng = np.random.default_rng(7)
     set_option("spmv_pipe", pipe)
     set_option("col16", col16)
-    set_option("spmv_w4", True)
+    set_option("spmv_w4", form)
     try:
         for name, A in _matrices().items():
             x = rng.normal(size=A.shape[1])
