@@ -8,7 +8,7 @@ SRC      := $(PKG)/csrc
 LIB      := $(PKG)/libspis.so
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I include -I $(SRC)
 HIPFLAGS := --offload-arch=$(ARCH) -munsafe-fp-atomics
-OBJS     := build/kernels.o build/sptrsv.o build/spis.o build/lsq.o build/ilu_plan.o
+OBJS     := build/kernels.o build/sptrsv.o build/spis.o build/lsq.o build/ilu_plan.o build/hash.o
 
 all: $(LIB) $(PKG)/liblsq_host.so
 
@@ -28,12 +28,16 @@ build/ilu_plan.o: $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h
 	@mkdir -p build
 	g++ $(CXXFLAGS) -c $< -o $@
 
+build/hash.o: $(SRC)/hash.cpp include/spis.h
+	@mkdir -p build
+	g++ $(CXXFLAGS) -c $< -o $@
+
 build/lsq.o: $(SRC)/lsq.cpp $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
 	g++ $(CXXFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
 
 # host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
 $(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp \

@@ -85,13 +85,36 @@ def dual_bytes(n_rows, nnz, col_bytes=4):
     return (8 + col_bytes) * nnz + 4 * (n_rows + 1) + 32 * n_rows
 
 
-def load_traffic(name="spmv_traffic.json"):
-    """Per-launch HBM bytes of a kernel from a committed PMC summary under profiles/, if any."""
-    path = os.path.join(ROOT, "profiles", name)
-    if os.path.exists(path):
-        with open(path) as f:
-            return json.load(f)
-    return None
+def k_per_solve(k):
+    """MGS chains per CGMRES(k) solve (one per Arnoldi step)."""
+    return k
+
+
+def kernels_sha256():
+    import hashlib
+
+    with open(os.path.join(ROOT, "structurepreservingiterativesolvers_amd", "csrc", "kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def load_traffic(args, c16, pipe):
+    """Per-launch PMC bytes from profiles/r04_traffic_<config>.json (tools/r04_pmc.sh), with the
+    reason when there are none: the file must have been measured on this csrc/kernels.hip (SHA-256)
+    with this run's SpMV and chain options, on the configuration's default size."""
+    path = os.path.join(ROOT, "profiles", f"r04_traffic_{args.config}.json")
+    if args.M is not None:
+        return {}, "no PMC traffic for a non-default mesh size"
+    if not os.path.exists(path):
+        return {}, f"no {os.path.relpath(path, ROOT)}"
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("kernels_sha256") != kernels_sha256():
+        return {}, f"{os.path.relpath(path, ROOT)} was measured on another kernels.hip (git {t.get('git_rev')})"
+    want = {"spmv_pipe": pipe, "col16": bool(c16), "slab_key": args.slab_key, "chain": args.chain,
+            "nt_basis": args.nt_basis, "orthog": args.orthog, "fuse": not args.no_fuse}
+    if t.get("options") != want:
+        return {}, f"{os.path.relpath(path, ROOT)} was measured with options {t.get('options')}, this run {want}"
+    return t.get("bytes_per_launch", {}), f"{os.path.relpath(path, ROOT)} (git {t.get('git_rev')})"
 
 
 def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
@@ -185,38 +208,20 @@ def main():
     ap.add_argument("--dist-mgs", type=int, default=1, choices=[0, 1],
                     help="several GPUs (SPIS_OPT_DIST_MGS): 1 MGS's projections in one all-reduce per Arnoldi "
                          "step, 0 one all-reduce per projection")
-    ap.add_argument("--graphs", action="store_true", help="replay captured Arnoldi steps (SPIS_OPT_GRAPHS)")
     ap.add_argument("--no-fuse", action="store_true", help="separate residual and Arnoldi SpMV launches")
-    ap.add_argument("--no-overlap", action="store_true", help="update GEMV on the main stream (no side stream)")
-    ap.add_argument("--gemv-sync", type=int, default=1, choices=[1, 2],
-                    help="how the dual SpMV waits for the side-stream GEMV (SPIS_OPT_OVERLAP_GEMV): "
-                         "1 stream write/wait on a device word, 2 the GEMV launch's completion event")
     ap.add_argument("--chain", type=int, default=3, choices=[0, 1, 2, 3, 4],
                     help="MGS chain (SPIS_OPT_MGS_CHAIN): 0 per-step launches, 1 persistent chain gathered by "
-                         "workgroup 0, 2 with a dedicated gathering workgroup, 3 pipelined (dots one step early), "
+                         "workgroup 0, 2 with a dedicated gathering workgroup, 3 pipelined (dots two steps early), "
                          "4 one-reduce two-pass MGS carrying the update GEMV")
     ap.add_argument("--nt-basis", type=int, default=2, choices=[0, 1, 2],
-                    help="MGS chain basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
-    ap.add_argument("--lag-mode", type=int, default=1, choices=[0, 1],
-                    help="L-mode schedule (SPIS_OPT_LAG_MODE): 1 where the MGS kernel supports it, 0 never")
-    ap.add_argument("--early-con", type=int, default=0, choices=[0, 1, 2],
-                    help="final step's constraint reduction (SPIS_OPT_EARLY_CON): 0 when reached, early on a "
-                         "third stream once A_{k-2} (1) / A_{k-1} (2) is queued")
-    ap.add_argument("--gram", default="mfma", choices=["staged", "ell", "csr", "mfma", "mfma_full"],
-                    help="constraint-Gram matrix form (SPIS_OPT_ELL_GRAM)")
-    ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "stride2", "xcd2", "auto", "sell", "xcd_natural"],
+                    help="MGS basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 never, 1 always, 2 auto")
+    ap.add_argument("--gram", default="mfma", choices=["generic", "csr", "mfma", "mfma_full"],
+                    help="constraint reduction (SPIS_OPT_CON_GRAM)")
+    ap.add_argument("--spmv-pipe", default="auto", choices=["off", "stride", "xcd", "auto", "xcd_natural"],
                     help="solver SpMV kernels (SPIS_OPT_SPMV_PIPE): unpipelined, pipelined grid-stride, "
-                         "pipelined XCD-local walk")
+                         "pipelined XCD-local walk (slab order / natural order)")
     ap.add_argument("--col16", type=int, default=1, choices=[0, 1, 2],
                     help="16-bit column copy for the pipelined SpMV: 1 beyond the Infinity Cache, 2 always, 0 never")
-    ap.add_argument("--spmv-nt", type=int, default=0, choices=[0, 1, 2],
-                    help="nontemporal matrix stream in the pipelined SpMV (SPIS_OPT_SPMV_NT): 0 never, 1 always, "
-                         "2 beyond the 256 MB Infinity Cache")
-    ap.add_argument("--c16-tm", type=int, default=0, choices=[0, 1],
-                    help="thread-major 16-bit column copy (SPIS_OPT_C16_TM, at upload)")
-    ap.add_argument("--spmv-w4", type=int, default=0, choices=[0, 1, 2],
-                    help="pipelined SpMV at 4 waves per SIMD (1) or its buffer-descriptor form at 3 (2) "
-                         "(SPIS_OPT_SPMV_W4)")
     ap.add_argument("--slab-key", type=int, default=1, choices=[0, 1],
                     help="SpMV row blocks of a slab by position (SPIS_OPT_SLAB_KEY, at upload): 1 groups side by "
                          "side, 0 group after group")
@@ -240,39 +245,26 @@ def main():
     A = wl["A"]
     n = A.shape[0]
     ctx = get_context(0)
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SLAB_KEY, args.slab_key), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_C16_TM, args.c16_tm), "spis_set_option")
-    device_matrix(A, ctx=ctx)
+    opt = {_lib.OPT_SLAB_KEY: args.slab_key, _lib.OPT_FUSE_SPMV: 0 if args.no_fuse else 1,
+           _lib.OPT_ORTHOG: 1 if args.orthog == "cgs2" else 0, _lib.OPT_MGS_CHAIN: args.chain,
+           _lib.OPT_NT_BASIS: args.nt_basis, _lib.OPT_COL16: args.col16,
+           _lib.OPT_CON_GRAM: {"generic": 0, "csr": 1, "mfma": 2, "mfma_full": 3}[args.gram],
+           _lib.OPT_SPMV_PIPE: {"off": 0, "stride": 1, "xcd": 2, "auto": 5, "xcd_natural": 7}[args.spmv_pipe]}
+    for k, v in opt.items():
+        _lib.check(ctx.L.spis_set_option(ctx.handle, k, v), "spis_set_option")
+    Ad = device_matrix(A, ctx=ctx)  # inputs resident in HBM before timing (the operator, b, x0, constraints)
     bd = DeviceVector.from_host(wl["b"], ctx=ctx)
     x0 = np.zeros(n)
     x0d = DeviceVector.from_host(x0, ctx=ctx)
     conlist = wl["conlist"]
-    conlist_dev = device_constraints(conlist, ctx=ctx)  # inputs resident in HBM before timing
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_GRAPHS, 1 if args.graphs else 0), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 0 if args.no_fuse else 1), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, 0 if args.no_overlap else args.gemv_sync),
-               "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1 if args.orthog == "cgs2" else 0),
-               "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, args.chain), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_EARLY_CON, args.early_con), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_COL16, args.col16), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_LAG_MODE, args.lag_mode), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_W4, args.spmv_w4), "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ELL_GRAM, {"csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}[args.gram]),
-               "spis_set_option")
-    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
-                                                                       "sell": 6, "xcd_natural": 7}[args.spmv_pipe]),
-               "spis_set_option")
+    conlist_dev = device_constraints(conlist, ctx=ctx)
 
     if wl["cycles"] > 1:
         def solve():
-            return solvers.cgmres_restarted(A, bd, x0d, args.k, wl["cycles"], tol=args.tol, conlist=conlist_dev)
+            return solvers.cgmres_restarted(Ad, bd, x0d, args.k, wl["cycles"], tol=args.tol, conlist=conlist_dev)
     else:
         def solve():
-            return solvers.cgmres(A, bd, x0d, args.k, tol=args.tol, conlist=conlist_dev)
+            return solvers.cgmres(Ad, bd, x0d, args.k, tol=args.tol, conlist=conlist_dev)
 
     for _ in range(args.warmup):
         solve()
@@ -317,53 +309,52 @@ def main():
     mgs_gbs = mgs_b / (mgs_ms * 1e-3) / 1e9 if mgs_ms > 0 and args.orthog == "mgs" else None
     res_ms = ms[_lib.PROF_SPMV_RES] / max(cnt[_lib.PROF_SPMV_RES], 1)
     gemv_ms = ms[_lib.PROF_GEMV] / max(cnt[_lib.PROF_GEMV], 1)
-    # the committed PMC summaries were measured on the C3 matrix: reported for that workload only
-    c3 = args.config == "c3" and args.M in (None, 289)
     fused = cnt[_lib.PROF_SPMV_DUAL] > 0
-    # the PMC summaries were measured on the default kernels (pipelined, XCD-local walk)
     pipe = args.spmv_pipe
     if pipe == "auto":  # as the library decides (SPIS_OPT_SPMV_PIPE 5): the XCD-local walk, on the
         # slab-ordered table when the upload found one (the swe configs), else while val/col fit
         # the 256 MB Infinity Cache
         pipe = "xcd" if args.config in ("c3", "c5") or 12 * A.nnz <= 256 * 1024 * 1024 else "stride"
-    traffic = load_traffic("spmv_dual_traffic.json") if c3 and fused and pipe == "xcd" and not c16 else None
-    if args.config in ("c2", "c4") and args.M is None and pipe == "xcd" and not c16 and args.spmv_nt == 0:
-        # profiles/r03_{c2,c4}_spmv_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the same launches
-        # standalone, back to back (tools/r03_pmc_c2c4.sh over tools/spmv_pmc.py)
-        tt = load_traffic(f"r03_{args.config}_spmv_traffic.json")
-        want = "spmv_pipe_kernel<2048, 4, false, 1, false>" if fused else "spmv_pipe_kernel<2048, 1, false, 1, false>"
-        rows = [r for r in (tt or {}).get("kernels", []) if want in r["kernel"]]
-        traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
-    c5 = args.config == "c5" and args.M in (None, 913)
-    if c5 and pipe == "xcd" and c16 and args.spmv_nt == 0:
-        # profiles/r03_c5_spmv_traffic[_key1].json: FETCH_SIZE / WRITE_SIZE passes of the same
-        # launches (tools/r03_pmc_c5.sh, tools/r03_slabkey.sh over tools/spmv_pmc.py, corrected by
-        # tools/pmc_kernels.py), on the table in slab order with / without the slab key
-        t5 = load_traffic("r03_c5_spmv_traffic_key1.json" if args.slab_key else "r03_c5_spmv_traffic.json")
-        tmpl = "true, true>" if args.spmv_w4 else "1, true>"
-        want = (f"spmv_pipe_kernel<2048, 4, false, {'4, ' if args.spmv_w4 else ''}{tmpl}" if fused else
-                f"spmv_pipe_kernel<2048, 1, false, {'4, ' if args.spmv_w4 else ''}{tmpl}")
-        rows = [r for r in (t5 or {}).get("kernels", []) if want in r["kernel"]]
-        traffic = {"bytes_per_launch": rows[0]["total_MB"] * 1e6} if rows else None
     kname = {"off": "spmv_dual_kernel", "stride": "spmv_pipe_kernel<2048, 4> (grid-stride walk)",
-             "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)", "stride2": "spmv_pipe2_kernel<2048, 4>",
-             "xcd2": "spmv_pipe2_kernel<2048, 4> (XCD-local walk)",
-             "sell": "spmv_sell_kernel<4> (SELL-64 copy, XCD-local walk)",
+             "xcd": "spmv_pipe_kernel<2048, 4> (XCD-local walk, slab order)",
              "xcd_natural": "spmv_pipe_kernel<2048, 4> (XCD-local walk, natural block order)"}[pipe]
-    if c16 and pipe in ("stride", "xcd", "xcd_natural"):
-        kname = kname.replace(", 4>", ", 4, C16>").replace(")", ", 16-bit columns)")
-    if fused:  # the dominant SpMV launch: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
-        roof = {"kernel": kname + ": true-residual SpMV of x_j, solvers.py:290, fused with the "
-                          "Arnoldi SpMV of z_{j+2}, :191; matrix read once",
-                "bound": "hbm", "achieved": dual_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": dual_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": SD,
-                "avg_launch_us": 1e3 * dual_ms, "launches": int(cnt[_lib.PROF_SPMV_DUAL])}
+    if c16 and pipe != "off":
+        kname = kname.replace(", 4>", ", 4, true>").replace(")", ", 16-bit columns)")
+    # PMC traffic (profiles/r04_traffic_<config>.json, tools/r04_pmc.sh): used only when it was
+    # measured on this kernels.hip and these SpMV / chain options (load_traffic checks both)
+    tr, tr_note = load_traffic(args, c16, pipe)
+    if fused:  # the SpMV of the north star: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
+        roof_spmv = {"kernel": kname + ": true-residual SpMV of x_j, solvers.py:290, fused with the "
+                                       "Arnoldi SpMV of z_{j+2}, :191; matrix read once",
+                     "bound": "hbm", "achieved": dual_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dual_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": SD,
+                     "avg_launch_us": 1e3 * dual_ms, "launches": int(cnt[_lib.PROF_SPMV_DUAL])}
     else:
-        roof = {"kernel": kname.replace("dual", "rowblock").replace(", 4>", ", 1>") + ": Arnoldi SpMV, solvers.py:191",
-                "bound": "hbm", "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": spmv_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": S,
-                "avg_launch_us": 1e3 * spmv_ms, "launches": int(cnt[_lib.PROF_SPMV])}
-    roof["traffic"] = None if traffic is None else traffic.get("bytes_per_launch")
+        roof_spmv = {"kernel": kname.replace(", 4", ", 1") + ": Arnoldi SpMV, solvers.py:191",
+                     "bound": "hbm", "achieved": spmv_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": spmv_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": S,
+                     "avg_launch_us": 1e3 * spmv_ms, "launches": int(cnt[_lib.PROF_SPMV])}
+    roof_spmv["traffic"] = tr.get("dual_solver" if fused else "arnoldi_solver")
+    roof_spmv["traffic_cold"] = tr.get("dual_cold" if fused else "arnoldi_cold")
+    # the MGS chain (+ normalise, + the update GEMV it carries): its launches' mean algorithmic bytes
+    # over the sampled chain positions / their mean duration (mgs_chain_bytes)
+    chain_name = {3: "mgs_chain_lag_kernel<8, PER, 5, 2, FX, NT> (K2q: MGS, dots two steps early)",
+                  4: "icwy_dot + cgs_update + normalise (K2w: one-reduce two-pass MGS)"}.get(args.chain, "MGS chain")
+    if args.chain == 3 and (n + 1) // 2 > 255 * 512 * 4:
+        chain_name = "icwy_dot + cgs_update + normalise (K2w: one-reduce two-pass MGS, beyond K2q's capacity)"
+    roof_mgs = {"kernel": chain_name + ": solvers.py:193-198 (+ the update GEMV of :287)", "bound": "hbm",
+                "achieved": mgs_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": None if mgs_gbs is None else mgs_gbs / HBM_PEAK_GBS,
+                "algorithmic_bytes_per_launch": mgs_b, "avg_launch_us": 1e3 * mgs_ms,
+                "launches": int(cnt[_lib.PROF_MGS]), "traffic": tr.get("mgs_solver")}
+    # the dominant kernel by GPU time per solve (the contract's roofline object); the other beside it
+    t_mgs = mgs_ms * k_per_solve(args.k)
+    t_spmv = (dual_ms if fused else spmv_ms) * max(args.k - 2, 1)
+    mgs_dominant = roof_mgs["frac"] is not None and t_mgs >= t_spmv
+    roof = dict(roof_mgs if mgs_dominant else roof_spmv)
+    roof["share_of_solve_kernel_time"] = "dominant by time per solve: MGS chain %.0f us vs SpMV %.0f us" % (
+        1e3 * t_mgs, 1e3 * t_spmv)
+    roof["traffic_note"] = tr_note
     # the same launch standalone (spis_spmv_bench: the solver's table, walk and grid), back to back
     # and behind a 1 GiB cache-evicting read, so the fraction is also quoted with the matrix and
     # the vectors coming from HBM, not from the 256 MB Infinity Cache
@@ -376,10 +367,10 @@ def main():
             _lib.check(L.spis_spmv_bench(ctx.handle, device_matrix(A, ctx=ctx).handle, kind, cold, 20, C.byref(v)),
                        "spis_spmv_bench")
             us[cold] = v.value
-        roof["standalone_warm_us"] = us[0]
-        roof["avg_launch_us_cold"] = us[1]
-        roof["achieved_cold"] = bytes_l / (us[1] * 1e-6) / 1e9
-        roof["frac_cold"] = roof["achieved_cold"] / HBM_PEAK_GBS
+        roof_spmv["standalone_warm_us"] = us[0]
+        roof_spmv["avg_launch_us_cold"] = us[1]
+        roof_spmv["achieved_cold"] = bytes_l / (us[1] * 1e-6) / 1e9
+        roof_spmv["frac_cold"] = roof_spmv["achieved_cold"] / HBM_PEAK_GBS
     out = {
         "metric": METRIC,
         "value": iters / elapsed,
@@ -403,6 +394,7 @@ def main():
             "parallelism": "single GPU",
         },
         "roofline": roof,
+        "roofline_spmv": roof_spmv,
         "kernels": {
             "spmv_arnoldi_us": 1e3 * spmv_ms,
             "spmv_arnoldi_GBs": spmv_gbs,

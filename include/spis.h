@@ -94,14 +94,19 @@ int spis_context_synchronize(spis_context* ctx);
 /* HIP stream (hipStream_t) the context orders its work on */
 int spis_context_stream(spis_context* ctx, void** stream_out);
 
+/* Content digest of a host array (no device needed): the drop-in's upload cache (device.py)
+ * re-verifies a cached SciPy matrix's data / indices / indptr with it on every solver call, on
+ * a second host thread beside spis_solve.  The bytes are hashed in 1 MiB pieces on up to
+ * `threads` threads; the digest does not depend on the thread count. */
+int spis_host_hash(const void* data, int64_t bytes, int32_t threads, uint64_t* out);
+
 /* ---- live kernel timing ------------------------------------------------------
  * spis_profile_enable(ctx, period): period > 0 makes spis_solve record HIP
  * events on the context stream around the Arnoldi SpMV, the MGS chain
  * (+ normalise), the GEMV and the true-residual SpMV of every period-th
  * iteration (an event pair costs a few us of queue time, so bench.py samples);
- * totals (ms) and launch counts accumulate until the next call.  period = 0
- * disables; a negative value (tests) additionally routes the constraint
- * reduction through the generic Gram path instead of the fused kernel. */
+ * totals (ms) and launch counts accumulate until the next call.  period <= 0
+ * disables. */
 enum spis_prof_kind {
   SPIS_PROF_SPMV = 0,       /* Arnoldi SpMV, solvers.py:191 (standalone launches)          */
   SPIS_PROF_MGS = 1,        /* MGS chain + normalise, :193-198                             */
@@ -123,114 +128,72 @@ int spis_spmv_bench(spis_context* ctx, spis_matrix* A, int32_t kind, int32_t col
  * SPIS_OPT_FUSE_SPMV (default 1): the true-residual SpMV of update j and the Arnoldi SpMV of
  *   step j+2 (adjacent in the pipelined stream) run as one launch reading the matrix once;
  *   results are bit-identical either way.
- * SPIS_OPT_GENERIC_GRAM (default 0): route the constraint reduction through the generic
- *   SpMM + tiled Gram path instead of the fused kernel (tests).
- * SPIS_OPT_GRAPHS (default 0): replay each Arnoldi step's launches (fused SpMV, MGS chain,
- *   normalise) from a captured hipGraph (single GPU, no host preconditioner callback).  Cuts host
- *   enqueue time ~9x, but each replay adds ~5 us of GPU time at its boundary: C3 is 2% slower.
  * SPIS_OPT_ORTHOG (default 0): 0 = modified Gram-Schmidt (the reference's, solvers.py:193-195);
  *   1 = CGS2, classical Gram-Schmidt with one re-orthogonalisation pass (3 reductions per
  *   Arnoldi step instead of j + 2; the low-synchronisation option of SURVEY §8e; steps with
  *   more than 32 basis vectors fall back to MGS).  Not MGS's arithmetic: opt-in only.
- * SPIS_OPT_ELL_GRAM (default 3): how the fused constraint reduction (p + 1 <= 32) reads each
- *   constraint matrix, from a copy built once on first use: 3 = on the f64 matrix cores, a
- *   symmetric matrix from a slot table of its upper triangle (K7t: G = H + H^T, half the
- *   gathers), any other from its CSR (K7m); 4 = K7m for every matrix; 1 = sliced ELL (static row
- *   boundaries), 2 = row chunks with their distinct columns (the basis rows of those columns
- *   staged in LDS once per chunk; a matrix with a row of > 64 entries or > 176 distinct columns
- *   falls back to 1; measured 12% slower than 1 at C3), 0 = the CSR itself.  C3 (swe energy
- *   matrix, p = 30): K7t 122 us, K7m 232 us, ELL 326 us, staged 371 us.
+ * SPIS_OPT_CON_GRAM (default 2): how the constraint terms (solvers.py:33-36) are reduced.  2 = the
+ *   fused reduction on the f64 matrix cores (p + 1 <= 32): a symmetric constraint matrix from a
+ *   slot table of its upper triangle (K7t: G = H + H^T, half the gathers), any other from its CSR
+ *   (K7m); 3 = K7m for every matrix; 1 = the fused reduction on the CSR without matrix cores (K7,
+ *   also the kernel for 32 < p + 1 <= 64); 0 = the generic path (one SpMM M Z, then a tiled Gram).
+ *   C3 (swe energy matrix, p = 30): K7t 122 us, K7m 232 us.
  * SPIS_OPT_MGS_CHAIN (default 3): each Arnoldi step's MGS chain + normalise runs as one persistent
  *   launch exchanging partial dots between workgroups in-launch (single GPU, N <= 2^20); 2 = the
- *   partials are gathered by a dedicated workgroup that holds no slice (N <= 2^20 - 4096), 1 = by
- *   workgroup 0; 0 = one launch per MGS step.  MGS's arithmetic either way; the partial sums are grouped differently,
- *   so results differ from the per-step launches at roundoff level.  3 = the pipelined chain:
- *   MGS's projections and updates, each dot product evaluated one step early by the distributive
- *   law (h_{i+1} = q_{i+1}.w^{(i)} - h_i q_{i+1}.q_i), so two exchanges overlap; roundoff differs
- *   from MGS's (N <= 2^20 - 4096; beyond, mode 4).  4 = the one-reduce two-pass MGS (the
- *   several-GPU K2w: every q_l.w and the newest Gram row in one pass, the projections by the
- *   distributive law, then the update pass, which also forms the previous iteration's update
- *   GEMV); MGS in exact arithmetic, not its rounding; k <= 32.  Mode 3 takes it beyond K2q's
- *   capacity, where it replaces K2b + a separate GEMV pass (C5: 826 -> 921 it/s).
- * SPIS_OPT_OVERLAP_GEMV (default 1): the solution-update GEMV of iteration j runs on a second
- *   stream, concurrently with the MGS chain of Arnoldi step j+1 (single GPU); results identical.
- *   The dual SpMV waits for it through a stream write / wait on a device word (1) or through the
- *   GEMV launch's own completion event (2; measured equal end to end); 0 = main stream.
+ *   partials are gathered by a dedicated workgroup that holds no slice (beyond 2^20, K2b: only w
+ *   in registers, N <= 10.4 M), 1 = by workgroup 0; 0 = one launch per MGS step.  MGS's
+ *   arithmetic either way; the partial sums are grouped differently, so results differ from the
+ *   per-step launches at roundoff level.  3 = the pipelined chain (K2q): MGS's projections and
+ *   updates, each dot product evaluated two steps early by the distributive law (h_m = q_m.w^(m-2)
+ *   - h_{m-2} q_m.q_{m-2} - h_{m-1} q_m.q_{m-1}), so three exchanges overlap; roundoff differs
+ *   from MGS's.  Beyond K2q's capacity (N > 2^20 - 4096) mode 3 takes mode 4: the one-reduce
+ *   two-pass MGS (K2w, the several-GPU kernels: every q_l.w and the newest Gram row in one pass,
+ *   the projections by the distributive law, then the update pass, which also forms the previous
+ *   iteration's update GEMV); MGS in exact arithmetic, not its rounding; k <= 32.
  * SPIS_OPT_SPMV_PIPE (default 5): the solver's SpMVs (and spis_spmv / spis_residual_norm) run the
- *   software-pipelined row-block kernels; 2 = each XCD's workgroups walk a contiguous eighth of
- *   the row blocks (its share of the gathered vectors stays in its own L2) in slab order when the
- *   upload found one (square matrices whose DoF groups are numbered one after another: the blocks
- *   sorted by the label their rows' columns carry, spis.cpp build_slab_order), 7 = 2 on the
- *   blocks' natural order, 1 = grid-stride walk,
- *   0 = the unpipelined kernels; 3 / 4 = as 1 / 2 with the next block's gathers also in flight;
- *   5 = 2 when the table has a slab order or the matrix's val/col fit the 256 MB Infinity Cache,
- *   else 1.  Rows are bit-identical in every mode; the reduction partials
- *   are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.
- * SPIS_OPT_EARLY_CON (default 0): the constraint reduction of CGMRES's forced final constrained
- *   step (j = k-1) is launched on a third stream once A_{k-1} (2; measured equal to 0 at C3) or
- *   A_{k-2} (1: the earliest, A_{k-2} writes the last basis vector it needs; measured 5% slower,
- *   it delays A_{k-1}'s persistent chain) is queued; 0 = when the step is reached.  Results
- *   identical.
- * SPIS_OPT_NT_BASIS (default 2): the persistent MGS chain loads basis vectors with nontemporal
- *   loads, so re-streaming the basis every Arnoldi step does not evict the matrix from the
- *   256 MB Infinity Cache before the next SpMV; 2 = when the matrix and the k+1 basis vectors
- *   exceed 256 MB, 1 = always, 0 = never.  Results identical.
- * SPIS_OPT_COL16 (default 1): the pipelined SpMV (K1p / K1dp, one-deep) reads the matrix's
- *   columns from a 16-bit copy made at upload when every row block spans <= 4 ranges of 2^14
- *   columns (csrc/col16.h: a 2-bit base index + 14-bit offset per nonzero, 4 base columns per
- *   block): 10 instead of 12 bytes per nonzero.  1 = when val/col exceed the 256 MB Infinity
- *   Cache (C5: dual 470 vs 494 us; a cache-resident C3 matrix is faster on 32-bit columns,
- *   37.6 vs 39.5 us), 2 = always, 0 = never.  Rows bit-identical.
+ *   software-pipelined row-block kernels (K1p / K1dp); 2 = each XCD's workgroups walk a contiguous
+ *   eighth of the row blocks (its share of the gathered vectors stays in its own L2), in slab
+ *   order when the upload found one (square matrices whose DoF groups are numbered one after
+ *   another: slab_order.h), 7 = 2 on the blocks' natural order, 1 = grid-stride walk, 0 = the
+ *   unpipelined kernels (K1 / K1d); 5 = 2 when the table has a slab order or the matrix's val/col
+ *   fit the 256 MB Infinity Cache, else 1.  Rows are bit-identical in every mode; the reduction
+ *   partials are grouped per workgroup, so scalars (h, residuals) differ between modes at roundoff.
+ * SPIS_OPT_NT_BASIS (default 2): the MGS kernels load basis vectors with nontemporal loads, so
+ *   re-streaming the basis every Arnoldi step does not evict the matrix from the 256 MB Infinity
+ *   Cache before the next SpMV; 2 = when the matrix and the k+1 basis vectors exceed 256 MB,
+ *   1 = always, 0 = never.  Results identical.
+ * SPIS_OPT_COL16 (default 1): the pipelined SpMV reads the matrix's columns from a 16-bit copy made
+ *   at upload when every row block spans <= 4 ranges of 2^14 columns (csrc/col16.h: a 2-bit base
+ *   index + 14-bit offset per nonzero, 4 base columns per block): 10 instead of 12 bytes per
+ *   nonzero.  1 = when val/col exceed the 256 MB Infinity Cache (C5: dual 470 vs 494 us; a
+ *   cache-resident C3 matrix is faster on 32-bit columns, 37.6 vs 39.5 us), 2 = always, 0 = never.
+ *   Rows bit-identical.
  * SPIS_OPT_DIST_MGS (default 1): several GPUs (after spis_comm_init), Arnoldi steps with at most
  *   32 basis vectors: MGS's projections in inverse-compact-WY form, h_l = q_l.w - sum_{m<l} h_m
  *   q_l.q_m, from one pass and one all-reduce (every q_l.w and the newest Gram row), then the
  *   update with ||w'||^2 and a second all-reduce: 2 all-reduces per Arnoldi step instead of
  *   MGS's j + 2.  MGS in exact arithmetic (the pipelined single-GPU chain's correction terms with
  *   an unbounded lag); roundoff differs.  0 = one MGS step launch and all-reduce per projection.
- * SPIS_OPT_SPMV_NT (default 0): the pipelined SpMV (one-deep) reads the matrix stream (values and
- *   columns) with nontemporal loads, so streaming a matrix larger than the 256 MB Infinity Cache
- *   does not evict the gathered vectors; 1 = always, 2 = when val/col exceed 256 MB, 0 = never.
- *   Results identical.  Measured at C5 (1.5 GB matrix, standalone, cold): Arnoldi SpMV 404 -> 397
- *   us, dual 497 -> 627 us; off by default.
- * SPIS_OPT_K7T_SLOTS (default 16): slots per block of K7t's slot table, 16 or 32 (32: twice the
- *   gathers in flight per lane at 2 waves per SIMD; measured slower at C3, kept for the test that
- *   walks many 32-slot blocks per wave).  Results equal up to the grouping of the Gram sums.
- * SPIS_OPT_LAG_MODE (default 1): the L-mode schedule (each Arnoldi step's MGS enqueued once the
- *   host holds the previous H column, carrying the previous update GEMV) where the MGS kernel
- *   supports it; 0 = the plain pipelined order (the GEMV as its own launch).  Same arithmetic.
- * SPIS_OPT_SLAB_KEY (default 1): read at spis_matrix_create.  1 = within a slab the row blocks
+ * SPIS_OPT_SLAB_KEY (default 1): read at spis_csr_upload.  1 = within a slab the row blocks
  *   follow their rows' mean position in the slab's dominant DoF group (slab_order.h), so the
  *   slab's DoF groups are walked side by side and each XCD gathers an x line about once; 0 = the
  *   groups one after another inside a slab (round 2's order).  Rows bit-identical; reduction
  *   partials grouped differently (roundoff).
- * SPIS_OPT_SPMV_W4 (default 0): the pipelined SpMV (one-deep, not nontemporal) in its 4-waves-per-
- *   SIMD form: matrix stream and gathers through buffer descriptors, the next block's values
- *   loaded once the current products are in LDS, partial sums in LDS (<= 128 VGPRs, 4 workgroups
- *   per CU instead of 3); 2 = the buffer-descriptor form at 3 waves per SIMD.  Rows
- *   bit-identical; partials grouped per workgroup (roundoff).
- * SPIS_OPT_C16_TM (default 0): read at spis_matrix_create.  1 = the 16-bit column copy is also
- *   kept thread-major per slab-order block (each thread's 8 columns contiguous: one 16-B load
- *   instead of 8 two-byte loads per block); used by the slab-ordered pipelined SpMV on 16-bit
- *   columns.  Same columns, same arithmetic: bit-identical. */
+ * Variants measured slower and removed from the library (round 4): hipGraph replay of the Arnoldi
+ *   step, the early constraint reduction on a third stream, the nontemporal / 4-waves-per-SIMD /
+ *   buffer-descriptor / thread-major-column / two-deep / SELL-64 SpMV kernels (now
+ *   tools/spmv_variants.hip), 32-slot K7t blocks, the sliced-ELL and chunk-staged K7 Gram kernels;
+ *   DESIGN.md §3 keeps their measurements. */
 enum spis_option {
   SPIS_OPT_FUSE_SPMV = 1,
-  SPIS_OPT_GENERIC_GRAM = 2,
-  SPIS_OPT_GRAPHS = 3,
   SPIS_OPT_ORTHOG = 4,
-  SPIS_OPT_ELL_GRAM = 5,
+  SPIS_OPT_CON_GRAM = 5,
   SPIS_OPT_MGS_CHAIN = 6,
-  SPIS_OPT_OVERLAP_GEMV = 7,
   SPIS_OPT_SPMV_PIPE = 8,
-  SPIS_OPT_EARLY_CON = 9,
   SPIS_OPT_NT_BASIS = 10,
   SPIS_OPT_COL16 = 11,
   SPIS_OPT_DIST_MGS = 12,
-  SPIS_OPT_SPMV_NT = 13,
-  SPIS_OPT_K7T_SLOTS = 14,
-  SPIS_OPT_LAG_MODE = 15,
-  SPIS_OPT_SLAB_KEY = 16,
-  SPIS_OPT_SPMV_W4 = 17,
-  SPIS_OPT_C16_TM = 18
+  SPIS_OPT_SLAB_KEY = 16
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -22,18 +22,16 @@ BRANCH_UNCON, BRANCH_CON, BRANCH_FALLBACK = 0, 1, 2
 EV_BREAKDOWN, EV_LS_MESSAGE, EV_NAN, EV_VIOLATION, EV_FALLBACK = 1, 2, 4, 8, 16
 PROF_SPMV, PROF_MGS, PROF_GEMV, PROF_SPMV_RES, PROF_SPMV_DUAL = range(5)
 PROF_KINDS = 5
-OPT_FUSE_SPMV, OPT_GENERIC_GRAM, OPT_GRAPHS, OPT_ORTHOG, OPT_ELL_GRAM, OPT_MGS_CHAIN, OPT_OVERLAP_GEMV = 1, 2, 3, 4, 5, 6, 7
+# spis_option (include/spis.h)
+OPT_FUSE_SPMV = 1
+OPT_ORTHOG = 4
+OPT_CON_GRAM = 5
+OPT_MGS_CHAIN = 6
 OPT_SPMV_PIPE = 8
-OPT_EARLY_CON = 9
 OPT_NT_BASIS = 10
 OPT_COL16 = 11
 OPT_DIST_MGS = 12
-OPT_SPMV_NT = 13
-OPT_K7T_SLOTS = 14
-OPT_LAG_MODE = 15
 OPT_SLAB_KEY = 16
-OPT_SPMV_W4 = 17
-OPT_C16_TM = 18
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",
@@ -120,6 +118,7 @@ SIGNATURES = [
     ("spis_context_destroy", C.c_int, [_VP]),
     ("spis_context_synchronize", C.c_int, [_VP]),
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
+    ("spis_host_hash", C.c_int, [_VP, _I64, _I32, C.POINTER(C.c_uint64)]),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),
     ("spis_spmv_bench", C.c_int, [_VP, _VP, _I32, _I32, _I32, _PD]),

@@ -50,25 +50,4 @@ inline bool build_col16(const int32_t* rp, const int32_t* ci, const std::vector<
   return true;
 }
 
-// The same 16-bit columns thread-major per block, for the pipelined SpMV: table block k (nonzeros
-// [e0, e1), in the table's order) occupies cap entries at k * cap, and thread t's per = cap / threads
-// entries (its nonzeros e0 + t + u * threads, u < per) are contiguous, so a thread loads its
-// columns with one 16-B load instead of per 2-B loads.  Padding entries are 0 (they decode to the
-// block's first base column, as the kernels' predicated loads do).
-inline void build_col16_tm(const std::vector<uint16_t>& col16, const std::vector<int32_t>& nz_ranges, int cap,
-                           int threads, std::vector<uint16_t>& out) {
-  const int64_t nb = static_cast<int64_t>(nz_ranges.size()) / 2;
-  const int per = cap / threads;
-  out.assign(static_cast<size_t>(std::max<int64_t>(nb, 1) * cap), 0);
-  for (int64_t k = 0; k < nb; ++k) {
-    const int64_t e0 = nz_ranges[2 * k], len = nz_ranges[2 * k + 1] - nz_ranges[2 * k];
-    uint16_t* o = out.data() + k * cap;
-    for (int t = 0; t < threads; ++t)
-      for (int u = 0; u < per; ++u) {
-        const int64_t i = t + static_cast<int64_t>(u) * threads;
-        if (i < len) o[t * per + u] = col16[e0 + i];
-      }
-  }
-}
-
 }  // namespace spis

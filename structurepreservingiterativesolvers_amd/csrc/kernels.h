@@ -57,28 +57,7 @@ struct CsrView {
   // C16 (col16.h): 16-bit columns + per-block base columns, in the table's block order
   const uint16_t* col16 = nullptr;
   const int4* blk_base = nullptr;
-  int depth = 1;  // 1: next block's loads in flight; 2: also its gathers (spmv_pipe2_kernel)
-  bool nt = false;  // K1p / K1dp: the matrix stream (val, col) read with nontemporal loads
-  // K1p / K1dp at 4 waves per SIMD (4 workgroups per CU instead of 3): buffer-descriptor matrix
-  // stream and gathers, the next block's values loaded after the current products are in LDS
-  // (SPIS_OPT_SPMV_W4; one-deep, not nontemporal)
-  bool w4 = false;
-  bool buf = false;  // the buffer-descriptor form at the default 3 waves per SIMD (SPIS_OPT_SPMV_W4 = 2)
-  // C16 columns thread-major per block (col16.h build_col16_tm; col16 then points at that copy, in
-  // the table's block order): one 16-B column load per thread and block (SPIS_OPT_C16_TM)
-  bool c16tm = false;
-  // K1s (SELL-64 copy, spmv_sell_kernel): when sl_col is set, the launch_spmv* entry points run
-  // it instead.  Slice s = rows [64 s, 64 s + 64); entry t of its lane l (row 64 s + l) at
-  // sl_off[s] + 64 t + l; rows padded to the slice's longest (col = the row, val = 0, skipped
-  // by the row length sl_len)
-  const int32_t* sl_col = nullptr;
-  const double* sl_val = nullptr;
-  const int64_t* sl_off = nullptr;
-  const uint16_t* sl_len = nullptr;
-  int32_t n_sl = 0;
 };
-constexpr int kSellW = 64;       // rows per slice (a wave, lane = row)
-constexpr int kSellMaxLen = 64;  // longest row of a SELL copy (longer: no copy, K1p serves)
 
 // grid sizes (a fixed count when partials are all-reduced across ranks)
 int spmv_grid(const CsrView& A, bool fixed);
@@ -97,14 +76,22 @@ hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, co
 // K1d: residual SpMV of x1 (||A x1 - b||^2 partials -> part1) and Arnoldi SpMV of x2 (w = A x2,
 // q0.w partials -> part2) reading the matrix once; both bit-identical to launch_spmv's.  A must
 // carry the kDualCap row-block table; grid <= kSpmvGrid (the partial arrays' length)
+// the dual's optional extra epilogue dots: q1 . w and q2 . w partials (grid of each) for the MGS
+// chain that follows, which then starts with its first two exchanges done (K2q, chain j >= 3)
+struct DualDots {
+  const double* q1;
+  const double* q2;
+  double* part3;
+  double* part4;
+};
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
-                            hipStream_t s, const LaunchEv* ev = nullptr);
+                            hipStream_t s, const LaunchEv* ev = nullptr, const DualDots* dd = nullptr);
 // K1p / K1dp (A.blk_meta on a kPipeCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
 // part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi)
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev = nullptr);
+                            int grid, hipStream_t s, const LaunchEv* ev = nullptr, const DualDots* dd = nullptr);
 // y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,
@@ -132,7 +119,10 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator = false,
                             bool nt = false, double* gsub = nullptr, const double* yx_host = nullptr, int px = 0,
-                            const double* x0 = nullptr, double* xo = nullptr);
+                            const double* x0 = nullptr, double* xo = nullptr, const double* xd1 = nullptr,
+                            const double* xd2 = nullptr);
+// (xd1, xd2: K2q only, j >= 3 — the partials, n_in of each, of q_1 . w and q_2 . w from the dual
+// SpMV that produced w (DualDots); the chain then starts with h_1 and h_2 formed by its gatherer)
 // (nt: the chain's basis loads are nontemporal — the matrix stays Infinity-Cache resident)
 // gsub != nullptr selects K2q, the pipelined chain (dot products one MGS step early by the
 // distributive law; gsub[m] = q_m . q_{m-1}, written by chain m, read by the later chains of the
@@ -167,7 +157,7 @@ hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t 
 // kCgsMax), h_l = q_l . w - sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
 hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
-                               hipStream_t s);
+                               hipStream_t s, int zero_to = 0);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,
@@ -183,51 +173,18 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 // G = [U^T M U | U^T v_0 .. U^T v_{nvv-1}] from Ut (M may be null: linear terms only);
 // partials: constraint_gram_partials() x (np1*np1 + nvv*np1) doubles
 int constraint_gram_partials();
-// Sliced ELL of a constraint matrix for K7: 16-row slices, slice c holds W_c = (off[c+1] -
-// off[c]) / 16 columns of entries, entry (row 16c + r, t) at off[c] + 16 t + r (zero padding).
-struct EllView {
-  const int32_t* col;
-  const double* val;
-  const int64_t* off;
-};
-constexpr int kEllRows = 16;
-
-// K7s: row chunks of a constraint matrix with the sorted distinct columns they touch (the chunk's
-// own rows included): the Ut rows of those columns are staged in LDS once per chunk, so each
-// nonzero reads its Ut row from LDS instead of gathering it from L2.  A chunk holds <= kStgRows
-// rows as 16-row slices in ELL order (entry (slice s, t, row i) at slice base + 16 t + i, padded
-// with zeros), <= kStgNz entries and <= kStgUmax distinct columns.
-constexpr int kStgRows = 64;
-constexpr int kStgNz = 1024;
-constexpr int kStgUmax = 176;
-struct StgView {
-  const int32_t* row;      // [nch + 1] first row of each chunk
-  const int32_t* uoff;     // [nch + 1] offsets into uniq
-  const int32_t* uniq;     // distinct columns per chunk, ascending
-  const int32_t* eoff;     // [nch + 1] offsets into loc / val
-  const int32_t* width;    // [4 nch] entries per row of each of the chunk's (up to 4) slices
-  const uint16_t* loc;     // per entry: its column's index in the chunk's uniq list
-  const double* val;       // per entry: the value (0 in padding)
-  const uint16_t* rowloc;  // per row: the row's own index in its chunk's uniq list
-  int32_t nch;
-};
-// K7s launch (np1 <= 32): M's StgView; Ut as for K7
-hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, const double* Ut,
-                                      int nvv, const double* const* v, double* partials, double* G,
-                                      hipStream_t s);
-
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
-                                  const double* const* v, double* partials, double* G, hipStream_t s,
-                                  const EllView* ell = nullptr);
+                                  const double* const* v, double* partials, double* G, hipStream_t s);
 // K7m: the same reduction on the f64 matrix cores from M's CSR (np1 <= 32, Ut in perm order).
 // split: the row bounds of the 8 XCD groups (balanced by nonzeros + rows; gram_split)
 struct GramSplit {
   int32_t row[9];
 };
 void gram_split(int64_t n, const int32_t* indptr, GramSplit* out);
-// K7t (symmetric M): slot table of 4-row-group segments packed into blocks of ns = 16 slots:
+// K7t (symmetric M): slot table of 4-row-group segments packed into blocks of ns = kSymSlots slots:
 // block b's entries (row-in-group g, slot t) at b * 4 ns + g ns + t, mask[b] = segment-start
 // bits | (slots used << 32); G (np1 x np1) = H + H^T
+constexpr int kSymSlots = 16;  // (32 measured slower: 166 vs 124 us at C3, profiles/r03_k7t_slots_kernel_stats.csv)
 struct SymTabView {
   const int32_t* col;
   const double* val;

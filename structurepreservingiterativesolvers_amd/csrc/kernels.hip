@@ -101,20 +101,6 @@ __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int 
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
 }
 
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-// one fp64 through a buffer descriptor at a 32-bit byte offset (K1s gathers: no 64-bit address
-// registers per entry)
-__device__ __forceinline__ double buf_ld1(__amdgpu_buffer_rsrc_t r, int voff) {
-  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
-  return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x));
-}
-
-// the same with the element's distance in the scalar offset (K1p's matrix stream: one lane offset
-// for all of a block's loads, the block's start in the descriptor's base)
-__device__ __forceinline__ double buf_ld1s(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-  return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x));
-}
 // a descriptor over [p, p + 2^31 B) with a wave-uniform base (callers index it with valid offsets)
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const T* p) {
@@ -320,6 +306,15 @@ struct PipeStage {
                           // stay in registers)
 };
 
+// MODE 5 (the dual SpMV for an MGS chain that takes its first two dots from it): w's dots with q1
+// and q2, per workgroup in the same order as q0's (part2)
+struct PipeXD {
+  const double* q1 = nullptr;
+  const double* q2 = nullptr;
+  double* part3 = nullptr;
+  double* part4 = nullptr;
+};
+
 // C16: column = base[k] + offset of a 16-bit entry (k = the top 2 bits)
 __device__ __forceinline__ int col16_decode(unsigned v, int b0, int b1, int b2, int b3) {
   const unsigned k = v >> 14;
@@ -329,18 +324,7 @@ __device__ __forceinline__ int col16_decode(unsigned v, int b0, int b1, int b2, 
 
 // block lb of the table (entries lb * ms, lb * ms + 1: ms = 1 consecutive starts, 2 (start, end)
 // pairs); C16: the columns from the 16-bit copy and the block's bases base[lb]
-// BUF stage: the values only (LATEV: issued once the current block's products are in LDS, so the
-// next block's values are not live in registers across the current block's gathers)
-template <int CAP>
-__device__ __forceinline__ void pipe_load_vals(PipeStage<CAP>& st, const double* __restrict__ va) {
-  if (st.nnz > CAP) return;
-  const __amdgpu_buffer_rsrc_t rv = span_rsrc(va + st.nz0);
-#pragma unroll
-  for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
-    st.vals[u] = threadIdx.x + u * kBlock < st.nnz ? buf_ld1s(rv, threadIdx.x * 8, u * kBlock * 8) : 0.0;
-}
-
-template <int CAP, int MODE, bool NT = false, bool C16 = false, bool BUF = false, bool VALS = true, bool TM = false>
+template <int CAP, int MODE, bool C16 = false>
 __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __restrict__ meta, int lb, int ms,
                                           const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                           const uint16_t* __restrict__ c16, const int4* __restrict__ base,
@@ -360,70 +344,24 @@ __device__ __forceinline__ void pipe_load(PipeStage<CAP>& st, const int2* __rest
   st.nz0 = m0.y;
   st.nnz = m1.y - m0.y;
   if (st.nnz > CAP) return;  // long row: read directly by the workgroup-wide path
-  if constexpr (TM && C16 && !NT && !BUF) {
-    // thread-major copy: this thread's kPer 16-bit columns in one 16-B load (no long rows here:
-    // the host builds the copy only for matrices without them)
-    static_assert(PipeStage<CAP>::kPer == 8, "one 16-B load = 8 columns");
-    const uint4 v = *reinterpret_cast<const uint4*>(c16 + static_cast<int64_t>(lb) * CAP + threadIdx.x * 8);
-    st.cols[0] = static_cast<int>(v.x & 0xffffu);
-    st.cols[1] = static_cast<int>(v.x >> 16);
-    st.cols[2] = static_cast<int>(v.y & 0xffffu);
-    st.cols[3] = static_cast<int>(v.y >> 16);
-    st.cols[4] = static_cast<int>(v.z & 0xffffu);
-    st.cols[5] = static_cast<int>(v.z >> 16);
-    st.cols[6] = static_cast<int>(v.w & 0xffffu);
-    st.cols[7] = static_cast<int>(v.w >> 16);
-#pragma unroll
-    for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
-      const int i = threadIdx.x + u * kBlock;
-      st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
-    }
-  } else if constexpr (BUF && !NT) {
-    // buffer descriptors based at the block's first nonzero: every load of the block shares the
-    // lane offset, its distance u * kBlock elements rides in the scalar offset (no 64-bit address
-    // registers per element, which is what kept the stage at 3 waves per SIMD)
-    if constexpr (C16) {
-      const __amdgpu_buffer_rsrc_t rc = span_rsrc(c16 + st.nz0);
-#pragma unroll
-      for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
-        st.cols[u] = threadIdx.x + u * kBlock < st.nnz
-                         ? static_cast<int>(__builtin_amdgcn_raw_buffer_load_b16(rc, threadIdx.x * 2, u * kBlock * 2, 0))
-                         : 0;
-    } else {
-      const __amdgpu_buffer_rsrc_t rc = span_rsrc(ci + st.nz0);
-#pragma unroll
-      for (int u = 0; u < PipeStage<CAP>::kPer; ++u)
-        st.cols[u] = threadIdx.x + u * kBlock < st.nnz
-                         ? static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(rc, threadIdx.x * 4, u * kBlock * 4, 0))
-                         : 0;
-    }
-    if constexpr (VALS) pipe_load_vals<CAP>(st, va);
-  } else {
 #pragma unroll
   for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
     const int i = threadIdx.x + u * kBlock;
-    if (C16 && NT) {  // streamed once (beyond the Infinity Cache): keep it for the gathered vectors
-      st.cols[u] = i < st.nnz ? __builtin_nontemporal_load(c16 + st.nz0 + i) : 0;
-      st.vals[u] = i < st.nnz ? __builtin_nontemporal_load(va + st.nz0 + i) : 0.0;
-    } else if (C16) {
+    if (C16) {
       st.cols[u] = i < st.nnz ? c16[st.nz0 + i] : 0;  // raw: decoded at the gathers, so the prefetch
                                                       // stays in flight (0 decodes to a column of the block)
       st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
-    } else if (NT) {  // streamed once: keep L2 for the gathered vectors
-      st.cols[u] = i < st.nnz ? __builtin_nontemporal_load(ci + st.nz0 + i) : 0;
-      st.vals[u] = i < st.nnz ? __builtin_nontemporal_load(va + st.nz0 + i) : 0.0;
     } else {
       st.cols[u] = i < st.nnz ? ci[st.nz0 + i] : 0;
       st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
     }
-  }
   }
   const int r = st.r0 + threadIdx.x;
   if (r < st.r1) {
     st.rs = rp[r] - st.nz0;
     st.re = rp[r + 1] - st.nz0;
     if (MODE != kEpiPlain) st.a1 = aux1[r];
-    if (MODE == 4) st.a2 = aux2[r];
+    if (MODE >= 4) st.a2 = aux2[r];
   } else {
     st.rs = st.re = 0;
   }
@@ -444,35 +382,30 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 }
 
 // x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
-// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half
+// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half (MODE 4); MODE 5 = 4 + q1.w and q2.w
+// partials (xd.part3, xd.part4) for the MGS chain that follows (K2q's E_1, E_2)
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
-// BUF: the matrix stream and the gathers through buffer descriptors (32-bit lane offsets), which
-// frees the registers for WPE = 4 waves per SIMD (4 workgroups per CU instead of 3)
-template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false, bool TM = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE > 3 ? WPE : (C16 ? 3 : 8)))) void spmv_pipe_kernel(
+// (variants measured and not adopted — nontemporal stream, 4 waves per SIMD, buffer descriptors,
+// thread-major columns, two-deep pipeline, SELL-64 — live in tools/spmv_variants.hip)
+template <int CAP, int MODE, bool C16 = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 5 ? 3 : 1, C16 ? 3 : 8))) void spmv_pipe_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
-  constexpr bool DUAL = MODE == 4;
+    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base, PipeXD xd) {
+  constexpr bool DUAL = MODE >= 4;
+  constexpr bool XD = MODE == 5;
   constexpr int kPer = PipeStage<CAP>::kPer;
-  constexpr bool LATEV = BUF && !NT && WPE > 3;  // 4 waves per SIMD: the next values loaded late
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
   // of 16 entries (swe's edge rows) would otherwise put a wave's lanes 256 B apart, all in one
   // LDS bank group; the pad staggers them
   __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
   __shared__ double s_wave[4];
-  // LATEV: each thread's partial sums live in its own LDS slot between blocks (in registers they
-  // were spilled, and a scratch reload waits for every load issued before it: the prefetch)
-  __shared__ double2 s_pt[LATEV ? kBlock : 1];
-  double pt1 = 0.0, pt2 = 0.0;
-  if (LATEV) s_pt[threadIdx.x] = make_double2(0.0, 0.0);
+  double pt1 = 0.0, pt2 = 0.0, pt3 = 0.0, pt4 = 0.0;
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
   const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
-  const __amdgpu_buffer_rsrc_t rx1 = span_rsrc(x1);
-  const __amdgpu_buffer_rsrc_t rx2 = span_rsrc(DUAL ? x2 : x1);
   // one block: cur's products and row sums, nxt (block nb) loaded meanwhile.  The loop below
   // alternates two stages (no stage copy at the back edge: the copy's register moves spilled)
   auto step = [&](PipeStage<CAP>& cur, PipeStage<CAP>& nxt, int blk) __attribute__((always_inline)) {
@@ -491,24 +424,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
       }
       if (threadIdx.x == 0) {
         const int r0 = cur.r0;
-        if (LATEV) {
-          pt1 = s_pt[0].x;
-          pt2 = s_pt[0].y;
-        }
         if (DUAL) {
           const double t = s1 - aux1[r0];
           pt1 += t * t;
           y2[r0] = s2;
           pt2 += aux2[r0] * s2;
         }
+        if (XD) {
+          pt3 += xd.q1[r0] * s2;
+          pt4 += xd.q2[r0] * s2;
+        }
         if (MODE == kEpiPlain) y1[r0] = s1;
         if (MODE == kEpiDot) { y1[r0] = s1; pt1 += aux1[r0] * s1; }
         if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
         if (MODE == kEpiR0) { const double t = aux1[r0] - s1; y1[r0] = t; pt1 += t * t; }
-        if (LATEV) s_pt[0] = make_double2(pt1, pt2);
       }
       nxt.nnz = 0;
-      if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, true, TM>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+      if (nb < b1) pipe_load<CAP, MODE, C16>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
       return;
     }
     // this block's gathers first, then the next block's loads: the gathers' vmcnt wait does not
@@ -517,19 +449,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
-      if constexpr (BUF) {
-        g1[u] = buf_ld1(rx1, c * 8);
-        if (DUAL) g2[u] = buf_ld1(rx2, c * 8);
-      } else {
-        g1[u] = x1[c];
-        if (DUAL) g2[u] = x2[c];
-      }
+      g1[u] = x1[c];
+      if (DUAL) g2[u] = x2[c];
+    }
+    // MODE 5: the row's q1 / q2 entries go out with the gathers (waited for with them, before the
+    // next block's loads are issued), not with the stage: in the stage they spilled
+    double xq1 = 0.0, xq2 = 0.0;
+    if (XD && cur.r0 + static_cast<int>(threadIdx.x) < cur.r1) {
+      xq1 = xd.q1[cur.r0 + threadIdx.x];
+      xq2 = xd.q2[cur.r0 + threadIdx.x];
     }
     nxt.nnz = 0;
-    if (nb < b1) pipe_load<CAP, MODE, NT, C16, BUF, !LATEV, TM>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
+    if (nb < b1) pipe_load<CAP, MODE, C16>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
     // entry i = tid + u kBlock sits at i + i/16 = (tid + tid/16) + u (kBlock + kBlock/16): one base
     // register and an immediate offset per u (the compiler's own form of i + i/16 kept 8 addresses
-    // live, which spilled at 4 waves per SIMD)
+    // live)
     const int pbase = threadIdx.x + (threadIdx.x >> 4);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
@@ -542,13 +476,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
       }
     }
     __syncthreads();
-    if (LATEV && nb < b1) pipe_load_vals<CAP>(nxt, va);
     const int r = cur.r0 + threadIdx.x;
     if (r < cur.r1) {
       double s1 = 0.0, s2 = 0.0;
       // LDS reads in flight in groups, then the adds in row order (the sum is still left to right)
       int t = cur.rs;
-      for (; WPE < 4 && t + 8 <= cur.re; t += 8) {  // (at 4 waves per SIMD the group of 8 spills)
+      for (; t + 8 <= cur.re; t += 8) {
         if constexpr (DUAL) {
           double2 pp[8];
 #pragma unroll
@@ -596,323 +529,77 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
           s1 += s_p[t + (t >> 4)];
         }
       }
-      if (LATEV) {
-        pt1 = s_pt[threadIdx.x].x;
-        pt2 = s_pt[threadIdx.x].y;
-      }
       if (DUAL) {
         const double t = s1 - cur.a1;
         pt1 += t * t;
         y2[r] = s2;
         pt2 += cur.a2 * s2;
       }
+      if (XD) {
+        pt3 += xq1 * s2;
+        pt4 += xq2 * s2;
+      }
       if (MODE == kEpiPlain) y1[r] = s1;
       if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
       if (MODE == kEpiResNorm) { const double t = s1 - cur.a1; pt1 += t * t; }
       if (MODE == kEpiR0) { const double t = cur.a1 - s1; y1[r] = t; pt1 += t * t; }
-      if (LATEV) s_pt[threadIdx.x] = make_double2(pt1, pt2);
     }
     __syncthreads();
   };
   PipeStage<CAP> sa, sb;
-  if (b0 < b1) pipe_load<CAP, MODE, NT, C16, BUF, true, TM>(sa, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
+  if (b0 < b1) pipe_load<CAP, MODE, C16>(sa, meta, b0, ms, rp, ci, c16, base, va, aux1, aux2);
   for (int blk = b0; blk < b1; blk += 2 * bs) {
     step(sa, sb, blk);
     if (blk + bs >= b1) break;
     step(sb, sa, blk + bs);
   }
-  if (LATEV) {
-    pt1 = s_pt[threadIdx.x].x;
-    pt2 = s_pt[threadIdx.x].y;
-  }
   if (MODE != kEpiPlain) {
     const double tot1 = block_sum(pt1, s_wave);
-    double tot2 = 0.0;
+    double tot2 = 0.0, tot3 = 0.0, tot4 = 0.0;
     if (DUAL) tot2 = block_sum(pt2, s_wave);
+    if (XD) {
+      tot3 = block_sum(pt3, s_wave);
+      tot4 = block_sum(pt4, s_wave);
+    }
     if (threadIdx.x == 0) {
       part1[blockIdx.x] = tot1;
       if (DUAL) part2[blockIdx.x] = tot2;
-    }
-  }
-}
-
-// Two-deep variant: block i+1's gathers and block i+2's val/col loads are in flight while block
-// i's products go through LDS, so a workgroup's wait per block is max(memory latency, LDS phase)
-// rather than their sum (~110 VGPRs: 4 workgroups per CU).  Same arithmetic as above.
-template <int CAP, int MODE>
-struct PipeGath {
-  double g1[CAP / kBlock], g2[CAP / kBlock];
-};
-
-template <int CAP, int MODE>
-__device__ __forceinline__ void pipe_gather(PipeGath<CAP, MODE>& G, const PipeStage<CAP>& st,
-                                            const double* __restrict__ x1, const double* __restrict__ x2) {
-  if (st.nnz > CAP) return;
-#pragma unroll
-  for (int u = 0; u < PipeStage<CAP>::kPer; ++u) {
-    G.g1[u] = x1[st.cols[u]];
-    if (MODE == 4) G.g2[u] = x2[st.cols[u]];
-  }
-}
-
-template <int CAP, int MODE>
-__global__ __launch_bounds__(kBlock) void spmv_pipe2_kernel(
-    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
-    const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
-    const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
-    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2) {
-  constexpr bool DUAL = MODE == 4;
-  constexpr int kPer = PipeStage<CAP>::kPer;
-  __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
-  __shared__ double s_wave[4];
-  double pt1 = 0.0, pt2 = 0.0;
-  int b0, b1, bs;
-  block_walk(n_blk, walk, b0, b1, bs);
-  const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
-  PipeStage<CAP> s0, s1;
-  PipeGath<CAP, MODE> g0, g1n;
-  s0.nnz = 0;
-  s1.nnz = 0;
-  if (b0 < b1) pipe_load<CAP, MODE>(s0, meta, b0, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
-  if (b0 < b1) pipe_gather<CAP, MODE>(g0, s0, x1, x2);
-  if (b0 + bs < b1) pipe_load<CAP, MODE>(s1, meta, b0 + bs, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
-  for (int blk = b0; blk < b1; blk += bs) {
-    // in flight from the previous round: g0 (block blk) and s1 (block blk + bs)
-    if (blk + bs < b1) pipe_gather<CAP, MODE>(g1n, s1, x1, x2);
-    PipeStage<CAP> s2;
-    s2.nnz = 0;
-    if (blk + 2 * bs < b1) pipe_load<CAP, MODE>(s2, meta, blk + 2 * bs, ms, rp, ci, nullptr, nullptr, va, aux1, aux2);
-    if (s0.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
-      double acc1 = 0.0, acc2 = 0.0;
-      for (int i = s0.nz0 + threadIdx.x; i < s0.nz0 + s0.nnz; i += kBlock) {
-        acc1 += va[i] * x1[ci[i]];
-        if (DUAL) acc2 += va[i] * x2[ci[i]];
+      if (XD) {
+        xd.part3[blockIdx.x] = tot3;
+        xd.part4[blockIdx.x] = tot4;
       }
-      const double s1v = block_sum(acc1, s_wave);
-      const double s2v = DUAL ? block_sum(acc2, s_wave) : 0.0;
-      if (threadIdx.x == 0) {
-        const int r0 = s0.r0;
-        if (DUAL) {
-          const double t = s1v - aux1[r0];
-          pt1 += t * t;
-          y2[r0] = s2v;
-          pt2 += aux2[r0] * s2v;
-        }
-        if (MODE == kEpiPlain) y1[r0] = s1v;
-        if (MODE == kEpiDot) { y1[r0] = s1v; pt1 += aux1[r0] * s1v; }
-        if (MODE == kEpiResNorm) { const double t = s1v - aux1[r0]; pt1 += t * t; }
-        if (MODE == kEpiR0) { const double t = aux1[r0] - s1v; y1[r0] = t; pt1 += t * t; }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const int i = threadIdx.x + u * kBlock;
-        if (i < s0.nnz) {
-          if constexpr (DUAL)
-            s_p[i + (i >> 4)] = make_double2(s0.vals[u] * g0.g1[u], s0.vals[u] * g0.g2[u]);
-          else
-            s_p[i + (i >> 4)] = s0.vals[u] * g0.g1[u];
-        }
-      }
-      __syncthreads();
-      const int r = s0.r0 + threadIdx.x;
-      if (r < s0.r1) {
-        double sa = 0.0, sb = 0.0;
-        for (int t = s0.rs; t < s0.re; ++t) {
-          if constexpr (DUAL) {
-            const double2 pp = s_p[t + (t >> 4)];
-            sa += pp.x;
-            sb += pp.y;
-          } else {
-            sa += s_p[t + (t >> 4)];
-          }
-        }
-        if (DUAL) {
-          const double t = sa - s0.a1;
-          pt1 += t * t;
-          y2[r] = sb;
-          pt2 += s0.a2 * sb;
-        }
-        if (MODE == kEpiPlain) y1[r] = sa;
-        if (MODE == kEpiDot) { y1[r] = sa; pt1 += s0.a1 * sa; }
-        if (MODE == kEpiResNorm) { const double t = sa - s0.a1; pt1 += t * t; }
-        if (MODE == kEpiR0) { const double t = s0.a1 - sa; y1[r] = t; pt1 += t * t; }
-      }
-      __syncthreads();
-    }
-    s0 = s1;
-    g0 = g1n;
-    s1 = s2;
-  }
-  if (MODE != kEpiPlain) {
-    const double tot1 = block_sum(pt1, s_wave);
-    double tot2 = 0.0;
-    if (DUAL) tot2 = block_sum(pt2, s_wave);
-    if (threadIdx.x == 0) {
-      part1[blockIdx.x] = tot1;
-      if (DUAL) part2[blockIdx.x] = tot2;
     }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// K1s: SpMV on a SELL-64 copy (sliced ELL, 64-row slices, entries t-major within a slice): one
-// wave per slice, lane = row.  Entry t of all 64 rows is one coalesced 256-B col / 512-B val
-// load, so a wave has its whole slice's (col, val) and gathers in flight with no LDS staging, no
-// barrier and no row-sum phase (K1p: two barriers and an LDS pass per 2048-nnz block).  Each
-// lane sums its row's rounded products left to right (contraction off): SciPy's csr_matvec
-// order, so rows are bit-identical to K1 / K1p and to A @ x.  Padding (t >= the row's length)
-// is loaded (col = the row itself) but never added.  MODE as K1p (0-3 = K1's epilogues on x1,
-// 4 = the dual: residual of x1, Arnoldi of x2).  Walk: XCD-local eighths (walk 1) or
-// grid-stride; partials per workgroup in wave order (deterministic).
-// Measured at C3 (opt-in, SPIS_OPT_SPMV_PIPE = 6): dual 43.2 vs 41.3 us for K1dp (130 VGPRs, 3
-// waves per SIMD, each slice two dependent round trips: col, then the gathers); forced to 4
-// waves per SIMD 46.3 us (spills); with the next slice's (col, val) prefetched (207 VGPRs, 2
-// waves per SIMD) 51.7 us.  The LDS-staged K1dp keeps more bytes in flight per VGPR.
-// ---------------------------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void spmv_sell_kernel(
-    int64_t n, int n_sl, int walk, const int64_t* __restrict__ off, const int32_t* __restrict__ scol,
-    const double* __restrict__ sval, const uint16_t* __restrict__ slen, const double* __restrict__ x1,
-    const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
-    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2) {
-#pragma clang fp contract(off)
-  constexpr bool DUAL = MODE == 4;
-  constexpr int TW = 16;  // entries per lane in flight per chunk
-  constexpr int NW = kBlock / 64;
-  __shared__ double s_wave[4];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t s0, s1e, ss;
-  if (walk == 1 && (gridDim.x & 7) == 0) {  // XCD x = blockIdx % 8 walks the x-th eighth of the slices
-    const int x = blockIdx.x & 7;
-    s0 = (static_cast<int64_t>(n_sl) * x >> 3) + static_cast<int64_t>(blockIdx.x >> 3) * NW + wid;
-    s1e = static_cast<int64_t>(n_sl) * (x + 1) >> 3;
-    ss = static_cast<int64_t>(gridDim.x >> 3) * NW;
-  } else {
-    s0 = static_cast<int64_t>(blockIdx.x) * NW + wid;
-    s1e = n_sl;
-    ss = static_cast<int64_t>(gridDim.x) * NW;
-  }
-  // gathers through buffer descriptors (32-bit offsets; the host checks 8 n < 2^31)
-  const __amdgpu_buffer_rsrc_t rx1 = vec_rsrc(x1, 8 * n);
-  const __amdgpu_buffer_rsrc_t rx2 = vec_rsrc(DUAL ? x2 : x1, 8 * n);
-  double pt1 = 0.0, pt2 = 0.0;
-  for (int64_t sl = s0; sl < s1e; sl += ss) {
-    const int64_t r = sl * kSellW + lane;
-    const bool valid = r < n;
-    const int len = valid ? static_cast<int>(slen[r]) : 0;
-    const int64_t o = off[sl];
-    const int w = static_cast<int>((off[sl + 1] - o) / kSellW);
-    double a1 = 0.0, a2 = 0.0;
-    for (int t0 = 0; t0 < w; t0 += TW) {
-      int c[TW];
-      double v[TW];
-#pragma unroll
-      for (int u = 0; u < TW; ++u)
-        if (t0 + u < w) {  // wave-uniform
-          c[u] = scol[o + static_cast<int64_t>(t0 + u) * kSellW + lane];
-          v[u] = sval[o + static_cast<int64_t>(t0 + u) * kSellW + lane];
-        }
-      double g1[TW], g2[TW];
-#pragma unroll
-      for (int u = 0; u < TW; ++u)
-        if (t0 + u < w) {
-          g1[u] = buf_ld1(rx1, c[u] * 8);
-          if (DUAL) g2[u] = buf_ld1(rx2, c[u] * 8);
-        }
-#pragma unroll
-      for (int u = 0; u < TW; ++u)
-        if (t0 + u < len) {
-          a1 += v[u] * g1[u];
-          if (DUAL) a2 += v[u] * g2[u];
-        }
-    }
-    if (valid) {
-      if (DUAL) {
-        const double t = a1 - aux1[r];
-        pt1 += t * t;
-        y2[r] = a2;
-        pt2 += aux2[r] * a2;
-      }
-      if (MODE == kEpiPlain) y1[r] = a1;
-      if (MODE == kEpiDot) { y1[r] = a1; pt1 += aux1[r] * a1; }
-      if (MODE == kEpiResNorm) { const double t = a1 - aux1[r]; pt1 += t * t; }
-      if (MODE == kEpiR0) { const double t = aux1[r] - a1; y1[r] = t; pt1 += t * t; }
-    }
-  }
-  if (MODE != kEpiPlain) {
-    const double tot1 = block_sum(pt1, s_wave);
-    double tot2 = 0.0;
-    if (DUAL) tot2 = block_sum(pt2, s_wave);
-    if (threadIdx.x == 0) {
-      part1[blockIdx.x] = tot1;
-      if (DUAL) part2[blockIdx.x] = tot2;
-    }
-  }
-}
-
-hipError_t launch_spmv_sell(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
-                            double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev) {
-  dim3 g(grid), b(kBlock);
-#define SPIS_SELL(M)                                                                                          \
-  launch_k(spmv_sell_kernel<M>, g, b, 0, s, ev, A.n_rows, A.n_sl, A.walk, A.sl_off, A.sl_col, A.sl_val, A.sl_len, \
-           x1, aux1, y1, part1, x2, aux2, y2, part2)
-  switch (mode) {
-    case 0: SPIS_SELL(0); break;
-    case 1: SPIS_SELL(1); break;
-    case 2: SPIS_SELL(2); break;
-    case 3: SPIS_SELL(3); break;
-    default: SPIS_SELL(4); break;
-  }
-#undef SPIS_SELL
-  return hipGetLastError();
 }
 
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev) {
+                            int grid, hipStream_t s, const LaunchEv* ev, const DualDots* dd) {
   dim3 g(grid), b(kBlock);
+  PipeXD xd;
+  if (dd != nullptr) {
+    if (mode != 4 || dd->q1 == nullptr || dd->q2 == nullptr || dd->part3 == nullptr || dd->part4 == nullptr)
+      return hipErrorInvalidValue;
+    xd.q1 = dd->q1;
+    xd.q2 = dd->q2;
+    xd.part3 = dd->part3;
+    xd.part4 = dd->part4;
+    mode = 5;
+  }
 #define SPIS_PIPE(M)                                                                                            \
-  if (A.depth == 2)                                                                                        \
-    launch_k(spmv_pipe2_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk, \
-             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2);                                                 \
-  else if (A.c16tm && A.col16 != nullptr && !A.nt && !A.w4)                                                     \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true, false, true>, g, b, 0, s, ev, A.indptr, A.indices,      \
-             A.vals, A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base); \
-  else if (A.buf && A.col16 != nullptr && !A.nt)                                                                \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
-  else if (A.buf && !A.nt)                                                                                      \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, false, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);            \
-  else if (A.w4 && A.col16 != nullptr)                                                                          \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, true, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,  \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
-  else if (A.w4)                                                                                                \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 4, false, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);            \
-  else if (A.col16 != nullptr && A.nt)                                                                          \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, true, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,         \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
-  else if (A.col16 != nullptr)                                                                                  \
-    launch_k(spmv_pipe_kernel<kPipeCap, M, false, 1, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals,        \
-             A.blk_meta, A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);         \
-  else if (A.nt)                                                                                                \
+  if (A.col16 != nullptr)                                                                                       \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
-             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr);                      \
+             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, xd);               \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
-             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr)
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, xd)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
     case 2: SPIS_PIPE(2); break;
     case 3: SPIS_PIPE(3); break;
-    default: SPIS_PIPE(4); break;
+    case 4: SPIS_PIPE(4); break;
+    default: SPIS_PIPE(5); break;
   }
 #undef SPIS_PIPE
   return hipGetLastError();
@@ -920,10 +607,10 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
 
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
-                            hipStream_t s, const LaunchEv* ev) {
-  if (A.sl_col != nullptr) return launch_spmv_sell(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
+                            hipStream_t s, const LaunchEv* ev, const DualDots* dd) {
   if (A.blk_meta != nullptr)
-    return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
+    return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev, dd);
+  if (dd != nullptr) return hipErrorInvalidValue;  // the unpipelined dual has no extra dots
   if (A.swz)
     launch_k(spmv_dual_kernel<kDualCap, 1>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
              A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
@@ -943,27 +630,16 @@ static int resident_grid(F kernel) {
   return t < 8 ? 8 : (t > kSpmvGrid ? kSpmvGrid : t);
 }
 
-static int pipe_grid_max(int depth, bool c16, bool w4) {
+static int pipe_grid_max(bool c16) {
   static const int g1 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
-  static const int g1c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 1, true>);
-  static const int g2 = resident_grid(spmv_pipe2_kernel<kPipeCap, 4>);
-  static const int g4 = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 4, false, true>);
-  static const int g4c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 4, true, true>);
-  if (w4 && depth == 1) return c16 ? g4c : g4;
-  return depth == 2 ? g2 : c16 ? g1c : g1;
+  static const int g1c = resident_grid(spmv_pipe_kernel<kPipeCap, 4, true>);
+  return c16 ? g1c : g1;
 }
 
 int spmv_grid(const CsrView& A, bool fixed) {
   // fixed (multi-GPU: partial arrays all-reduced element-wise) = the same count on every rank
   if (fixed) return A.blk_meta != nullptr ? kPipeGridFixed : kSpmvGrid;
-  if (A.sl_col != nullptr) {  // K1s: resident workgroups, waves walk the slices
-    static const int gs = resident_grid(spmv_sell_kernel<4>);
-    const int64_t need = (static_cast<int64_t>(A.n_sl) + (kBlock / 64) - 1) / (kBlock / 64);
-    int g = need < gs ? static_cast<int>(need) : gs;
-    if (g > 8) g &= ~7;
-    return g < 1 ? 1 : g;
-  }
-  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.depth, A.col16 != nullptr, A.w4) : kSpmvGrid;
+  const int cap = A.blk_meta != nullptr ? pipe_grid_max(A.col16 != nullptr) : kSpmvGrid;
   int g = A.n_blk < cap ? A.n_blk : cap;
   if (A.blk_meta != nullptr && g > 8) g &= ~7;  // the XCD-local walk deals workgroups 8 at a time
   return g < 1 ? 1 : g;
@@ -978,8 +654,6 @@ int blas_grid(int64_t n, bool fixed) {
 
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
                        double* partials, int grid, hipStream_t s, const LaunchEv* ev) {
-  if (A.sl_col != nullptr)
-    return launch_spmv_sell(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
   if (A.blk_meta != nullptr)
     return launch_spmv_pipe(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
   dim3 g(grid), b(kBlock);
@@ -1402,9 +1076,15 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
+    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo, const double* __restrict__ xd1,
+    const double* __restrict__ xd2, int n_xd) {
 #pragma clang fp contract(off)
   static_assert(LAG >= 1 && LAG <= 2 && NS >= LAG + 3, "ring: q_{i-1}, the dotted q_{i+LAG}, one loading");
+  // pre: E_1 and E_2's dots q_1.w, q_2.w came from the dual SpMV that produced w (MODE 5: per
+  // SpMV workgroup, n_xd partials each): the gatherer forms h_1, h_2 at once and the data
+  // workgroups neither compute nor publish them (j >= 3: neither is the newest vector's, which
+  // carries the Gram entries G(j, .))
+  const bool pre = LAG == 2 && xd1 != nullptr && j >= 3;
   constexpr int DT = DW * 64;  // data threads
   constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
   __shared__ double2 s_acc[FX ? PER * DT : 1];
@@ -1505,7 +1185,15 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         return all_ok;
       };
       double hm = 0.0;
-      bool ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &hm);
+      bool ok = true;
+      if (pre && m <= 2) {  // a_m from the SpMV's partials: each lane its strided share, in order
+        const double* xp = m == 1 ? xd1 : xd2;
+        double acc = 0.0;
+        for (int t = lane; t < n_xd; t += 64) acc += xp[t];
+        hm = wave_sum_dpp(acc);
+      } else {
+        ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &hm);
+      }
       if (m <= j) {
         // h_m = a_m - sum_{l = max(0, m-LAG)}^{m-1} h_l G(m, l), l ascending
         double gv[LAG];
@@ -1700,11 +1388,12 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     }
     // q_{i+NS-1} into the slot q_{i-1} just left
     if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
-    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
-    if (i == 0) {
+    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well); pre: E_1 and
+    // E_2 are the gatherer's already
+    if (i == 0 && !pre) {
       if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
     }
-    if (i + LAG <= j) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
+    if (i + LAG <= j && !(pre && i == 0)) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
     // x += yx_i q_i (K4's order; x0 is added after the last coefficient), after this step's
     // partials are published: its LDS read-modify-write overlaps the exchange instead of
     // delaying the dots (q_i stays in slot R until the next step's update)
@@ -1940,7 +1629,8 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt,
-                            double* gsub, const double* yx_host, int px, const double* x0, double* xo) {
+                            double* gsub, const double* yx_host, int px, const double* x0, double* xo,
+                            const double* xd1, const double* xd2) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
   // K2q counts (n + 1) / 2 pairs (an odd n's last pair padded): its fallback test must too
@@ -1985,7 +1675,8 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
 #define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
   launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
-           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo)
+           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo,     \
+           xd1, xd2, n_in)
 #define SPIS_LAG_PER(FX_, NT_, LAG_)          \
   switch (per) {                              \
     case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \
@@ -2307,9 +1998,11 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
 }
 
 // workgroup i reduces vector i's partials; add (nullable) + c -> h_out (host H column, nullable)
+// zero_to > gridDim.x: workgroup 0 also zeroes c[gridDim.x, zero_to) (the slack a merged
+// all-reduce carries beside the dots: summed every step, it must not grow)
 __global__ __launch_bounds__(kBlock) void cgs_finalize_kernel(const double* __restrict__ part, int n_in,
                                                               double* __restrict__ c, const double* __restrict__ add,
-                                                              double* __restrict__ h_out) {
+                                                              double* __restrict__ h_out, int zero_to) {
   __shared__ double s_wave[4];
   const int i = blockIdx.x;
   const double t = sum_partials(part + static_cast<int64_t>(i) * n_in, n_in, s_wave);
@@ -2317,6 +2010,8 @@ __global__ __launch_bounds__(kBlock) void cgs_finalize_kernel(const double* __re
     c[i] = t;
     if (h_out != nullptr) h_out[i] = add[i] + t;
   }
+  if (i == 0)
+    for (int z = static_cast<int>(gridDim.x) + threadIdx.x; z < zero_to; z += kBlock) c[z] = 0.0;
 }
 
 hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
@@ -2356,8 +2051,8 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
 }
 
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
-                               hipStream_t s) {
-  hipLaunchKernelGGL(cgs_finalize_kernel, dim3(nv), dim3(kBlock), 0, s, part, n_in, c, add, h_out);
+                               hipStream_t s, int zero_to) {
+  hipLaunchKernelGGL(cgs_finalize_kernel, dim3(nv), dim3(kBlock), 0, s, part, n_in, c, add, h_out, zero_to);
   return hipGetLastError();
 }
 
@@ -3164,334 +2859,6 @@ __global__ __launch_bounds__(kBlock, NP <= 32 ? 3 : 2) void constraint_gram_kern
   }
 }
 
-// K7 on a sliced-ELL copy of M (p + 1 <= 32): row boundaries are static, so each lane half keeps 8
-// rows' w in registers (row 2r + h), gather addresses come straight from per-lane ELL loads, and
-// the slice's t loop has no control flow: independent gathers in flight.  Same chunk / XCD-group
-// schedule, W tile and rank-16 update as constraint_gram_kernel.
-__global__ __launch_bounds__(kBlock, 3) void constraint_gram_ell_kernel(
-    int64_t n, int np1, const int32_t* __restrict__ ecol, const double* __restrict__ eval,
-    const int64_t* __restrict__ eoff, const double* __restrict__ Ut, int nvv, const double* __restrict__ v0,
-    const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ v3,
-    double* __restrict__ partials) {
-  constexpr int NP = 32, SEG = 16, NW = kBlock / 64;
-  constexpr int kWin = 16 * kConRows;  // ELL entries staged per wave and window (16 slice columns)
-  __shared__ __attribute__((aligned(16))) double s_w[NW][kConRows][NP];
-  __shared__ double s_acc[64 * (SEG + 4)];
-  __shared__ int s_ecol[NW][kWin];
-  __shared__ double s_eval[NW][kWin];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int la = lane % NP;
-  const int h = lane / NP;
-  const bool on = la < np1;
-  const int lac = on ? la : 0;
-  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
-  const int grp = blockIdx.x % ngrp;
-  const int64_t wpg = static_cast<int64_t>(gridDim.x / ngrp) * NW;
-  const int64_t gw = static_cast<int64_t>(blockIdx.x / ngrp) * NW + wid;
-  const int64_t rpg = ((n + ngrp - 1) / ngrp + kConRows - 1) / kConRows * kConRows;
-  const int64_t g0 = grp * rpg;
-  const int64_t g1 = g0 + rpg < n ? g0 + rpg : n;
-  const int64_t nch = g1 > g0 ? (g1 - g0 + kConRows - 1) / kConRows : 0;
-  const bool has_m = ecol != nullptr;
-  double acc[SEG];
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
-  double gv[4] = {0.0, 0.0, 0.0, 0.0};
-  double (*W)[NP] = s_w[wid];
-  for (int64_t ch = gw; ch < nch; ch += wpg) {
-    const int64_t r0 = g0 + ch * kConRows;
-    const int nr = static_cast<int>(g1 - r0 < kConRows ? g1 - r0 : kConRows);
-    const int64_t cg = r0 / kConRows;  // global slice index (g0 is a multiple of 16)
-    double u[kConRows];
-#pragma unroll
-    for (int i = 0; i < kConRows; ++i) u[i] = Ut[(r0 + (i < nr ? i : 0)) * ut_ld(np1) + lac];
-    double vc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (lane < nr) {
-      if (nvv > 0) vc[0] = v0[r0 + lane];
-      if (nvv > 1) vc[1] = v1[r0 + lane];
-      if (nvv > 2) vc[2] = v2[r0 + lane];
-      if (nvv > 3) vc[3] = v3[r0 + lane];
-    }
-    if (has_m) {
-      const int64_t e0 = eoff[cg];
-      const int width = static_cast<int>((eoff[cg + 1] - e0) / kConRows);
-      double wr[kConRows / 2];
-#pragma unroll
-      for (int r = 0; r < kConRows / 2; ++r) wr[r] = 0.0;
-      int* sc = s_ecol[wid];
-      double* sv = s_eval[wid];
-      for (int t0 = 0; t0 < width; t0 += 16) {  // windows of 16 slice columns
-        const int nt = width - t0 < 16 ? width - t0 : 16;
-        const int ne = nt * kConRows;
-        // stage the window's (col, val): contiguous in HBM, coalesced, one round trip
-#pragma unroll
-        for (int q = 0; q < kWin / 64; ++q) {
-          const int e = q * 64 + lane;
-          const int64_t src = e0 + static_cast<int64_t>(t0) * kConRows + (e < ne ? e : 0);
-          sc[e] = ecol[src];
-          sv[e] = eval[src];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll 2
-        for (int t = 0; t < nt; ++t) {
-          double g[kConRows / 2];
-#pragma unroll
-          for (int r = 0; r < kConRows / 2; ++r)
-            g[r] = Ut[static_cast<int64_t>(sc[t * kConRows + 2 * r + h]) * ut_ld(np1) + lac];
-#pragma unroll
-          for (int r = 0; r < kConRows / 2; ++r) wr[r] += sv[t * kConRows + 2 * r + h] * g[r];
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-#pragma unroll
-      for (int r = 0; r < kConRows / 2; ++r) W[2 * r + h][la] = on ? wr[r] : 0.0;
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < kConRows; ++i) {  // rank-16 update, this lane's segment of G's row
-        const double ui = (on && i < nr) ? u[i] : 0.0;
-        const double2* wrow = reinterpret_cast<const double2*>(&W[i][SEG * h]);
-#pragma unroll
-        for (int j = 0; j < SEG; j += 2) {
-          const double2 x2 = wrow[j >> 1];
-          acc[j] += ui * x2.x;
-          acc[j + 1] += ui * x2.y;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (h == 0) {
-#pragma unroll
-      for (int i = 0; i < kConRows; ++i) {
-        const double ui = (on && i < nr) ? u[i] : 0.0;
-        if (nvv > 0) gv[0] += ui * readlane_f64(vc[0], i);
-        if (nvv > 1) gv[1] += ui * readlane_f64(vc[1], i);
-        if (nvv > 2) gv[2] += ui * readlane_f64(vc[2], i);
-        if (nvv > 3) gv[3] += ui * readlane_f64(vc[3], i);
-      }
-    }
-  }
-  for (int w = 0; w < NW; ++w) {
-    if (wid == w) {
-#pragma unroll
-      for (int j = 0; j < SEG; ++j) s_acc[lane * (SEG + 4) + j] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + j]) + acc[j];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        s_acc[lane * (SEG + 4) + SEG + c] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + SEG + c]) + gv[c];
-    }
-    __syncthreads();
-  }
-  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
-  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
-  for (int idx = threadIdx.x; idx < stride; idx += kBlock) {
-    if (idx < np1 * np1) {
-      const int a = idx / np1, b = idx - (idx / np1) * np1;
-      out[idx] = has_m ? s_acc[(a + NP * (b / SEG)) * (SEG + 4) + (b % SEG)] : 0.0;
-    } else {
-      const int k2 = idx - np1 * np1;
-      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
-      out[idx] = s_acc[a * (SEG + 4) + SEG + c];
-    }
-  }
-}
-
-// K7s: chunk-staged constraint Gram (p + 1 <= 32), software-pipelined over the chunks of a
-// workgroup.  Per chunk (<= 64 rows = <= 4 slices of 16):
-//   A. the registers holding the chunk (its distinct columns' Ut rows, its ELL entries, row
-//      locations, linear-term values) go to LDS; the next chunk's column list (loaded a round
-//      earlier) goes to the second column-list buffer;  barrier;
-//   B. the next chunk's loads are issued into registers (they stay in flight through C);
-//   C. wave w takes slice w: lane (a, h) accumulates w_r[a] = sum_t val * U[loc][a] for its 8
-//      rows r = 2i + h of the slice (8 independent chains, LDS operands only), the rows' w go to
-//      the wave's W tile, then K7's rank-16 update G[a][b] += U_r[a] W[r][b] and linear terms.
-// Chunks of XCD group g (blockIdx % 8) are a contiguous eighth of the chunk list, dealt
-// round-robin to its workgroups (speed only: chunk -> workgroup is a fixed function of the grid
-// and chunk count, so the partial sums are deterministic).
-template <int RU>
-__global__ __launch_bounds__(kBlock, 2) void constraint_gram_stg_kernel(
-    int np1, StgView S, const double* __restrict__ Ut, int nvv, const double* __restrict__ v0,
-    const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ v3,
-    double* __restrict__ partials) {
-  constexpr int NP = 32, SEG = 16, NW = kBlock / 64;
-  constexpr int kQ = kStgUmax * NP / 2 / kBlock;  // staged Ut double2 per thread (11)
-  constexpr int kE = kStgNz / kBlock;         // staged entries per thread (4)
-  __shared__ __attribute__((aligned(16))) double s_u[kStgUmax * NP];
-  __shared__ double s_val[kStgNz];
-  __shared__ uint16_t s_loc[kStgNz];
-  __shared__ uint16_t s_rl[kStgRows];
-  __shared__ double s_v[4][kStgRows];
-  __shared__ int s_uq[2][kStgUmax];
-  __shared__ __attribute__((aligned(16))) double s_w[NW][16][NP];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int la = lane % NP;
-  const int h = lane / NP;
-  const bool on = la < np1;
-  const int ngrp = (gridDim.x & 7) == 0 ? 8 : 1;
-  const int grp = blockIdx.x % ngrp;
-  const int cs = static_cast<int>(gridDim.x) / ngrp;
-  const int cb = static_cast<int>((static_cast<int64_t>(S.nch) * grp) / ngrp) + static_cast<int>(blockIdx.x) / ngrp;
-  const int ce = static_cast<int>((static_cast<int64_t>(S.nch) * (grp + 1)) / ngrp);
-  double acc[SEG];
-#pragma unroll
-  for (int j = 0; j < SEG; ++j) acc[j] = 0.0;
-  double gv[4] = {0.0, 0.0, 0.0, 0.0};
-  // staged registers of the next chunk
-  double2 ru[kQ];
-  double rv[kE];
-  uint16_t rloc[kE];
-  uint16_t rrl = 0;
-  double rvc[4] = {0.0, 0.0, 0.0, 0.0};
-  int ruq = 0;  // the column list one chunk further ahead
-  auto load_uq = [&](int ch) {
-    if (ch < ce) {
-      const int u0 = S.uoff[ch], nu = S.uoff[ch + 1] - u0;
-      if (tid < nu) ruq = S.uniq[u0 + tid];
-    }
-  };
-  auto stage = [&](int ch, int buf) {  // loads only: values land in registers
-    const int row0 = S.row[ch], nr = S.row[ch + 1] - row0;
-    const int nu = S.uoff[ch + 1] - S.uoff[ch];
-    const int e0 = S.eoff[ch], ne = S.eoff[ch + 1] - e0;
-    const int* uq = s_uq[buf];
-#pragma unroll
-    for (int q = 0; q < kQ; ++q) {  // 16 lanes per 256-B Ut row (zero padded beyond np1)
-      const int idx = tid + q * kBlock;
-      const int t = idx >> 4, a = 2 * (idx & 15);
-      ru[q] = t < nu ? *reinterpret_cast<const double2*>(Ut + static_cast<int64_t>(uq[t]) * NP + a)
-                     : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int q = 0; q < kE; ++q) {
-      const int e = tid + q * kBlock;
-      rv[q] = e < ne ? S.val[e0 + e] : 0.0;
-      rloc[q] = e < ne ? S.loc[e0 + e] : 0;
-    }
-    if (tid < nr) {
-      rrl = S.rowloc[row0 + tid];
-      if (nvv > 0) rvc[0] = v0[row0 + tid];
-      if (nvv > 1) rvc[1] = v1[row0 + tid];
-      if (nvv > 2) rvc[2] = v2[row0 + tid];
-      if (nvv > 3) rvc[3] = v3[row0 + tid];
-    }
-  };
-  int buf = 0;
-  if (cb < ce) {
-    load_uq(cb);
-    if (tid < kStgUmax) s_uq[0][tid] = ruq;
-    __syncthreads();
-    stage(cb, 0);
-    load_uq(cb + cs);
-  }
-  for (int ch = cb; ch < ce; ch += cs) {
-    const int row0 = S.row[ch], nr = S.row[ch + 1] - row0;
-    // A: this chunk's registers -> LDS; the next chunk's column list -> the other buffer
-#pragma unroll
-    for (int q = 0; q < kQ; ++q) reinterpret_cast<double2*>(s_u)[tid + q * kBlock] = ru[q];
-#pragma unroll
-    for (int q = 0; q < kE; ++q) {
-      s_val[tid + q * kBlock] = rv[q];
-      s_loc[tid + q * kBlock] = rloc[q];
-    }
-    if (tid < kStgRows) {
-      s_rl[tid] = rrl;
-      s_v[0][tid] = rvc[0];
-      s_v[1][tid] = rvc[1];
-      s_v[2][tid] = rvc[2];
-      s_v[3][tid] = rvc[3];
-    }
-    if (tid < kStgUmax) s_uq[buf ^ 1][tid] = ruq;
-    __syncthreads();
-    // B: the next chunk's loads (in flight through C), and the column list after it
-    if (ch + cs < ce) {
-      stage(ch + cs, buf ^ 1);
-      load_uq(ch + 2 * cs);
-    }
-    // C: slice wid of this chunk
-    const int ns = (nr + 15) >> 4;
-    if (wid < ns) {
-      int sb = 0;
-      for (int s2 = 0; s2 < wid; ++s2) sb += 16 * S.width[4 * ch + s2];
-      const int width = S.width[4 * ch + wid];
-      double wr[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) wr[i] = 0.0;
-      for (int t = 0; t < width; ++t) {
-        const int eb = sb + 16 * t + h;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wr[i] += s_val[eb + 2 * i] * s_u[s_loc[eb + 2 * i] * NP + la];
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s_w[wid][2 * i + h][la] = on ? wr[i] : 0.0;
-      __builtin_amdgcn_wave_barrier();
-      const int rows = nr - 16 * wid < 16 ? nr - 16 * wid : 16;
-#pragma unroll RU
-      for (int ii = 0; ii < 16; ++ii) {
-        const bool rv_ok = ii < rows;
-        const int i = 16 * wid + ii;
-        const double ui = (on && rv_ok) ? s_u[s_rl[i] * NP + la] : 0.0;
-        const double2* wrow = reinterpret_cast<const double2*>(&s_w[wid][ii][SEG * h]);
-#pragma unroll
-        for (int j = 0; j < SEG; j += 2) {
-          const double2 x2 = wrow[j >> 1];
-          acc[j] += ui * x2.x;
-          acc[j + 1] += ui * x2.y;
-        }
-        if (h == 0 && rv_ok) {
-          if (nvv > 0) gv[0] += ui * s_v[0][i];
-          if (nvv > 1) gv[1] += ui * s_v[1][i];
-          if (nvv > 2) gv[2] += ui * s_v[2][i];
-          if (nvv > 3) gv[3] += ui * s_v[3][i];
-        }
-      }
-    }
-    buf ^= 1;
-    __syncthreads();
-  }
-  // combine the block's waves in wave order through LDS (s_u reused), one partial per block
-  double* s_acc = s_u;  // 64 x (SEG + 4) doubles
-  for (int w = 0; w < NW; ++w) {
-    if (wid == w) {
-#pragma unroll
-      for (int j = 0; j < SEG; ++j) s_acc[lane * (SEG + 4) + j] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + j]) + acc[j];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        s_acc[lane * (SEG + 4) + SEG + c] = (w == 0 ? 0.0 : s_acc[lane * (SEG + 4) + SEG + c]) + gv[c];
-    }
-    __syncthreads();
-  }
-  const int64_t stride = static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1;
-  double* out = partials + static_cast<int64_t>(blockIdx.x) * stride;
-  for (int idx = tid; idx < stride; idx += kBlock) {
-    if (idx < np1 * np1) {
-      const int a = idx / np1, b = idx - (idx / np1) * np1;
-      out[idx] = s_acc[(a + NP * (b / SEG)) * (SEG + 4) + (b % SEG)];
-    } else {
-      const int k2 = idx - np1 * np1;
-      const int c = k2 / np1, a = k2 - (k2 / np1) * np1;
-      out[idx] = s_acc[a * (SEG + 4) + SEG + c];
-    }
-  }
-}
-
-hipError_t launch_constraint_gram_stg(int64_t n, int np1, const StgView& S, const double* Ut, int nvv,
-                                      const double* const* v, double* partials, double* G, hipStream_t s) {
-  (void)n;
-  if (np1 > 32 || nvv > 4) return hipErrorInvalidValue;
-  const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
-  for (int c = 0; c < nvv; ++c) vv[c] = v[c];
-  const int grid = 256 * 2;  // resident: 2 workgroups per CU (LDS-bound), a multiple of 8
-  // (rank-update unroll 2 measured equal: 1)
-  hipLaunchKernelGGL(constraint_gram_stg_kernel<1>, dim3(grid), dim3(kBlock), 0, s, np1, S, Ut, nvv, vv[0], vv[1],
-                     vv[2], vv[3], partials);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int npairs = np1 * np1 + nvv * np1;
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, grid, partials, G, 0);
-  return hipGetLastError();
-}
-
 hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   double* Ut, hipStream_t s, bool perm) {
   const int np1 = p + 1;
@@ -3763,8 +3130,7 @@ hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, con
 int constraint_gram_partials() { return kConGramGrid; }
 
 hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const double* Ut, int nvv,
-                                  const double* const* v, double* partials, double* G, hipStream_t s,
-                                  const EllView* ell) {
+                                  const double* const* v, double* partials, double* G, hipStream_t s) {
   if (np1 > 64 || nvv > 4 || (M == nullptr && nvv == 0)) return hipErrorInvalidValue;
   const int32_t* rp = M ? M->indptr : nullptr;
   const int32_t* ci = M ? M->indices : nullptr;
@@ -3774,10 +3140,7 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
   // one resident wave-set (256 CUs x blocks per CU at the kernel's occupancy): every group's
   // waves sweep their row range together; a multiple of 8 and <= constraint_gram_partials()
   const int grid = np1 <= 32 ? 256 * 3 : 256 * 2;
-  if (np1 <= 32 && ell != nullptr)
-    hipLaunchKernelGGL(constraint_gram_ell_kernel, dim3(grid), dim3(kBlock), 0, s, n, np1, ell->col, ell->val,
-                       ell->off, Ut, nvv, vv[0], vv[1], vv[2], vv[3], partials);
-  else if (np1 <= 32)
+  if (np1 <= 32)
     hipLaunchKernelGGL(constraint_gram_kernel<32>, dim3(grid), dim3(kBlock), 0, s, n, np1, rp, ci, va, Ut,
                        nvv, vv[0], vv[1], vv[2], vv[3], partials);
   else
@@ -3809,8 +3172,7 @@ hipError_t launch_constraint_gram(int64_t n, int np1, const CsrView* M, const do
 template <int NS>
 __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabView T,
                                                                         const double* __restrict__ Ut,
-                                                                        double* __restrict__ partials, int np1,
-                                                                        int chunk) {
+                                                                        double* __restrict__ partials, int np1) {
   constexpr int NW = kBlock / 64;
   constexpr int NJ = NS / 16;  // table entries per lane and block
   constexpr int NA = 16;
@@ -3822,18 +3184,10 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
   const double2* __restrict__ U2 = reinterpret_cast<const double2*>(Ut);
   // waves take the blocks round-robin over the whole table: blocks differ widely in cost (an
   // edge-row block of swe holds one segment, a rho-row block sixteen, with 4 MFMAs each), and
-  // giving each XCD a contiguous eighth (K7m's schedule) measured 251 vs 141 us at C3
-  // chunk > 0 (opt-in): XCD-local schedule.  Chunk q of `chunk` consecutive blocks belongs to XCD
-  // q mod 8 (blockIdx % 8); that XCD's waves take its chunks' blocks round-robin, so neighbouring
-  // rows' Ut gathers mostly meet in one L2 while every XCD still sees the whole field mix.
-  // The wave's i-th block is blk(L0 + i * wpg), increasing in i (gridDim.x is a multiple of 8).
-  const bool xl = chunk > 0;
-  const int64_t wpg = xl ? static_cast<int64_t>(gridDim.x >> 3) * NW : static_cast<int64_t>(gridDim.x) * NW;
-  const int64_t gw = xl ? static_cast<int64_t>(blockIdx.x >> 3) * NW + wid : static_cast<int64_t>(blockIdx.x) * NW + wid;
-  const int64_t xcd = blockIdx.x & 7;
-  auto blk = [&](int64_t L) -> int64_t {
-    return xl ? ((L / chunk) * 8 + xcd) * chunk + (L % chunk) : L;
-  };
+  // giving each XCD a contiguous eighth (K7m's schedule) measured 251 vs 141 us at C3; an
+  // XCD-local schedule of table chunks measured 131-222 vs 122 us (profiles/r02e_k7t_chunk_sweep.txt)
+  const int64_t wpg = static_cast<int64_t>(gridDim.x) * NW;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * NW + wid;
   const int64_t kb1 = T.nblk;
   v4d_t acc00 = {0.0, 0.0, 0.0, 0.0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
   struct Ent {  // zero-initialised: a block past the range is never loaded, never undefined
@@ -3858,9 +3212,9 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
   };
   int64_t L = gw;
   Ent cur, nxt;  // the table two blocks ahead is in flight: its wait never stalls a block
-  if (blk(L) < kb1) load(blk(L), cur);
-  if (blk(L + wpg) < kb1) load(blk(L + wpg), nxt);
-  for (; blk(L) < kb1; L += wpg) {
+  if (L < kb1) load(L, cur);
+  if (L + wpg < kb1) load(L + wpg, nxt);
+  for (; L < kb1; L += wpg) {
     // readfirstlane returns int: widen through unsigned, or a start bit at slot 31 (32-slot
     // blocks) sign-extends into the slot count (ns = -1: the whole block skipped; the round-2
     // 32-slot failure, tools/k7t_probe.py)
@@ -3896,7 +3250,7 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
       }
     }
     Ent nx2;
-    if (blk(L + 2 * wpg) < kb1) load(blk(L + 2 * wpg), nx2);  // in flight through this block and the next
+    if (L + 2 * wpg < kb1) load(L + 2 * wpg, nx2);  // in flight through this block and the next
     double2 a = make_double2(0.0, 0.0);
     double w0 = 0.0, w1 = 0.0;
 #pragma unroll
@@ -3948,12 +3302,12 @@ __global__ __launch_bounds__(kBlock, 2) void constraint_gram_sym_kernel(SymTabVi
   }
 }
 
-template <int NS>
 static int sym_grid() {
   static const int grid = [] {
     int dev = 0, cus = 256, per = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, constraint_gram_sym_kernel<NS>, kBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, constraint_gram_sym_kernel<kSymSlots>, kBlock, 0) !=
+            hipSuccess ||
         per < 1)
       per = 1;
     int t = (cus * per) & ~7;
@@ -3965,17 +3319,9 @@ static int sym_grid() {
 hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
                                       hipStream_t s) {
   if (np1 > 32) return hipErrorInvalidValue;
-  if (T.ns != 16 && T.ns != 32) return hipErrorInvalidValue;
-  const int grid = T.ns == 16 ? sym_grid<16>() : sym_grid<32>();
-  static const int chunk = [] {  // SPIS_K7T_CHUNK: blocks per XCD-local chunk (0: whole-table round robin)
-    const char* e = std::getenv("SPIS_K7T_CHUNK");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 0;
-  }();
-  if (T.ns == 16)
-    hipLaunchKernelGGL(constraint_gram_sym_kernel<16>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
-  else
-    hipLaunchKernelGGL(constraint_gram_sym_kernel<32>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1, chunk);
+  if (T.ns != kSymSlots) return hipErrorInvalidValue;
+  const int grid = sym_grid();
+  hipLaunchKernelGGL(constraint_gram_sym_kernel<kSymSlots>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int np2 = np1 * np1;

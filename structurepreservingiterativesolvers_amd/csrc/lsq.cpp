@@ -478,7 +478,7 @@ bool second_order_ok(const KKTState& st, const QuadCon* cons, const double* y, c
 }  // namespace
 
 KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, const QuadCon* cons,
-                     const double* y0, double* y, int max_iter) {
+                     const double* y0, double* y, int max_iter, std::vector<double>* lam0) {
   KKTResult res;
   for (int a = 0; a < p; ++a) y[a] = y0[a];
   if (m > p) {  // SLSQP exit mode 2 leaves x at the initial guess
@@ -514,12 +514,13 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   }
   st.tau.assign(m, 0.0);
 
-  // least-squares multipliers at a start point: (J J') lam = -J grad f
-  auto init_lam = [&](const double* ys, std::vector<double>& lam) {
+  // least-squares multipliers at a start point: (J J') lam = -J grad f, with the constraints the
+  // SQP runs on (cc: scaled to unit gradient at y0, as st.S is by then)
+  auto init_lam = [&](const QuadCon* cc, const double* ys, std::vector<double>& lam) {
     lam.assign(m, 0.0);
     if (m == 0) return;
     std::vector<double> J(static_cast<size_t>(m) * p), F(p + m), JJ(static_cast<size_t>(m) * m), r(m);
-    st.residual(cons, ys, lam.data(), F.data(), J);
+    st.residual(cc, ys, lam.data(), F.data(), J);
     for (int i = 0; i < m; ++i) {
       for (int k = 0; k < m; ++k) {
         double t = 0.0;
@@ -599,7 +600,8 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   }
   const QuadCon* cs = sc.data();
   auto run_from = [&](double* ys, std::vector<double>& lam) {
-    init_lam(ys, lam);
+    init_lam(cs, ys, lam);
+    if (lam0 != nullptr && lam0->empty()) *lam0 = lam;  // the first start's (tests)
     return sqp_run(st, cs, ys, lam, max_iter);
   };
   auto accept_s = [&](const Run& run, const double* yr, std::vector<double>& lam) {

@@ -52,8 +52,10 @@ struct KKTResult {
 // min ||g - R y||^2  s.t.  c_i(y) = 0, i < m ; y initialised with y0.  R upper triangular
 // p x p column-major with leading dimension ld.  Mirrors SLSQP's observable outcomes:
 // m > p -> y = y0, message "More equality constraints than independent variables".
+// lam0 (tests): receives the first start's initial multipliers (least squares on the scaled
+// constraint Jacobian at y0)
 KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, const QuadCon* cons,
-                     const double* y0, double* y, int max_iter = 100);
+                     const double* y0, double* y, int max_iter = 100, std::vector<double>* lam0 = nullptr);
 
 // dense LU with partial pivoting; returns false if singular / non-finite
 bool lu_solve(int n, std::vector<double>& A /* row-major n x n, destroyed */, double* b);

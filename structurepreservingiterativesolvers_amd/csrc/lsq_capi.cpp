@@ -45,6 +45,29 @@ int lsq_kkt_solve(int p, const double* H, double beta, int m, const double* term
   return r.finite ? 0 : 1;
 }
 
+// the first start's initial multipliers of kkt_newton (lam0_out[m]); same arguments as lsq_kkt_solve
+int lsq_kkt_init_multipliers(int p, const double* H, double beta, int m, const double* term0, const double* term1,
+                             const double* term2, const double* y0, double* lam0_out) {
+  GivensQR qr;
+  qr.reset(p, beta);
+  std::vector<double> col(p + 1);
+  for (int j = 0; j < p; ++j) {
+    for (int i = 0; i <= j + 1; ++i) col[i] = H[static_cast<size_t>(j) * (p + 1) + i];
+    qr.add_column(j, col.data());
+  }
+  std::vector<QuadCon> cons(m);
+  for (int i = 0; i < m; ++i) {
+    cons[i].term0 = term0[i];
+    cons[i].term1.assign(term1 + static_cast<size_t>(i) * p, term1 + static_cast<size_t>(i + 1) * p);
+    cons[i].term2.assign(term2 + static_cast<size_t>(i) * p * p, term2 + static_cast<size_t>(i + 1) * p * p);
+  }
+  std::vector<double> y(p), lam0;
+  (void)kkt_newton(p, qr.R(), qr.ld(), qr.g(), m, cons.data(), y0, y.data(), 100, &lam0);
+  if (static_cast<int>(lam0.size()) != m) return 1;
+  for (int i = 0; i < m; ++i) lam0_out[i] = lam0[i];
+  return 0;
+}
+
 double lsq_con_value(int p, double term0, const double* term1, const double* term2, const double* y) {
   QuadCon c;
   c.term0 = term0;

@@ -101,6 +101,8 @@ struct spis_context {
   double* partA = nullptr;  // reduction partials, ping
   double* partB = nullptr;  // reduction partials, pong
   double* partR = nullptr;  // true-residual partials
+  double* partC = nullptr;  // q1.w partials of a dual SpMV feeding a K2q chain (DualDots)
+  double* partD = nullptr;  // q2.w partials
   double* dscal = nullptr;  // small device scalars (kMaxK + 8)
   double* pinned = nullptr;  // pinned, device-mapped host staging (kernels write h / partials here)
   double* pinned_dev = nullptr;  // the same memory as seen from the device
@@ -125,7 +127,6 @@ struct spis_context {
   int prof_period = 1;            // time every prof_period-th Arnoldi iteration
   int prof_iter = 0;              // iteration counter for the sampling
   int prof_phase = 0;             // advanced per solve: the sampled iterations rotate through every position
-  bool force_generic_gram = false;  // tests: take the MZ + tiled-Gram path
   bool fuse_spmv = true;            // residual SpMV of U_j + Arnoldi SpMV of A_{j+2} in one launch
   bool cgs2 = false;                // opt-in CGS2 orthogonalisation (SPIS_OPT_ORTHOG = 1)
   double* cgs_part = nullptr;       // kCgsMax x kRedGrid partials
@@ -138,30 +139,17 @@ struct spis_context {
   double* icwy_G = nullptr;         // kCgsMax x kCgsMax Gram rows G(l, m) = q_l . q_m, m < l
   double* ut_send = nullptr;        // several GPUs: the Ut rows a constraint matrix's halo sends
   size_t ut_send_len = 0;
-  int ell_gram = 3;                 // K7 on: 0 CSR, 1 the sliced-ELL copy, 2 the chunk-staged copy, 3 K7t / K7m, 4 K7m (SPIS_OPT_ELL_GRAM)
+  // constraint reduction (SPIS_OPT_CON_GRAM): 0 generic (M Z SpMM + tiled Gram), 1 K7 on the CSR, 2 K7t for
+  // symmetric matrices / K7m otherwise, 3 K7m for every matrix
+  int con_gram = 2;
   int mgs_chain = 3;                // persistent MGS chain (SPIS_OPT_MGS_CHAIN): 0 off, 1 K2p gathered by workgroup 0, 2 by a dedicated workgroup, 3 K2q pipelined
   int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
-  // U_j's GEMV on stream2, beside A_{j+1}'s chain (SPIS_OPT_OVERLAP_GEMV): 0 off; the dual SpMV
-  // waits for it through 1 a stream write / wait on a device word, 2 the GEMV launch's own
-  // completion event (hipStreamWaitEvent: no blit kernels)
-  int overlap_gemv = 1;
-  hipEvent_t ev_gemv = nullptr;
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
-  int k7t_slots = 16;               // K7t slot-table width (SPIS_OPT_K7T_SLOTS): 16 or 32
-  int lag_mode = 1;                 // SPIS_OPT_LAG_MODE: 1 = L mode where it applies, 0 = never
   int slab_key = 1;                 // SPIS_OPT_SLAB_KEY: slab order's blocks by position within a slab (at upload)
-  int spmv_w4 = 0;                  // SPIS_OPT_SPMV_W4: the pipelined SpMV at 4 waves per SIMD (buffer-descriptor form)
-  int c16tm = 0;                    // SPIS_OPT_C16_TM: thread-major 16-bit column copy (built at upload)
-  int spmv_nt = 0;                  // the pipelined SpMV's matrix stream nontemporal (SPIS_OPT_SPMV_NT): 0 never, 1 always, 2 beyond the Infinity Cache
-  int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 3/4 = two-deep; 5 = auto (2 or 1); 6 = K1s (SELL-64)
+  int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 5 = auto (2 or 1); 7 = 2 on the natural block order
+  // U_j's GEMV on stream2 beside A_{j+1}'s chain when the chain does not carry it (outside L mode,
+  // or a constrained LS_j); the dual SpMV waits for it through a stream write / wait on a device word
   hipStream_t stream2 = nullptr;
-  // early constraint reduction (SPIS_OPT_EARLY_CON): the final forced constrained step's Gram runs
-  // on stream3 as soon as its basis exists, beside the last Arnoldi step and update
-  int early_con = 0;  // 0 off; launched once A_{k-2} (1: measured 5% slower, it delays A_{k-1}'s chain) / A_{k-1} (2: equal)
-  hipStream_t stream3 = nullptr;
-  hipEvent_t ev_pre_in = nullptr, ev_pre_done = nullptr;
-  double* pre_pinned = nullptr;  // the early reduction's results
-  size_t pre_pinned_len = 0;
   double* con_pinned = nullptr;  // the synchronous reduction's results
   size_t con_pinned_len = 0;
   void* gemv_flag = nullptr;  // device word: the side stream's GEMV count
@@ -171,8 +159,6 @@ struct spis_context {
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
   unsigned* chain_err_dev = nullptr;
-  bool use_graphs = false;          // replay captured Arnoldi steps (opt-in: each replay's boundary
-                                    // costs ~5 us of GPU time, more than the host launches it saves)
   std::vector<hipEvent_t> ev_free;
   struct Pending { int kind; hipEvent_t a, b; };
   std::vector<Pending> ev_pending;
@@ -202,33 +188,14 @@ struct spis_matrix {
   uint16_t* col16_d = nullptr;   // C16 copy of the columns (col16.h), or null
   int4* base_nat_d = nullptr;     // its per-block bases, natural block order
   int4* base_slab_d = nullptr;    // the same in slab order
-  uint16_t* col16t_slab_d = nullptr;  // the 16-bit columns thread-major per slab-order block (SPIS_OPT_C16_TM)
-  // sliced-ELL copy for the constraint Gram (K7), built on first use as a constraint matrix
-  int32_t* ell_col = nullptr;
-  double* ell_val = nullptr;
-  int64_t* ell_off = nullptr;
-  // chunk-staged copy for K7s (built on first use; stg_state -1 unknown, 0 not stageable, 1 built)
-  int stg_state = -1;
-  int32_t *stg_row = nullptr, *stg_uoff = nullptr, *stg_uniq = nullptr, *stg_eoff = nullptr, *stg_width = nullptr;
-  uint16_t *stg_loc = nullptr, *stg_rowloc = nullptr;
-  double* stg_val = nullptr;
-  int32_t stg_nch = 0;
   bool all_zero = false;
-  // K1s's SELL-64 copy (built on first use by a solve in SpMV mode 6; sell_state -1 unknown, 0 not
-  // eligible: a row longer than kSellMaxLen or > 25% padding, 1 built)
-  int sell_state = -1;
-  int32_t* sl_col = nullptr;
-  double* sl_val = nullptr;
-  int64_t* sl_off = nullptr;
-  uint16_t* sl_len = nullptr;
-  int32_t n_sl = 0;
   GramSplit gram_rows{};  // K7m's XCD-group row ranges (natural row order)
   // K7t's slot table (symmetric matrices; sym_state -1 unknown, 0 not symmetric, 1 built)
   int sym_state = -1;
   int32_t* sym_col = nullptr;
   double* sym_val = nullptr;
   unsigned long long* sym_mask = nullptr;
-  int32_t sym_nblk = 0, sym_ns = 0;
+  int32_t sym_nblk = 0;
   // halo plan
   int32_t n_ghost = 0;
   std::vector<int32_t> nbr, scnt, rcnt, soff, roff;
@@ -273,28 +240,7 @@ struct spis_workspace {
   int steps = 0;
   int n_iter_y = 0;           // iterations with a stored y
   bool broke_at_start = false;
-  double* bcopy = nullptr;    // b copied at solve start: graph nodes never capture caller pointers
-  // captured [dual SpMV + MGS chain + normalise] of Arnoldi step ja (single GPU, no callback),
-  // replayed with one hipGraphLaunch; valid while graph_key matches
-  std::vector<hipGraphExec_t> arn_graph;
-  struct GraphKey {
-    uint64_t A = 0;  // matrix upload id (an address can be reused by a later upload)
-    const double* pinned_dev = nullptr;
-    int gs = 0, gb = 0;
-    bool cgs2 = false;
-    int chain = 0;
-    bool operator==(const GraphKey& o) const {
-      return A == o.A && pinned_dev == o.pinned_dev && gs == o.gs && gb == o.gb && cgs2 == o.cgs2 &&
-             chain == o.chain;
-    }
-  } graph_key;
 };
-
-static void drop_graphs(spis_workspace* ws) {
-  for (auto& g : ws->arn_graph)
-    if (g) (void)hipGraphExecDestroy(g);
-  ws->arn_graph.clear();
-}
 
 // ------------------------------------------------------------------------------------------------
 // helpers
@@ -317,32 +263,14 @@ CsrView spis_matrix::dual_view() const {
   // 44-45 us grid-stride), the grid-stride walk beyond (C5, 1.5 GB: 502 vs 574 us)
   // (the slab-ordered table wins at both sizes: C5 dual 485 vs 498 us grid-stride)
   if (mode == 5) mode = blk_slab_d != nullptr || 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
-  if (mode == 6 && sell_state == 1) {  // K1s, XCD-local walk
-    v.sl_col = sl_col;
-    v.sl_val = sl_val;
-    v.sl_off = sl_off;
-    v.sl_len = sl_len;
-    v.n_sl = n_sl;
-    v.walk = 1;
-    return v;
-  }
-  if (mode == 6) mode = 12.0 * static_cast<double>(nnz) <= 256.0 * 1024 * 1024 ? 2 : 1;
-  v.nt = ctx->spmv_nt == 1 || (ctx->spmv_nt == 2 && 12.0 * static_cast<double>(nnz) > 256.0 * 1024 * 1024);
-  v.w4 = ctx->spmv_w4 == 1 && !v.nt && n_cols + n_ghost < (int64_t{1} << 28);  // 32-bit byte offsets
-  v.buf = ctx->spmv_w4 == 2 && !v.nt && n_cols + n_ghost < (int64_t{1} << 28);
   if (mode == 7) mode = 2;  // XCD-local walk on the contiguous table (A/B against the slab order)
-  else if ((mode == 2 || mode == 4) && blk_slab_d != nullptr) {
+  else if (mode == 2 && blk_slab_d != nullptr) {
     v.blk_meta = blk_slab_d;
     v.n_blk = n_blk;
     v.walk = 2;
-    v.depth = mode == 4 ? 2 : 1;
-    if (v.depth == 1 && use_col16()) {
+    if (use_col16()) {
       v.col16 = col16_d;
       v.blk_base = base_slab_d;
-      if (col16t_slab_d != nullptr && ctx->c16tm) {
-        v.col16 = col16t_slab_d;
-        v.c16tm = true;
-      }
     }
     return v;
   }
@@ -350,68 +278,12 @@ CsrView spis_matrix::dual_view() const {
     v.blk_meta = blk_meta_d;
     v.n_blk = n_blk;
     v.walk = (mode & 1) == 0 ? 1 : 0;
-    v.depth = mode >= 3 ? 2 : 1;
-    if (v.depth == 1 && use_col16()) {
+    if (use_col16()) {
       v.col16 = col16_d;
       v.blk_base = base_nat_d;
     }
   }
   return v;
-}
-
-// K1s's SELL-64 copy of A (CsrView::sl_*), built once from the device CSR
-static int ensure_sell(spis_context* c, spis_matrix* M) {
-  if (M->sell_state >= 0) return SPIS_OK;
-  M->sell_state = 0;
-  const int64_t n = M->n_rows, nnz = M->nnz;
-  if (n == 0 || M->n_long > 0 || 8 * M->n_cols >= (int64_t(1) << 31)) return SPIS_OK;  // 32-bit gather offsets
-  std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
-  std::vector<double> va(std::max<int64_t>(nnz, 1));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
-  if (nnz > 0) {
-    HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
-  }
-  const int64_t ns = (n + kSellW - 1) / kSellW;
-  std::vector<int64_t> off(ns + 1, 0);
-  for (int64_t sl = 0; sl < ns; ++sl) {
-    int w = 0;
-    for (int64_t r = sl * kSellW; r < std::min<int64_t>(n, (sl + 1) * kSellW); ++r) w = std::max(w, rp[r + 1] - rp[r]);
-    if (w > kSellMaxLen) return SPIS_OK;
-    off[sl + 1] = off[sl] + static_cast<int64_t>(w) * kSellW;
-  }
-  if (static_cast<double>(off[ns]) > 1.25 * static_cast<double>(std::max<int64_t>(nnz, 1)) + kSellW) return SPIS_OK;
-  const int64_t tot = std::max<int64_t>(off[ns], 1);
-  std::vector<int32_t> scol(tot, 0);
-  std::vector<double> sval(tot, 0.0);
-  std::vector<uint16_t> slen(n);
-  for (int64_t sl = 0; sl < ns; ++sl) {
-    const int64_t w = (off[sl + 1] - off[sl]) / kSellW;
-    for (int l = 0; l < kSellW; ++l) {
-      const int64_t r = sl * kSellW + l;
-      const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
-      if (r < n) slen[r] = static_cast<uint16_t>(len);
-      for (int64_t t = 0; t < w; ++t) {
-        const int64_t e = off[sl] + t * kSellW + l;
-        scol[e] = t < len ? ci[rp[r] + t] : static_cast<int32_t>(r < n ? r : 0);
-        sval[e] = t < len ? va[rp[r] + t] : 0.0;
-      }
-    }
-  }
-  auto up = [&](auto** dst, const auto& v) -> int {
-    using T = typename std::remove_reference<decltype(v)>::type::value_type;
-    HIP_TRY(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
-    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
-    return SPIS_OK;
-  };
-  ST_TRY(up(&M->sl_col, scol));
-  ST_TRY(up(&M->sl_val, sval));
-  ST_TRY(up(&M->sl_off, off));
-  ST_TRY(up(&M->sl_len, slen));
-  M->n_sl = static_cast<int32_t>(ns);
-  M->sell_state = 1;
-  return SPIS_OK;
 }
 
 // ---- live kernel timing ------------------------------------------------------------------------
@@ -635,12 +507,13 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     c->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
     HIP_TRY(hipMalloc(&c->gemv_flag, 16));
     HIP_TRY(hipMemset(c->gemv_flag, 0, 16));
     const int np = std::max(kSpmvGrid, kRedGrid);
     HIP_TRY(hipMalloc(&c->partA, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
+    HIP_TRY(hipMalloc(&c->partC, sizeof(double) * np));
+    HIP_TRY(hipMalloc(&c->partD, sizeof(double) * np));
     // partR lives behind the one-reduce MGS's dot vector (icwy_d): on several GPUs the residual
     // partials then ride in the same all-reduce as the dots (arnoldi_post_icwy)
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
@@ -674,9 +547,6 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_gemv, hipEventDisableTiming | hipEventReleaseToDevice));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_pre_in, hipEventDisableTiming | hipEventReleaseToDevice));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_pre_done, hipEventDisableTiming));  // system scope: host reads
     *out = c.release();
     return SPIS_OK;
   })
@@ -699,8 +569,6 @@ static void free_workspace(spis_workspace* ws) {
   (void)hipFree(ws->ydev);
   if (ws->ext) (void)hipFree(ws->ext);
   if (ws->Ut) (void)hipFree(ws->Ut);
-  if (ws->bcopy) (void)hipFree(ws->bcopy);
-  drop_graphs(ws);
   for (auto& cc : ws->con) {
     if (cc.MZ) (void)hipFree(cc.MZ);
     if (cc.Mx0) (void)hipFree(cc.Mx0);
@@ -718,6 +586,8 @@ extern "C" int spis_context_destroy(spis_context* c) {
     for (auto& kv : c->live_blocks) (void)hipFree(kv.first);
     (void)hipFree(c->partA);
     (void)hipFree(c->partB);
+    (void)hipFree(c->partC);
+    (void)hipFree(c->partD);
     (void)hipFree(c->dscal);
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
@@ -745,13 +615,10 @@ extern "C" int spis_context_destroy(spis_context* c) {
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->stream2);
-    (void)hipStreamSynchronize(c->stream3);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_gemv, c->ev_pre_in, c->ev_pre_done})
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
-    (void)hipStreamDestroy(c->stream3);
-    if (c->pre_pinned) (void)hipHostFree(c->pre_pinned);
     if (c->con_pinned) (void)hipHostFree(c->con_pinned);
     delete c;
     return SPIS_OK;
@@ -778,30 +645,21 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     switch (option) {
       case SPIS_OPT_FUSE_SPMV: c->fuse_spmv = value != 0; return SPIS_OK;
-      case SPIS_OPT_GENERIC_GRAM: c->force_generic_gram = value != 0; return SPIS_OK;
-      case SPIS_OPT_GRAPHS: c->use_graphs = value != 0; return SPIS_OK;
-      case SPIS_OPT_ELL_GRAM:
-        if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "ell gram %lld: 0 .. 4", (long long)value);
-        c->ell_gram = static_cast<int>(value);
+      case SPIS_OPT_CON_GRAM:
+        if (value < 0 || value > 3) return fail(SPIS_ERR_ARG, "con gram %lld: 0 .. 3", (long long)value);
+        c->con_gram = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_MGS_CHAIN:
         if (value < 0 || value > 4) return fail(SPIS_ERR_ARG, "mgs chain %lld: 0 .. 4", (long long)value);
         c->mgs_chain = static_cast<int>(value);
         return SPIS_OK;
-      case SPIS_OPT_OVERLAP_GEMV:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "overlap gemv %lld: 0, 1 or 2", (long long)value);
-        c->overlap_gemv = static_cast<int>(value);
-        return SPIS_OK;
       case SPIS_OPT_NT_BASIS:
         if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "nt basis %lld: 0, 1 or 2", (long long)value);
         c->nt_basis = static_cast<int>(value);
         return SPIS_OK;
-      case SPIS_OPT_EARLY_CON:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "early con %lld: 0, 1 or 2", (long long)value);
-        c->early_con = static_cast<int>(value);
-        return SPIS_OK;
       case SPIS_OPT_SPMV_PIPE:
-        if (value < 0 || value > 7) return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0 .. 7", (long long)value);
+        if (value != 0 && value != 1 && value != 2 && value != 5 && value != 7)
+          return fail(SPIS_ERR_ARG, "spmv pipe %lld: 0, 1, 2, 5 or 7", (long long)value);
         c->spmv_pipe = static_cast<int>(value);
         return SPIS_OK;
       case SPIS_OPT_COL16:
@@ -812,33 +670,13 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "orthogonalisation %lld: 0 = MGS, 1 = CGS2", (long long)value);
         c->cgs2 = value == 1;
         return SPIS_OK;
-      case SPIS_OPT_SPMV_NT:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "spmv_nt %lld: 0, 1 or 2", (long long)value);
-        c->spmv_nt = static_cast<int>(value);
-        return SPIS_OK;
       case SPIS_OPT_DIST_MGS:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "dist_mgs %lld: 0 or 1", (long long)value);
         c->dist_mgs = static_cast<int>(value);
         return SPIS_OK;
-      case SPIS_OPT_LAG_MODE:
-        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "lag_mode %lld: 0 or 1", (long long)value);
-        c->lag_mode = static_cast<int>(value);
-        return SPIS_OK;
-      case SPIS_OPT_C16_TM:
-        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "c16_tm %lld: 0 or 1", (long long)value);
-        c->c16tm = static_cast<int>(value);
-        return SPIS_OK;
-      case SPIS_OPT_SPMV_W4:
-        if (value < 0 || value > 2) return fail(SPIS_ERR_ARG, "spmv_w4 %lld: 0, 1 or 2", (long long)value);
-        c->spmv_w4 = static_cast<int>(value);
-        return SPIS_OK;
       case SPIS_OPT_SLAB_KEY:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "slab_key %lld: 0 or 1", (long long)value);
         c->slab_key = static_cast<int>(value);
-        return SPIS_OK;
-      case SPIS_OPT_K7T_SLOTS:
-        if (value != 16 && value != 32) return fail(SPIS_ERR_ARG, "k7t_slots %lld: 16 or 32", (long long)value);
-        c->k7t_slots = static_cast<int>(value);
         return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }
@@ -854,7 +692,6 @@ extern "C" int spis_profile_enable(spis_context* c, int32_t on) {
     c->prof_period = on > 0 ? on : 1;
     c->prof_iter = 0;
     c->prof_phase = 0;
-    c->force_generic_gram = on < 0;  // (negative: test hook selecting the generic Gram path)
     for (int i = 0; i < SPIS_PROF_KINDS; ++i) {
       c->prof_ms[i] = 0.0;
       c->prof_n[i] = 0;
@@ -902,7 +739,6 @@ extern "C" int spis_spmv_bench(spis_context* c, spis_matrix* A, int32_t kind, in
       for (double* d : {x, z, bb, q0}) HIP_TRY(hipMemcpy(d, h.data(), sizeof(double) * pn, hipMemcpyHostToDevice));
     }
     if (cold) HIP_TRY(hipMemsetAsync(fl, 0, sizeof(double) * big, c->stream));
-    if (c->spmv_pipe == 6) ST_TRY(ensure_sell(c, A));  // K1s's copy, as spis_solve builds it
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -1088,17 +924,6 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
                       bs.begin() + kCol16Bases * i);
           HIP_TRY(hipMalloc(&M->base_slab_d, sizeof(int32_t) * bs.size()));
           HIP_TRY(hipMemcpy(M->base_slab_d, bs.data(), sizeof(int32_t) * bs.size(), hipMemcpyHostToDevice));
-          if (c->c16tm && M->n_long == 0) {  // thread-major copy in slab order (no long-row block)
-            std::vector<int32_t> rng(2 * order.size());
-            for (size_t i = 0; i < order.size(); ++i) {
-              rng[2 * i] = pairs[4 * i + 1];
-              rng[2 * i + 1] = pairs[4 * i + 3];
-            }
-            std::vector<uint16_t> tm;
-            build_col16_tm(c16, rng, kPipeCap, kBlock, tm);
-            HIP_TRY(hipMalloc(&M->col16t_slab_d, sizeof(uint16_t) * tm.size()));
-            HIP_TRY(hipMemcpy(M->col16t_slab_d, tm.data(), sizeof(uint16_t) * tm.size(), hipMemcpyHostToDevice));
-          }
         }
       }
     }
@@ -1153,16 +978,8 @@ extern "C" int spis_matrix_destroy(spis_matrix* M) {
     (void)hipFree(M->col16_d);
     (void)hipFree(M->base_nat_d);
     (void)hipFree(M->base_slab_d);
-    (void)hipFree(M->col16t_slab_d);
     (void)hipFree(M->blk_slab_d);
-    if (M->ell_col) (void)hipFree(M->ell_col);
-    if (M->ell_val) (void)hipFree(M->ell_val);
-    if (M->ell_off) (void)hipFree(M->ell_off);
-    for (void* p : {static_cast<void*>(M->stg_row), static_cast<void*>(M->stg_uoff), static_cast<void*>(M->stg_uniq),
-                    static_cast<void*>(M->stg_eoff), static_cast<void*>(M->stg_width), static_cast<void*>(M->stg_loc),
-                    static_cast<void*>(M->stg_val), static_cast<void*>(M->stg_rowloc), static_cast<void*>(M->sym_col),
-                    static_cast<void*>(M->sl_col), static_cast<void*>(M->sl_val), static_cast<void*>(M->sl_off),
-                    static_cast<void*>(M->sl_len), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
+    for (void* p : {static_cast<void*>(M->sym_col), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
       if (p) (void)hipFree(p);
     if (M->send_idx) (void)hipFree(M->send_idx);
     if (M->send_buf) (void)hipFree(M->send_buf);
@@ -1393,7 +1210,6 @@ extern "C" int spis_memcpy_d2h(spis_context* c, void* dst, const void* src, int6
 extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) {
   ABI_GUARD({
     if (!c || !A || !x || !y) return fail(SPIS_ERR_ARG, "null argument");
-    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));
     ST_TRY(exchange(c, A, x));
     HIP_TRY(launch_spmv(A->dual_view(), kEpiPlain, x, y, nullptr, nullptr, spmv_grid(A->dual_view(), fixed_grid(c)),
                         c->stream));
@@ -1405,7 +1221,6 @@ extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) 
 extern "C" int spis_residual_norm(spis_context* c, spis_matrix* A, double* x, const double* b, double* out) {
   ABI_GUARD({
     if (!c || !A || !x || !b || !out) return fail(SPIS_ERR_ARG, "null argument");
-    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));
     ST_TRY(exchange(c, A, x));
     const int g = spmv_grid(A->dual_view(), fixed_grid(c));
     HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, x, nullptr, b, c->partA, g, c->stream));
@@ -1482,72 +1297,12 @@ extern "C" int spis_gram(spis_context* c, int64_t n, int32_t nu, const double* c
 //   G = [z_0 .. z_{p-1}, x0]^T [M_1 Z, v_1, M_1 x0, M_2 Z, v_2, M_2 x0, ...]
 // from which term0 / term1 / term2 of every constraint are read off.
 // ------------------------------------------------------------------------------------------------
-// fused path (single GPU, p + 1 <= 64, <= 4 linear terms): transpose [Z, x0] once, then one
-// wave-per-row pass per constraint matrix (K7) — no M Z columns are materialised
-// One-time sliced-ELL copy of a constraint matrix (kEllRows-row slices, each padded to its longest
-// row with zero entries whose column is the row itself): the CSR comes back to the host once.
-static int ensure_ell(spis_context* c, spis_matrix* M, EllView* out) {
-  if (!M->ell_col) {
-    const int64_t n = M->n_rows, nnz = M->nnz;
-    std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
-    std::vector<double> va(std::max<int64_t>(nnz, 1));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
-    if (nnz > 0) {
-      HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
-    }
-    const int64_t nch = (n + kEllRows - 1) / kEllRows;
-    std::vector<int64_t> off(nch + 1, 0);
-    for (int64_t ch = 0; ch < nch; ++ch) {
-      int64_t width = 0;
-      for (int64_t r = ch * kEllRows; r < std::min<int64_t>(n, (ch + 1) * kEllRows); ++r)
-        width = std::max<int64_t>(width, rp[r + 1] - rp[r]);
-      off[ch + 1] = off[ch] + kEllRows * width;
-    }
-    const int64_t tot = std::max<int64_t>(off[nch], 1);
-    std::vector<int32_t> ecol(tot, 0);
-    std::vector<double> eval(tot, 0.0);
-    for (int64_t ch = 0; ch < nch; ++ch) {
-      const int64_t width = (off[ch + 1] - off[ch]) / kEllRows;
-      for (int rr = 0; rr < kEllRows; ++rr) {
-        const int64_t r = ch * kEllRows + rr;
-        const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
-        for (int64_t t = 0; t < width; ++t) {
-          const int64_t e = off[ch] + t * kEllRows + rr;
-          if (t < len) {
-            ecol[e] = ci[rp[r] + t];
-            eval[e] = va[rp[r] + t];
-          } else {
-            ecol[e] = static_cast<int32_t>(r < n ? r : 0);
-          }
-        }
-      }
-    }
-    HIP_TRY(hipMalloc(&M->ell_col, sizeof(int32_t) * tot));
-    HIP_TRY(hipMalloc(&M->ell_val, sizeof(double) * tot));
-    HIP_TRY(hipMalloc(&M->ell_off, sizeof(int64_t) * (nch + 1)));
-    HIP_TRY(hipMemcpy(M->ell_col, ecol.data(), sizeof(int32_t) * tot, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->ell_val, eval.data(), sizeof(double) * tot, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(M->ell_off, off.data(), sizeof(int64_t) * (nch + 1), hipMemcpyHostToDevice));
-  }
-  out->col = M->ell_col;
-  out->val = M->ell_val;
-  out->off = M->ell_off;
-  return SPIS_OK;
-}
-
+// fused path (p + 1 <= 64, <= 4 linear terms): transpose [Z, x0] once, then one pass per
+// constraint matrix (K7t / K7m on the matrix cores, K7 on the CSR) — no M Z columns are materialised
 // K7t's slot table (kernels.h SymTabView) of a square matrix that equals its transpose exactly;
-// *ok = false otherwise.  Built once per matrix (ns = slots per block).
-static int ensure_symtab(spis_context* c, spis_matrix* M, int ns, SymTabView* out, bool* ok) {
-  if (M->sym_state == 1 && M->sym_ns != ns) {  // another slot count: rebuild
-    for (void* p : {static_cast<void*>(M->sym_col), static_cast<void*>(M->sym_val), static_cast<void*>(M->sym_mask)})
-      if (p) HIP_TRY(hipFree(p));
-    M->sym_col = nullptr;
-    M->sym_val = nullptr;
-    M->sym_mask = nullptr;
-    M->sym_state = -1;
-  }
+// *ok = false otherwise.  Built once per matrix (ns = kSymSlots slots per block).
+static int ensure_symtab(spis_context* c, spis_matrix* M, SymTabView* out, bool* ok) {
+  constexpr int ns = kSymSlots;
   if (M->sym_state < 0) {
     M->sym_state = 0;
     const int64_t n = M->n_rows, nnz = M->nnz;
@@ -1669,130 +1424,11 @@ static int ensure_symtab(spis_context* c, spis_matrix* M, int ns, SymTabView* ou
       ST_TRY(up_(&M->sym_val, tval));
       ST_TRY(up_(&M->sym_mask, tmask));
       M->sym_nblk = static_cast<int32_t>(tmask.size());
-      M->sym_ns = ns;
       M->sym_state = 1;
     }
   }
   *ok = M->sym_state == 1;
-  if (*ok) *out = SymTabView{M->sym_col, M->sym_val, M->sym_mask, M->sym_nblk, M->sym_ns};
-  return SPIS_OK;
-}
-
-// One-time chunking of a constraint matrix for K7s: greedy row chunks of <= kStgRows rows,
-// <= kStgNz ELL entries (16-row slices, each padded to its longest row) and <= kStgUmax distinct
-// columns (the chunk's own rows counted as columns: the rank-1 update reads U_r from the same LDS
-// image).  *ok = false if a single row does not fit (the ELL / CSR kernels then serve the matrix).
-static int ensure_stg(spis_context* c, spis_matrix* M, StgView* out, bool* ok) {
-  if (M->stg_state < 0) {
-    const int64_t n = M->n_rows, nnz = M->nnz;
-    std::vector<int32_t> rp(n + 1), ci(std::max<int64_t>(nnz, 1));
-    std::vector<double> va(std::max<int64_t>(nnz, 1));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(rp.data(), M->indptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
-    if (nnz > 0) {
-      HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
-    }
-    std::vector<int32_t> mark(static_cast<size_t>(std::max<int64_t>(M->n_cols, n)), -1), pos(mark.size(), 0);
-    std::vector<int32_t> row{0}, uoff{0}, uniq, eoff{0}, width;
-    std::vector<uint16_t> eloc, rowloc(std::max<int64_t>(n, 1));
-    std::vector<double> evals;
-    std::vector<int32_t> cur;  // the open chunk's distinct columns
-    int64_t slice_max[kStgRows / 16] = {0, 0, 0, 0};
-    int64_t padded = 0;  // the open chunk's ELL entries
-    bool good = true;
-    int32_t chunk = 0;
-    int64_t r0 = 0;
-    auto close = [&](int64_t r1) {  // sort the chunk's columns, then its ELL slices
-      std::sort(cur.begin(), cur.end());
-      for (size_t t = 0; t < cur.size(); ++t) pos[cur[t]] = static_cast<int32_t>(t);
-      for (int64_t r = r0; r < r1; ++r) rowloc[r] = static_cast<uint16_t>(pos[r]);
-      for (int sl = 0; sl < kStgRows / 16; ++sl) {
-        const int64_t w = slice_max[sl];
-        width.push_back(static_cast<int32_t>(w));
-        for (int64_t t = 0; t < w; ++t)
-          for (int i = 0; i < 16; ++i) {
-            const int64_t r = r0 + 16 * sl + i;
-            const bool in = r < r1 && t < rp[r + 1] - rp[r];
-            eloc.push_back(in ? static_cast<uint16_t>(pos[ci[rp[r] + t]]) : 0);
-            evals.push_back(in ? va[rp[r] + t] : 0.0);
-          }
-        slice_max[sl] = 0;
-      }
-      uniq.insert(uniq.end(), cur.begin(), cur.end());
-      uoff.push_back(static_cast<int32_t>(uniq.size()));
-      eoff.push_back(static_cast<int32_t>(eloc.size()));
-      row.push_back(static_cast<int32_t>(r1));
-      cur.clear();
-      ++chunk;
-      r0 = r1;
-      padded = 0;
-    };
-    std::vector<int32_t> fresh;  // distinct columns row r adds to the open chunk
-    auto probe = [&](int64_t r) {
-      const int32_t tag = -2 - static_cast<int32_t>(r & 0x3fffffff);  // never a chunk id or -1
-      fresh.clear();
-      auto one = [&](int32_t col) {
-        if (mark[col] != chunk && mark[col] != tag) {
-          mark[col] = tag;
-          fresh.push_back(col);
-        }
-      };
-      one(static_cast<int32_t>(r));
-      for (int64_t e = rp[r]; e < rp[r + 1]; ++e) one(ci[e]);
-    };
-    for (int64_t r = 0; r < n; ++r) {
-      const int64_t len = rp[r + 1] - rp[r];
-      probe(r);
-      int64_t rows = r - r0;
-      auto grown = [&](int64_t rw) {  // the chunk's ELL entries with row r at position rw
-        const int sl = static_cast<int>(rw / 16);
-        return padded + 16 * (std::max(slice_max[sl], len) - slice_max[sl]);
-      };
-      if (rows > 0 && (rows + 1 > kStgRows || grown(rows) > kStgNz ||
-                       static_cast<int64_t>(cur.size() + fresh.size()) > kStgUmax)) {
-        for (int32_t col : fresh) mark[col] = -1;
-        close(r);
-        probe(r);
-        rows = 0;
-      }
-      if (16 * len > kStgNz || static_cast<int64_t>(fresh.size()) > kStgUmax) {
-        good = false;
-        break;
-      }
-      padded = grown(rows);
-      slice_max[rows / 16] = std::max(slice_max[rows / 16], len);
-      for (int32_t col : fresh) {
-        mark[col] = chunk;
-        cur.push_back(col);
-      }
-    }
-    if (good && r0 < n) close(n);
-    if (!good || eloc.size() >= (size_t(1) << 31)) {
-      M->stg_state = 0;
-    } else {
-      M->stg_nch = chunk;
-      auto up = [&](auto** dst, const auto& v) -> int {
-        using T = typename std::remove_reference<decltype(v)>::type::value_type;
-        HIP_TRY(hipMalloc(dst, sizeof(T) * std::max<size_t>(v.size(), 1)));
-        if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
-        return SPIS_OK;
-      };
-      ST_TRY(up(&M->stg_row, row));
-      ST_TRY(up(&M->stg_uoff, uoff));
-      ST_TRY(up(&M->stg_uniq, uniq));
-      ST_TRY(up(&M->stg_eoff, eoff));
-      ST_TRY(up(&M->stg_width, width));
-      ST_TRY(up(&M->stg_loc, eloc));
-      ST_TRY(up(&M->stg_val, evals));
-      ST_TRY(up(&M->stg_rowloc, rowloc));
-      M->stg_state = 1;
-    }
-  }
-  *ok = M->stg_state == 1;
-  if (*ok)
-    *out = StgView{M->stg_row, M->stg_uoff, M->stg_uniq, M->stg_eoff, M->stg_width,
-                   M->stg_loc, M->stg_val,  M->stg_rowloc, M->stg_nch};
+  if (*ok) *out = SymTabView{M->sym_col, M->sym_val, M->sym_mask, M->sym_nblk, ns};
   return SPIS_OK;
 }
 
@@ -1846,25 +1482,20 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     if (cons[ci].v_dev) vlist.push_back(cons[ci].v_dev);
   struct Launch {
     int ci;
-    bool stg, ell, sym;
-    EllView ev;
-    StgView sv;
+    bool sym;
     SymTabView tv;
   };
-  // ell_gram 3: K7t for symmetric matrices, K7m otherwise, the linear terms from the transpose;
-  // 4: K7m for every matrix.  Both read Ut in the MFMA column order.
-  const int eg = c->ell_gram;
-  const bool mfma = np1 <= 32 && eg >= 3;
+  // con_gram 2: K7t for symmetric matrices, K7m otherwise, the linear terms from the transpose;
+  // 3: K7m for every matrix.  Both read Ut in the MFMA column order.  1 (and p + 1 > 32): K7 on the CSR.
+  const int eg = c->con_gram;
+  const bool mfma = np1 <= 32 && eg >= 2;
   // K7t's symmetric pairing needs both (r, c) and (c, r) in one rank's rows: single GPU only
-  const bool tsym = mfma && eg == 3 && !c->comm;
+  const bool tsym = mfma && eg == 2 && !c->comm;
   std::vector<Launch> plan;
   for (int ci = 0; ci < m; ++ci) {
     if (cons[ci].M == nullptr || cons[ci].M->all_zero) continue;
-    Launch L{ci, false, false, false, {}, {}, {}};
-    if (np1 <= 32 && eg == 2) ST_TRY(ensure_stg(c, cons[ci].M, &L.sv, &L.stg));
-    L.ell = !L.stg && np1 <= 32 && (eg == 1 || eg == 2);
-    if (L.ell) ST_TRY(ensure_ell(c, cons[ci].M, &L.ev));
-    if (tsym) ST_TRY(ensure_symtab(c, cons[ci].M, c->k7t_slots, &L.tv, &L.sym));
+    Launch L{ci, false, {}};
+    if (tsym) ST_TRY(ensure_symtab(c, cons[ci].M, &L.tv, &L.sym));
     plan.push_back(L);
   }
   const size_t voff = static_cast<size_t>(m) * np1 * np1;
@@ -1890,11 +1521,8 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     } else if (mfma) {
       HIP_TRY(launch_constraint_gram_mfma(n, np1, &mv, &Mc->gram_rows, ws->Ut, nvv, vlist.data(),
                                           c->cg_part, c->cg_G, st));
-    } else if (L.stg) {
-      HIP_TRY(launch_constraint_gram_stg(n, np1, L.sv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st));
     } else {
-      HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st,
-                                     L.ell ? &L.ev : nullptr));
+      HIP_TRY(launch_constraint_gram(n, np1, &mv, ws->Ut, nvv, vlist.data(), c->cg_part, c->cg_G, st));
     }
     ST_TRY(allreduce_on(c, c->cg_G, static_cast<int64_t>(np1) * np1 + static_cast<int64_t>(nvv) * np1, st));
     HIP_TRY(hipMemcpyAsync(dst + static_cast<size_t>(L.ci) * np1 * np1, c->cg_G, sizeof(double) * np1 * np1,
@@ -1955,8 +1583,8 @@ static bool fused_con_ok(const spis_context* c, int p, int m, const spis_constra
   int nlin = 0;
   for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
   // several GPUs: K7m on the local rows, the ghost Ut rows exchanged per matrix, G all-reduced
-  if (c->comm && !(p + 1 <= 32 && c->ell_gram >= 3)) return false;
-  return p + 1 <= 64 && nlin <= 4 && !c->force_generic_gram;
+  if (c->comm && !(p + 1 <= 32 && c->con_gram >= 2)) return false;
+  return p + 1 <= 64 && nlin <= 4 && c->con_gram != 0;
 }
 
 static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
@@ -2227,6 +1855,26 @@ struct Solver {
   }
 
   double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
+  // the dual SpMV feeding A_ja's chain also forms q_1.w and q_2.w (MODE 5, DualDots) when that
+  // chain is a K2q one that can start from them (single GPU, pipelined SpMV table, ja >= 3): the
+  // chain's first two exchanges are then done before it starts
+  int xd_for = -1;  // the Arnoldi step whose chain the last dual SpMV computed E_1, E_2 for
+  bool xd_ok(int ja) const {
+    return ja >= 3 && c->mgs_chain == 3 && !c->cgs2 && !fixed_grid(c) && k2q_fits() && !icwy_on() &&
+           A->dual_view().blk_meta != nullptr;
+  }
+  int launch_dual(int j, int ja, const double* bvec, const LaunchEv* le) {
+    const CsrView v = A->dual_view();
+    if (xd_ok(ja)) {
+      const DualDots dd{Qv(1), Qv(2), c->partC, c->partD};
+      HIP_TRY(launch_spmv_dual(v, xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream, le, &dd));
+      xd_for = ja;
+    } else {
+      HIP_TRY(launch_spmv_dual(v, xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream, le));
+      xd_for = -1;
+    }
+    return SPIS_OK;
+  }
   // rows the update GEMV computes.  Several GPUs: n + n_ghost.  Every basis vector z_l's ghost
   // rows hold its owners' values (exchanged before A_l's SpMV) and x0's were exchanged at the
   // start, so x_j's ghost rows come out bitwise equal to the owners' x_j (same y, same order):
@@ -2338,9 +1986,11 @@ struct Solver {
       const LaunchEv both{e_first.start, e_last.stop};
       if (lag_chain()) arm_hcol(j);
       const int px = (gsub && yx) ? jx + 1 : 0;
+      const bool xd = gsub != nullptr && xd_for == j;  // E_1, E_2 from the dual SpMV (DualDots)
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
                                c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub, yx, px,
-                               ws->x0, px > 0 ? xbuf(jx) : nullptr));
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr, xd ? c->partC : nullptr,
+                               xd ? c->partD : nullptr));
       return SPIS_OK;
     }
     if (yx) return fail(SPIS_ERR_STATE, "fused update GEMV without the pipelined chain");
@@ -2390,7 +2040,8 @@ struct Solver {
     double* coef = c->cgs_c;
     const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
     HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt));
-    HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s));
+    // (merged: the slack between the dots and partR is zeroed, since the all-reduce sums it too)
+    HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s, merged ? kIcwyROff : 0));
     if (merged) {
       ST_TRY(allreduce(c, d, kIcwyROff + gs));  // [d | slack | partR]
       HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
@@ -2444,6 +2095,7 @@ struct Solver {
       ProfEv ps(c, SPIS_PROF_SPMV);
       const LaunchEv le = ps.both();
       HIP_TRY(launch_spmv(A->dual_view(), kEpiDot, Zv(j), ws->w, Qv(0), c->partA, gs, c->stream, &le));
+      xd_for = -1;
     }
     return with_chain ? arnoldi_post(j) : SPIS_OK;
   }
@@ -2457,9 +2109,7 @@ struct Solver {
     c->prof_iter = j;
     ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
     const LaunchEv le = pd.both();
-    HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), b, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs,
-                             c->stream, &le));
-    return SPIS_OK;
+    return launch_dual(j, ja, b, &le);
   }
   // A_ja's chain; jres >= 0: it also reduces U_jres's residual (the dual before it) and publishes
   // it; yx != nullptr: it also computes x_{ja-1} = Z y_{ja-1} + x0
@@ -2467,8 +2117,10 @@ struct Solver {
     if (jres >= 0) return arnoldi_post(ja, c->partR, c->pinned_dev + roff(jres), flag_dev(), seq_dev(jres), yx, ja - 1);
     return arnoldi_post(ja, nullptr, nullptr, nullptr, nullptr, yx, ja - 1);
   }
-  // U_j's GEMV: beside a running chain on the side stream (the main stream waits for it), or in
-  // stream order on the main stream
+  // U_j's GEMV: beside a running chain on the side stream (the main stream waits for it through a
+  // stream write / wait on a device word: ~1.5% faster end to end than an event record + wait, and
+  // equal to waiting on the GEMV dispatch's own completion event), or in stream order on the main
+  // stream
   int enqueue_gemv(int j, int p, const double* y, bool overlap) {
     if (!overlap || p > kYArg) return update_gemv(j, p, y);
     ST_TRY(update_gemv(j, p, y, c->stream2));
@@ -2497,18 +2149,12 @@ struct Solver {
   }
 
   // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
-  // done (optional): the GEMV launch carries a completion event, returned here (the sampled
-  // profiling stop event when this launch is timed, else ev_gemv)
-  int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr, hipEvent_t* done = nullptr) {  // :287
+  int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr) {  // :287
     hipStream_t s = s_gemv ? s_gemv : c->stream;
     c->prof_iter = j;
     {
       ProfEv pg(c, SPIS_PROF_GEMV);
-      LaunchEv le = pg.both();
-      if (done != nullptr) {
-        if (le.stop == nullptr) le.stop = c->ev_gemv;
-        *done = le.stop;
-      }
+      const LaunchEv le = pg.both();
       // several GPUs: over the ghost rows too (n_gx), so x_j's halo needs no exchange
       if (p <= kYArg) {
         // several GPUs: the GEMV runs every iteration beside the distributed MGS; nontemporal basis
@@ -2550,89 +2196,27 @@ struct Solver {
     return SPIS_OK;
   }
 
-  // the dual SpMV of (U_j, A_ja) and A_ja's MGS chain + normalise, as launched on the stream
-  int fused_tail(int j, int ja) {
+  // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch: U_j's
+  // GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM traffic;
+  // multi-GPU: its per-step all-reduces) still running on the main stream; the dual SpMV
+  // (multi-GPU: x_j's halo exchange before it) waits for it.  Safe: every reader of x_j's previous
+  // contents (the dual of U_{j-1}) finished before the chain that published U_{j-1}'s residual
+  // started, and the GEMV's inputs were written before that.
+  int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
+    ST_TRY(enqueue_gemv(j, p, y, true));
+    ST_TRY(arnoldi_pre(ja));
+    if (!c->comm) next_seq(j);
     c->prof_iter = j;
     {
       ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
       const LaunchEv le = pd.both();
-      HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), graphable() ? ws->bcopy : b, c->partR, Zv(ja), ws->w, Qv(0),
-                               c->partA, gs, c->stream, &le));
+      ST_TRY(launch_dual(j, ja, b, &le));
     }
     if (c->comm) {
       ST_TRY(update_comm_finish(j));
       return arnoldi_post(ja);
     }
     return arnoldi_post(ja, c->partR, c->pinned_dev + roff(j), flag_dev(), seq_dev(j));
-  }
-
-  bool graphable() const { return c->use_graphs && !c->comm && !o->pre_fn && !o->pre_matrix && !o->pre_ilu; }
-
-  // captured once per workspace and step index; every pointer in it is a workspace / context /
-  // matrix pointer (graph_key), the per-call values (seq) are read from pinned memory
-  int arn_graph(int ja, hipGraphExec_t* out) {
-    const spis_workspace::GraphKey key{A->uid, c->pinned_dev, gs, gb, c->cgs2, c->mgs_chain};
-    if (!(ws->graph_key == key)) {
-      drop_graphs(ws);
-      ws->graph_key = key;
-    }
-    if (ws->arn_graph.size() < static_cast<size_t>(k + 2)) ws->arn_graph.resize(k + 2, nullptr);
-    if (!ws->arn_graph[ja]) {
-      const bool prof = c->prof;
-      c->prof = false;  // no events inside a captured graph
-      hipGraph_t g = nullptr;
-      HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-      const int st = fused_tail(ja - 2, ja);
-      const hipError_t ec = hipStreamEndCapture(c->stream, &g);
-      c->prof = prof;
-      ST_TRY(st);
-      HIP_TRY(ec);
-      hipGraphExec_t ge = nullptr;
-      const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      HIP_TRY(ei);
-      ws->arn_graph[ja] = ge;
-    }
-    *out = ws->arn_graph[ja];
-    return SPIS_OK;
-  }
-
-  // U_j and A_ja (ja = j + 2, adjacent in stream order) with their two SpMVs in one launch
-  int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
-    if (c->overlap_gemv && p <= kYArg) {
-      // U_j's GEMV on the side stream, next to A_{j+1}'s MGS chain (latency-bound, little HBM
-      // traffic; multi-GPU: its per-step all-reduces) still running on the main stream; the dual
-      // SpMV (multi-GPU: x_j's halo exchange before it) waits for it.  Safe: every
-      // reader of x_j's previous contents (the dual of U_{j-1}) finished before the chain that
-      // published U_{j-1}'s residual started, and the GEMV's inputs were written before that.
-      if (c->overlap_gemv == 2) {
-        // cross-stream order through the GEMV dispatch's own completion event: no marker packet
-        // and no stream-ops blit kernels (those cost ~4.7 us on the main stream per iteration)
-        hipEvent_t done = nullptr;
-        ST_TRY(update_gemv(j, p, y, c->stream2, &done));
-        HIP_TRY(hipStreamWaitEvent(c->stream, done, 0));
-      } else {
-        ST_TRY(update_gemv(j, p, y, c->stream2));
-        // cross-stream order through a stream memory write / wait on a device word (~1.5% faster
-        // end to end than hipEventRecord + hipStreamWaitEvent)
-        ++c->gemv_seq;
-        HIP_TRY(hipStreamWriteValue64(c->stream2, c->gemv_flag, c->gemv_seq, 0));
-        HIP_TRY(hipStreamWaitValue64(c->stream, c->gemv_flag, c->gemv_seq, hipStreamWaitValueGte, ~0ull));
-      }
-    } else {
-      ST_TRY(update_gemv(j, p, y));
-    }
-    ST_TRY(arnoldi_pre(ja));
-    if (!c->comm) next_seq(j);
-    const bool sampled =
-        c->prof && (((j + c->prof_phase) % c->prof_period) == 0 || ((ja + c->prof_phase) % c->prof_period) == 0);
-    if (graphable() && !sampled) {
-      hipGraphExec_t ge = nullptr;
-      ST_TRY(arn_graph(ja, &ge));
-      HIP_TRY(hipGraphLaunch(ge, c->stream));
-      return SPIS_OK;
-    }
-    return fused_tail(j, ja);
   }
 
   // host wait for U_j (which also covers every earlier launch on the stream)
@@ -2700,7 +2284,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
 
     // every solver SpMV runs on the kDualCap row blocks, so the fused and the single launches
     // group their partial sums identically (bit-identical results either way)
-    if (c->spmv_pipe == 6 && !c->comm) ST_TRY(ensure_sell(c, A));  // K1s's copy, once per matrix
     Solver S{c, A, o, ws, b, n, k, spmv_grid(A->dual_view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
     ST_TRY(ensure_pinned(c, S.pinned_need()));
     hipStream_t s = c->stream;
@@ -2714,12 +2297,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
 
     // r0 = b - A x0 ; beta = ||r0|| ; q0 = r0 / beta      (solvers.py:167-177)
     // copies: x0 into the workspace (zero padding for K2q's pairs, one buffer for every x0 use);
-    // b only for graph replays (graph nodes never capture caller pointers); x0 into a halo'd
-    // buffer only when the SpMV reads ghost entries
-    if (S.graphable()) {
-      if (!ws->bcopy) HIP_TRY(hipMalloc(&ws->bcopy, sizeof(double) * ws->pitch));
-      HIP_TRY(launch_copy(n, b, ws->bcopy, s));
-    }
+    // x0 into a halo'd buffer only when the SpMV reads ghost entries
     HIP_TRY(launch_copy(n, x0, ws->x0, s));
     const double* xr0 = ws->x0;
     if (A->n_ghost > 0 || c->comm) {
@@ -2742,7 +2320,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
     // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
     // L mode: the solver loop below (lag_chain: K2q chains publish H[:, j] to the host themselves)
-    const bool L = S.lag_chain() && c->fuse_spmv && !S.graphable() && c->lag_mode == 1;
+    const bool L = S.lag_chain() && c->fuse_spmv;
     if (stamps) stamps[0] = now_s();
     ST_TRY(S.enqueue_arnoldi(0));
     if (!L) HIP_TRY(hipEventRecord(c->ev_arn, s));  // L mode waits for H[:, 0] itself
@@ -2769,31 +2347,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     std::vector<QuadCon> cons(std::max(o->n_constraints, 0));
     bool have_x = false;   // ws->xj holds x[-1] (else x[-1] = r0)
     int pending = -1;      // iteration whose update U_j is in flight and not yet read
-    // early reduction of the final forced constrained step (j = k-1, solvers.py:230): launched on
-    // stream3 once A_{k-2} (the producer of its last basis vector) is queued; class-form
-    // constraints on the fused single-GPU path, no separate preconditioned basis
-    int nlin = 0;
-    for (int i = 0; i < (use_cb ? 0 : o->n_constraints); ++i) nlin += o->constraints[i].v_dev ? 1 : 0;
-    // never beside a persistent MGS chain (K2p / K2b): the chain needs all of its workgroups
-    // resident at once, and a concurrent Gram could hold the CU slots its last workgroups wait
-    // for (the chain would then time out and fail the solve with SPIS_ERR_STATE)
-    const bool chain_runs = !fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, c->mgs_chain >= 2) &&
-                            !(c->cgs2 && k <= kCgsMax);
-    const bool early = c->early_con && o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 && !c->comm &&
-                       k + 1 <= 64 && nlin <= 4 && !c->force_generic_gram && ws->Zb == ws->Q && k >= 4 &&
-                       !chain_runs;
-    bool pre_launched = false;
-    auto launch_early = [&]() -> int {
-      ST_TRY(ensure_host_buf(&c->pre_pinned, &c->pre_pinned_len, con_result_len(o->n_constraints, k)));
-      HIP_TRY(hipEventRecord(c->ev_pre_in, s));
-      HIP_TRY(hipStreamWaitEvent(c->stream3, c->ev_pre_in, 0));
-      ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, k, ws->Zb, ws->pitch, ws->x0, c->stream3,
-                              c->pre_pinned));
-      HIP_TRY(hipEventRecord(c->ev_pre_done, c->stream3));
-      pre_launched = true;
-      return SPIS_OK;
-    };
-
     if (beta == 0.0) {  // x0 solves the system: q0 would be 0/0 (reference: NaNs); report breakdown
       out->events_host[0] |= SPIS_EV_BREAKDOWN;
       ws->broke_at_start = true;
@@ -2816,7 +2369,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // queued ahead of the residual of the iterate before it (queue_gram)
     auto gram_early_ok = [&](int jc) {
       return o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 &&
-             fused_con_ok(c, jc + 1, o->n_constraints, o->constraints) && !pre_launched;
+             fused_con_ok(c, jc + 1, o->n_constraints, o->constraints);
     };
     auto queue_gram = [&](int jc) -> int {
       ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(o->n_constraints, jc + 1)));
@@ -2940,16 +2493,12 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       } else {
         // class-form constraints reduced on the device (:242-247), KKT on the host (:251-255)
         if (stamps) stamps[2 * k + j] = now_s();
-        if (m_active > 0 && pre_launched && p == k && m_active == o->n_constraints) {
-          ST_TRY(wait_event(c->ev_pre_done));  // reduced early, beside the last Arnoldi step
-          con_terms_assemble(m_active, o->constraints, p, c->pre_pinned, cons.data());
-        } else if (m_active > 0 && spec_kkt == j && m_active == o->n_constraints) {
+        if (m_active > 0 && spec_kkt == j && m_active == o->n_constraints) {
           // terms assembled and the KKT solved before res_{j-1} was waited for (above)
         } else if (m_active > 0 && gram_queued == j && m_active == o->n_constraints) {
           ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
           con_terms_assemble(m_active, o->constraints, p, c->con_pinned, cons.data());
         } else if (m_active > 0) {
-          if (pre_launched) HIP_TRY(hipStreamWaitEvent(s, c->ev_pre_done, 0));  // shares Ut / Gram buffers
           ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
                                       cons.data()));
         }
@@ -3010,7 +2559,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (L) {
         // x_j: from c_{j+1} (fused), else a GEMV beside c_{j+1} on the side stream, or after it
         // on the main stream when c_{j+1} computed x_j from the speculative unconstrained y_j
-        if (!fused || constrained) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k && c->overlap_gemv));
+        if (!fused || constrained) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
           ST_TRY(S.enqueue_dual(j, j + 2));
@@ -3030,7 +2579,6 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           ST_TRY(S.enqueue_arnoldi(j + 2));
         }
       }
-      if (early && !pre_launched && j + 2 == k - 3 + c->early_con) ST_TRY(launch_early());  // A_{k-2} / A_{k-1} queued
       have_x = true;
       last_x = j;
       pending = j;
@@ -3046,9 +2594,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
     }
-    // speculative Arnoldi steps (and an unused early reduction) finish before x / ws are used
+    // speculative Arnoldi steps finish before x / ws are used
     // (event spin: a blocking synchronize wakes the host up tens of us late, per solve)
-    if (pre_launched) HIP_TRY(hipStreamWaitEvent(s, c->ev_pre_done, 0));
     HIP_TRY(hipEventRecord(c->ev_gram, s));
     ST_TRY(wait_event(c->ev_gram));
     prof_drain(c);

@@ -3,15 +3,19 @@
 The reference hands SciPy CSR matrices and NumPy vectors to ``solvers.cgmres``
 on every call (e.g. ``swe/LinearSolver.py:46``) and never mutates them
 (``solvers.py:167`` allocates).  This module keeps one HBM copy per matrix
-object: uploads are cached on ``id(A)`` guarded by the identity of its three
-arrays (``data``/``indices``/``indptr`` buffers, shape, nnz) and dropped when the
-SciPy object is garbage collected.  Code that mutates ``A.data`` in place must
-call :func:`invalidate`.
+object: uploads are cached on ``id(A)`` and the addresses of its three arrays
+(``data``/``indices``/``indptr``), dropped when the SciPy object is garbage
+collected, and every solver call re-verifies the cached copy against a digest of
+the arrays' full contents (``spis_host_hash``), on a host thread beside the solve:
+an in-place edit of any entry is detected and the solve is redone on the new
+values (:func:`device_matrix`).
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
+import queue
+import threading
 import weakref
 
 import numpy as np
@@ -23,11 +27,15 @@ _DOUBLE_P = C.POINTER(C.c_double)
 _I32_P = C.POINTER(C.c_int32)
 
 
+_CTX_TOKENS = iter(range(1, 1 << 62))
+
+
 class Context:
     """One HIP device + stream (+ optional RCCL communicator)."""
 
     def __init__(self, device=0):
         self.L = _lib.lib()
+        self.token = next(_CTX_TOKENS)  # never reused (an id() can be, after a Context is dropped)
         h = C.c_void_p()
         _lib.check(self.L.spis_context_create(int(device), C.byref(h)), "spis_context_create")
         self.handle = h
@@ -43,8 +51,8 @@ class Context:
         """Destroy the context; device objects still alive become inert (their finalizers
         see the closed context and do nothing)."""
         if self.handle:
-            for (cid, _), ptrs in list(_POOL.items()):
-                if cid == id(self):
+            for (tok, _), ptrs in list(_POOL.items()):
+                if tok == self.token:
                     for p in ptrs:
                         self.L.spis_free(self.handle, C.c_void_p(p))
                     ptrs.clear()
@@ -54,25 +62,15 @@ class Context:
 
 _OPTIONS = {
     "fuse_spmv": (_lib.OPT_FUSE_SPMV, None),
-    "generic_gram": (_lib.OPT_GENERIC_GRAM, None),
-    "graphs": (_lib.OPT_GRAPHS, None),
     "orthog": (_lib.OPT_ORTHOG, {"mgs": 0, "cgs2": 1}),
-    "ell_gram": (_lib.OPT_ELL_GRAM, {False: 0, True: 1, "csr": 0, "ell": 1, "staged": 2, "mfma": 3, "mfma_full": 4}),
+    "con_gram": (_lib.OPT_CON_GRAM, {"generic": 0, "csr": 1, "mfma": 2, "mfma_full": 3}),
     "mgs_chain": (_lib.OPT_MGS_CHAIN, {False: 0, True: 3, "gather0": 1, "aggregator": 2, "pipelined": 3,
                                        "one_reduce": 4}),
-    "overlap_gemv": (_lib.OPT_OVERLAP_GEMV, {False: 0, True: 1, "word": 1, "event": 2}),
     "nt_basis": (_lib.OPT_NT_BASIS, {False: 0, True: 1, "auto": 2}),
-    "early_con": (_lib.OPT_EARLY_CON, {False: 0, True: 2, "a_k-2": 1, "a_k-1": 2}),  # default False
-    "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "stride2": 3, "xcd2": 4, "auto": 5,
-                                        "sell": 6, "xcd_natural": 7}),
+    "spmv_pipe": (_lib.OPT_SPMV_PIPE, {"off": 0, "stride": 1, "xcd": 2, "auto": 5, "xcd_natural": 7}),
     "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
     "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
-    "spmv_nt": (_lib.OPT_SPMV_NT, {False: 0, True: 1, "auto": 2}),
-    "k7t_slots": (_lib.OPT_K7T_SLOTS, {16: 16, 32: 32}),
-    "lag_mode": (_lib.OPT_LAG_MODE, None),
     "slab_key": (_lib.OPT_SLAB_KEY, None),
-    "spmv_w4": (_lib.OPT_SPMV_W4, {False: 0, True: 1, "buf": 2, 2: 2}),
-    "c16_tm": (_lib.OPT_C16_TM, None),
 }
 
 
@@ -80,32 +78,27 @@ def set_option(name, value, ctx=None):
     """Per-context solver options (``spis_set_option``, include/spis.h):
 
     * ``fuse_spmv`` (True): true-residual and Arnoldi SpMVs in one launch (bit-identical);
-    * ``graphs`` (False): replay captured Arnoldi steps;
     * ``orthog`` ("mgs"): "mgs", the reference's modified Gram-Schmidt, or "cgs2", the
       low-synchronisation option (3 reductions per step; not MGS's rounding);
-    * ``generic_gram`` (False): constraint reduction via SpMM + tiled Gram (tests);
-    * ``ell_gram`` ("mfma"): the fused constraint reduction's kernel: "mfma" (f64 matrix cores;
-      a symmetric constraint matrix through a slot table of its upper triangle, K7t, any other
-      from its CSR, K7m), "mfma_full" (K7m for every matrix), "ell" (sliced ELL; True), "staged"
-      (row chunks whose distinct columns' basis rows are staged in LDS; falls back to "ell" for
-      a matrix with a row that does not fit a chunk) or "csr" (False);
+    * ``con_gram`` ("mfma"): how the constraint terms are reduced: "mfma" (f64 matrix cores; a
+      symmetric constraint matrix through a slot table of its upper triangle, K7t, any other
+      from its CSR, K7m), "mfma_full" (K7m for every matrix), "csr" (the fused reduction without
+      matrix cores, K7) or "generic" (SpMM ``M Z`` + tiled Gram);
     * ``mgs_chain`` (True = "pipelined"): each Arnoldi step's MGS chain + normalise as one persistent
       launch, partial dots gathered by a dedicated workgroup ("aggregator") or by workgroup 0
-      ("gather0"); "pipelined": each dot product one MGS step early by the distributive law
-      (h_{i+1} = q_{i+1}.w^(i) - h_i q_{i+1}.q_i), two exchanges in flight (not MGS's rounding),
-      and beyond its capacity (N > ~1.04M) the one-reduce MGS; "one_reduce": two passes per
-      step (every q_l.w and the newest Gram row, then the update carrying the previous
-      iteration's GEMV), k <= 32; False = one launch per MGS step;
-    * ``overlap_gemv`` (True): the update GEMV on a second stream beside the next MGS chain;
-    * ``nt_basis`` ("auto"): the MGS chain's basis loads are nontemporal when the matrix and the
+      ("gather0"); "pipelined": each dot product two MGS steps early by the distributive law
+      (three exchanges in flight; not MGS's rounding), and beyond its capacity (N > ~1.04M) the
+      one-reduce MGS; "one_reduce": two passes per step (every q_l.w and the newest Gram row, then
+      the update carrying the previous iteration's GEMV), k <= 32; False = one launch per MGS step;
+    * ``nt_basis`` ("auto"): the MGS kernels' basis loads are nontemporal when the matrix and the
       basis exceed the 256 MB Infinity Cache (True: always; False: never), results identical;
-    * ``early_con`` (False): CGMRES's final forced constrained step reduces its constraints on a
-      third stream once the last Arnoldi step is queued (True / "a_k-1") or the one before it
-      ("a_k-2"); results identical, measured no faster at C3;
     * ``spmv_pipe`` ("auto"): solver SpMV kernels — "xcd" pipelined with an XCD-local walk of
-      the row blocks, "stride" pipelined grid-stride, "off" unpipelined, "auto" = "xcd" while
-      the matrix fits the 256 MB Infinity Cache, else "stride" (rows bit-identical in every
-      mode; reduction partials grouped per workgroup);
+      the row blocks (slab order when the upload found one), "xcd_natural" the same on the natural
+      block order, "stride" pipelined grid-stride, "off" unpipelined, "auto" = "xcd" while the
+      matrix fits the 256 MB Infinity Cache or has a slab order, else "stride" (rows bit-identical
+      in every mode; reduction partials grouped per workgroup);
+    * ``col16`` ("auto"): the pipelined SpMV on the 16-bit column copy: "auto" beyond the Infinity
+      Cache, True always, False never (rows bit-identical);
     * ``device_ilu`` ("auto"): how a SuperLU ``pre`` (``spilu``/``splu``) is applied — True on
       the device (K8), False by its host ``pre.solve`` through the callback (as the reference
       does), "auto" on the device when the plan's cost model predicts it is faster
@@ -114,22 +107,20 @@ def set_option(name, value, ctx=None):
     * ``dist_mgs`` ("one_reduce"): several GPUs, MGS's projections in inverse-compact-WY form
       (K2w: 2 all-reduces per Arnoldi step; MGS in exact arithmetic, not its rounding), or
       "per_step" (MGS's j + 2 all-reduces, its rounding);
-    * ``spmv_nt`` (False): nontemporal matrix-stream loads in the pipelined SpMV (True: always;
-      "auto": when values + columns exceed the 256 MB Infinity Cache); results identical;
-    * ``k7t_slots`` (16): K7t slot-table width, 16 or 32 (32 measured slower; kept for tests);
-    * ``lag_mode`` (True): the L-mode schedule (MGS enqueued after the host holds the previous H
-      column, carrying the update GEMV); False: the plain pipelined order;
     * ``slab_key`` (True): matrices uploaded afterwards order the row blocks of a slab by their
       rows' position, so a slab's DoF groups are walked side by side (False: group after group);
-    * ``spmv_w4`` (False): the pipelined SpMV in its 4-waves-per-SIMD buffer-descriptor form
-      (True), or the buffer-descriptor form at the default 3 waves per SIMD ("buf");
-    * ``c16_tm`` (False): matrices uploaded afterwards also keep their 16-bit columns thread-major
-      per slab-order block (one 16-B column load per thread and block); bit-identical."""
+    * ``verify_uploads`` (True): solver calls that take a SciPy matrix check its full content
+      against the cached HBM copy (see :func:`device_matrix`); False trusts identity and buffer
+      addresses only (then call :func:`invalidate` after an in-place change)."""
     ctx = ctx or get_context()
     if name == "device_ilu":
         if value not in (True, False, "auto"):
             raise ValueError("device_ilu must be True, False or 'auto'")
         ctx.device_ilu = value
+        return
+    if name == "verify_uploads":
+        global _VERIFY
+        _VERIFY = bool(value)
         return
     opt, names = _OPTIONS[name]
     v = names[value] if names is not None else int(bool(value))
@@ -199,7 +190,7 @@ _POOL_MAX = 4
 def _pool_release(ctx, n, ptr):
     if not ctx.handle:
         return
-    lst = _POOL.setdefault((id(ctx), n), [])
+    lst = _POOL.setdefault((ctx.token, n), [])
     if len(lst) < _POOL_MAX:
         lst.append(ptr)
     else:
@@ -218,11 +209,17 @@ class DeviceVector(DeviceBuffer):
         """A length-``n`` vector with unspecified contents, from the context's pool of released
         ones when there is one (for outputs a kernel overwrites whole)."""
         n = int(n)
-        lst = _POOL.get((id(ctx), n))
+        lst = _POOL.get((ctx.token, n))
         obj = cls.__new__(cls)
         obj.ctx, obj.n, obj.n_valid = ctx, n, n
+        ptr = None
         if lst:
-            obj.ptr = lst.pop()
+            try:  # a finalizer may run between the test and the pop
+                ptr = lst.pop()
+            except IndexError:
+                ptr = None
+        if ptr is not None:
+            obj.ptr = ptr
         else:
             p = C.c_void_p()
             _lib.check(ctx.L.spis_malloc(ctx.handle, 8 * max(n, 1), C.byref(p)), "spis_malloc")
@@ -304,54 +301,114 @@ def _as_csr(A):
 
 # ---- upload caches --------------------------------------------------------------------------
 _MATRIX_CACHE: dict = {}
+_VERIFY = True  # set_option("verify_uploads", ...)
+_HASH_THREADS = max(1, min(8, len(os.sched_getaffinity(0))))
+_ASYNC_MIN_BYTES = 1 << 22  # smaller matrices are re-verified inline (a thread hand-off costs more)
 
 
 def _matrix_key(A):
     return (id(A), A.shape, int(A.nnz), A.data.ctypes.data, A.indices.ctypes.data, A.indptr.ctypes.data)
 
 
-_FP_SAMPLES = 256
+def content_digest(A):
+    """Digest of a sparse matrix's full contents: ``data``, ``indices`` and ``indptr`` (every
+    byte, spis_host_hash: ~0.1 ms per 1 MiB per thread), its shape and dtypes."""
+    L = _lib.load_library()
+    out = C.c_uint64()
+    parts = [A.shape, str(A.data.dtype), str(A.indices.dtype), str(A.indptr.dtype)]
+    for arr in (A.data, A.indices, A.indptr):
+        a = np.ascontiguousarray(arr)
+        _lib.check(L.spis_host_hash(C.c_void_p(a.ctypes.data), a.nbytes, _HASH_THREADS, C.byref(out)),
+                   "spis_host_hash")
+        parts.append(out.value)
+    return hash(tuple(parts))
 
 
-def fingerprint(A):
-    """Cheap content sample of a sparse matrix: up to 256 evenly strided entries of ``data``
-    and ``indices`` plus ``indptr``'s ends (~7 us at any size; 4096 samples cost 0.1 ms, 2% of
-    a C3 solve, since every solve call checks it).  Cache entries carry it, so an in-place
-    change of ``A.data`` / ``A.indices`` at a sampled position is seen and re-uploaded; a
-    change confined to unsampled entries is not: call :func:`invalidate` after modifying a
-    matrix in place (INTEGRATION.md)."""
-    nnz = int(A.nnz)
-    s = max(1, nnz // _FP_SAMPLES)
-    return hash((A.data[::s].tobytes(), A.indices[::s].tobytes(), int(A.indptr[0]), int(A.indptr[-1])))
+def _nbytes(A):
+    return A.data.nbytes + A.indices.nbytes + A.indptr.nbytes
 
 
-def _cached(cache, key, A, fp, make):
-    """Per-object cache entry ``key -> (fingerprint, value)``, evicted when ``A`` is collected
-    (so a later object that reuses ``id(A)`` can never hit it) and rebuilt on a changed
-    fingerprint."""
+class _Checker:
+    """One daemon host thread that re-verifies cached uploads while the solve runs (the hash and
+    spis_solve are both ctypes calls, which release the GIL)."""
+
+    def __init__(self):
+        self.q: queue.Queue = queue.Queue()
+        self.t = threading.Thread(target=self._loop, name="spis-verify", daemon=True)
+        self.t.start()
+
+    def _loop(self):
+        while True:
+            chk = self.q.get()
+            try:
+                chk.result = content_digest(chk.A) == chk.digest
+            except BaseException as e:  # re-raised by the caller's ok()
+                chk.result = e
+            chk.done.set()
+
+
+_CHECKER = None
+
+
+class PendingCheck:
+    """The re-verification of one cached object against its digest (``ok()`` waits for it)."""
+
+    def __init__(self, A, digest, cache, key):
+        global _CHECKER
+        self.A, self.digest, self.cache, self.key = A, digest, cache, key
+        self.result = None
+        self.done = threading.Event()
+        if _CHECKER is None:
+            _CHECKER = _Checker()
+        _CHECKER.q.put(self)
+
+    def ok(self):
+        self.done.wait()
+        if isinstance(self.result, BaseException):
+            raise self.result
+        if not self.result:  # stale: the next lookup rebuilds the entry
+            self.cache.pop(self.key, None)
+        return self.result
+
+
+def _cached(cache, key, A, make, checks=None):
+    """Per-object cache entry ``key -> (digest, value)``, evicted when ``A`` is collected (so a later
+    object that reuses ``id(A)`` can never hit it).  A hit is re-verified against the full
+    contents: inline, or, when ``checks`` is a list and the arrays are large, by a
+    :class:`PendingCheck` appended to it, which the caller resolves after the work that used the
+    value (solvers._run redoes that work on a stale result)."""
     hit = cache.get(key)
-    if hit is not None and hit[0] == fp:
-        return hit[1]
+    dig = None
+    if hit is not None:
+        if not _VERIFY:
+            return hit[1]
+        if checks is not None and _nbytes(A) >= _ASYNC_MIN_BYTES:
+            checks.append(PendingCheck(A, hit[0], cache, key))
+            return hit[1]
+        dig = content_digest(A)
+        if dig == hit[0]:
+            return hit[1]
     val = make()
     if hit is None:
         try:
             weakref.finalize(A, cache.pop, key, None)
         except TypeError:  # not weak-referenceable: keep until invalidate()
             pass
-    cache[key] = (fp, val)
+    cache[key] = (content_digest(A) if dig is None else dig, val)
     return val
 
 
-def device_matrix(A, ctx=None) -> DeviceMatrix:
-    """HBM copy of SciPy CSR ``A``, cached for the lifetime of ``A`` (keyed on identity, buffer
-    addresses and a content :func:`fingerprint`; after an in-place change call :func:`invalidate`)."""
+def device_matrix(A, ctx=None, checks=None) -> DeviceMatrix:
+    """HBM copy of SciPy CSR ``A``, cached for the lifetime of ``A`` (keyed on identity and buffer
+    addresses) and re-verified against the digest of its full contents on every call — inline,
+    or on the verifier thread when ``checks`` (a list the caller resolves) is given."""
     if isinstance(A, DeviceMatrix):
         return A
     ctx = ctx or get_context()
-    if not sps.issparse(A):
+    if not sps.issparse(A) or A.format not in ("csr", "csc"):
         return DeviceMatrix(ctx, A)
     key = _matrix_key(A) + (ctx.device,)
-    return _cached(_MATRIX_CACHE, key, A, fingerprint(A), lambda: DeviceMatrix(ctx, A))
+    return _cached(_MATRIX_CACHE, key, A, lambda: DeviceMatrix(ctx, A), checks)
 
 
 class DeviceILU:
@@ -454,19 +511,20 @@ def device_ilu(pre, ctx=None) -> DeviceILU:
 _ZERO_CACHE: dict = {}
 
 
-def is_zero_matrix(M):
+def is_zero_matrix(M, checks=None):
     """Whether a sparse matrix has no nonzero value (the reference wrappers' mass ``0*A`` keeps
     A's pattern with all-zero values).  O(nnz) once per matrix, then cached like
-    :func:`device_matrix`: evicted with the object, rebuilt on a changed :func:`fingerprint`."""
+    :func:`device_matrix`: evicted with the object, re-verified against its full contents."""
     if M.nnz == 0:
         return True
-    return _cached(_ZERO_CACHE, _matrix_key(M), M, fingerprint(M), lambda: not np.any(M.data))
+    if M.format not in ("csr", "csc"):
+        return not np.any(M.data)
+    return _cached(_ZERO_CACHE, _matrix_key(M), M, lambda: not np.any(M.data), checks)
 
 
 def invalidate(A=None):
-    """Forget cached uploads and zero tests (of ``A``, or all).  Needed after changing a matrix's
-    values or pattern in place: the caches key on identity, buffer addresses and a sampled
-    :func:`fingerprint`, not on the full contents."""
+    """Forget cached uploads and zero tests (of ``A``, or all).  Not needed for correctness (every
+    call re-verifies the full contents); it frees the HBM copy early."""
     for cache in (_MATRIX_CACHE, _ZERO_CACHE):
         if A is None:
             cache.clear()

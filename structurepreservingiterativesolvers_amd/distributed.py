@@ -375,11 +375,8 @@ def bench_main(args, metric):
     if getattr(args, "orthog", "mgs") == "cgs2":
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_ORTHOG, 1), "spis_set_option")
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_DIST_MGS, getattr(args, "dist_mgs", 1)), "spis_set_option")
-    if hasattr(args, "gemv_sync"):  # bench.py's shared solver flags
-        ov = 0 if args.no_overlap else args.gemv_sync
-        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_OVERLAP_GEMV, ov), "spis_set_option")
+    if hasattr(args, "nt_basis"):  # bench.py's shared solver flags
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_NT_BASIS, args.nt_basis), "spis_set_option")
-        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_SPMV_NT, args.spmv_nt), "spis_set_option")
     bd = sysd.vector(wl["b"])
     x0d = DeviceVector.from_host(np.zeros(sysd.n_local), ctx=ctx)
     conlist = distribute_constraints(sysd, wl["conlist"])

@@ -103,9 +103,15 @@ def _gauss01(npts):
 
 def dg_operators(M, length, q=1):
     """DG(q) mass and ``g`` on a periodic interval (exact Gauss quadrature): (Mass, G, Gpat,
-    cdofs).  q = 1 is :func:`dg1_operators` itself (the golden fixtures were made from it)."""
+    cdofs).  q = 1 is :func:`dg1_operators` itself (the golden fixtures were made from it; the
+    general code at q = 1 agrees with it to rounding, tests/test_assembly_dgq.py)."""
     if q == 1:
         return dg1_operators(M, length)
+    return _dg_operators_general(M, length, q)
+
+
+def _dg_operators_general(M, length, q):
+    """dg_operators' element algebra for any q >= 1 (Lagrange basis on equispaced nodes)."""
     h = length / M
     nl = q + 1
     n = nl * M
@@ -137,6 +143,10 @@ def project_dg(f, M, length, q=1):
     :func:`project_dg1`."""
     if q == 1:
         return project_dg1(f, M, length)
+    return _project_dg_general(f, M, length, q)
+
+
+def _project_dg_general(f, M, length, q):
     h = length / M
     C = _lagrange(q)
     xg, wg = _gauss01(q + 2)

@@ -116,7 +116,7 @@ def _reduce_on_device(const, x0, Z):
 # ------------------------------------------------------------------------------------------------
 # device-side constraint descriptors
 # ------------------------------------------------------------------------------------------------
-def _is_zero_matrix(M):
+def _is_zero_matrix(M, checks=None):
     """O(1) for an empty sparse matrix or a device matrix; O(nnz) once per sparse object
     (:func:`~.device.is_zero_matrix`) otherwise."""
     if M is None:
@@ -124,16 +124,17 @@ def _is_zero_matrix(M):
     if isinstance(M, DeviceMatrix):
         return M.all_zero or M.nnz == 0
     if sps.issparse(M):
-        return is_zero_matrix(M)
+        return is_zero_matrix(M, checks)
     return not np.any(M)
 
 
-def _constraint_desc(const, n, ctx):
+def _constraint_desc(const, n, ctx, checks=None):
     keep = []
     M = getattr(const, "M", None)
     Mh = None
-    if not _is_zero_matrix(M):
-        dm = M if isinstance(M, DeviceMatrix) else device_matrix(M if sps.issparse(M) else sps.csr_matrix(M), ctx=ctx)
+    if not _is_zero_matrix(M, checks):
+        dm = M if isinstance(M, DeviceMatrix) else device_matrix(M if sps.issparse(M) else sps.csr_matrix(M), ctx=ctx,
+                                                                 checks=checks)
         if dm.shape[0] != n:
             raise ValueError(f"constraint matrix has {dm.shape[0]} rows, expected {n}")
         keep.append(dm)
@@ -254,7 +255,7 @@ class IterateList(collections.abc.Sequence):
 # ------------------------------------------------------------------------------------------------
 # preconditioners (solvers.py:149-161)
 # ------------------------------------------------------------------------------------------------
-def _precond_setup(pre, n, ctx, keep):
+def _precond_setup(pre, n, ctx, keep, checks=None):
     """Returns (pre_matrix handle or None, PRECOND_FN or null, pre_ilu handle or None).
 
     A SuperLU object (``spilu``/``splu``) is applied on the device (K8) as the context's
@@ -263,7 +264,7 @@ def _precond_setup(pre, n, ctx, keep):
     if pre is None:
         return None, _lib.PRECOND_FN(), None
     if sps.issparse(pre) and not hasattr(pre, "solve"):
-        dm = device_matrix(pre, ctx=ctx)
+        dm = device_matrix(pre, ctx=ctx, checks=checks)
         keep.append(dm)
         return dm.handle.value, _lib.PRECOND_FN(), None
     if is_superlu(pre) and ctx.nranks == 1 and tuple(pre.shape) == (n, n):
@@ -416,7 +417,10 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     _cp()
     # a device matrix carries its context (distributed rank / communicator); else the default one
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
-    Ad = device_matrix(A, ctx=ctx)
+    # cached uploads of SciPy matrices are re-verified against their full contents on the verifier
+    # thread while the solve runs (device.PendingCheck); a stale one makes the call run again
+    checks = []
+    Ad = device_matrix(A, ctx=ctx, checks=checks)
     n = Ad.shape[0]
     device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
     bd = device_vector(b, ctx=ctx)
@@ -427,7 +431,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     if k < 1:
         raise ValueError("k must be >= 1")
     keep = []
-    pre_mat, pre_fn, pre_ilu = _precond_setup(pre, n, ctx, keep)
+    pre_mat, pre_fn, pre_ilu = _precond_setup(pre, n, ctx, keep, checks)
     conlist = list(conlist)
     descs = None
     conls = _NO_CONLS
@@ -436,7 +440,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
         if all(kd == "class" for kd in kinds):
             arr = (_lib.ConstraintDesc * len(conlist))()
             for i, c in enumerate(conlist):
-                arr[i], kp = _constraint_desc(c, n, ctx)
+                arr[i], kp = _constraint_desc(c, n, ctx, checks)
                 keep.extend(kp)
             descs = arr
         elif "bad" in kinds and method == _lib.CGMRES_P:
@@ -460,6 +464,10 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
                               C.byref(out), C.byref(ws))
     _cp()
+    if not all([chk.ok() for chk in checks]):  # an input matrix changed in place since its upload
+        if status == _lib.OK and ws.value:
+            ctx.L.spis_workspace_release(ws)
+        return _run(method, A, b, x0, k, tol, contol, conlist, pre, timing)
     for item in keep:  # a Python exception inside a callback is re-raised as itself
         if isinstance(item, list) and item:
             raise item[0]

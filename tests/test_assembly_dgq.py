@@ -2,7 +2,7 @@
 CPU.  The reference's lkdvRK driver defaults to degree 3 (``lkdvRK/Evolve.py:19``) and
 ``lkdvRK/lkdvRK.py:48`` takes ``degree``.  Firedrake is absent, so these are exact element
 algebra checks, not a comparison with Firedrake's matrices (parity unpinned for q > 1):
-q = 1 is the round-1 DG(1) assembly bit for bit (the golden fixtures were made from it); for
+q = 1's general code is the round-1 DG(1) assembly to rounding (the golden fixtures were made from it); for
 every q the mass integrates to the domain length, ``g`` annihilates constants and is skew on
 the periodic mesh (central flux), and Mass^-1 G u converges to u' under refinement."""
 import numpy as np
@@ -12,13 +12,28 @@ from structurepreservingiterativesolvers_amd.lkdv import assembly as la
 from structurepreservingiterativesolvers_amd.lkdvRK import assembly as ra
 
 
-def test_degree1_is_the_dg1_assembly():
-    M, G, Gp, c = la.dg_operators(37, 40.0, 1)
+def test_general_dgq_code_at_degree1_is_the_dg1_assembly():
+    """The general DG(q) element algebra run at q = 1 (not dg_operators' q = 1 shortcut, which
+    returns dg1_operators itself) reproduces the round-1 DG(1) assembly the golden fixtures were
+    made from: the same mass and g to rounding, the same facet pattern, the same projection."""
+    M, G, Gp, cdofs = la._dg_operators_general(37, 40.0, 1)
     M1, G1, Gp1, c1 = la.dg1_operators(37, 40.0)
-    for a, b in ((M, M1), (G, G1), (Gp, Gp1)):
-        assert (a != b).nnz == 0
-    f = lambda x: np.sin(x) + 2  # noqa: E731
-    assert np.array_equal(la.project_dg(f, 37, 40.0, 1), la.project_dg1(f, 37, 40.0))
+    for a, b in ((M, M1), (G, G1)):
+        assert a.shape == b.shape
+        np.testing.assert_allclose(a.toarray(), b.toarray(), rtol=0, atol=1e-14 * abs(b).max())
+    pa, pb = Gp.copy(), Gp1.copy()
+    pa.data[:] = 1.0
+    pb.data[:] = 1.0
+    assert (pa != pb).nnz == 0
+    assert np.array_equal(np.asarray(cdofs), np.asarray(c1))
+    # projections: DG(1) integrates f phi with 2 Gauss points per cell, the general code with
+    # q + 2 = 3; both are exact for f of degree <= 2 (f phi of degree <= 3), where they must agree
+    # to rounding (for other f they differ by the 2-point rule's quadrature error: 5e-3 for sin)
+    f = lambda x: -0.2 * x**2 + x + 2  # noqa: E731
+    np.testing.assert_allclose(la._project_dg_general(f, 37, 40.0, 1), la.project_dg1(f, 37, 40.0), rtol=1e-12)
+    # and the public entry points keep returning the DG(1) objects themselves at q = 1
+    Ms, Gs, _, _ = la.dg_operators(37, 40.0, 1)
+    assert (Ms != M1).nnz == 0 and (Gs != G1).nnz == 0
 
 
 @pytest.mark.parametrize("q", [1, 2, 3, 4])

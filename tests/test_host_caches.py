@@ -1,18 +1,28 @@
-"""Host-side upload / zero-test caches (device.py): keyed on identity + buffer addresses + a
-sampled content fingerprint, evicted with the object.  CPU only: no upload happens here."""
+"""Host-side upload / zero-test caches (device.py): keyed on identity + buffer addresses, evicted
+with the object, and re-verified against a digest of the full contents on every use
+(spis_host_hash).  CPU only: no upload happens here (the hash runs in libspis.so without a device)."""
 import gc
 
 import numpy as np
+import pytest
 import scipy.sparse as sps
 
-from structurepreservingiterativesolvers_amd import device
+from structurepreservingiterativesolvers_amd import _lib, device
 
 
-def _mat(seed, zero=False):
+def _mat(seed, zero=False, n=500):
     rng = np.random.default_rng(seed)
-    A = sps.random(500, 500, density=0.02, random_state=rng, format="csr") + sps.identity(500, format="csr")
+    A = sps.random(n, n, density=0.02, random_state=rng, format="csr") + sps.identity(n, format="csr")
     A = sps.csr_matrix(A)
     return 0 * A if zero else A
+
+
+@pytest.fixture(autouse=True)
+def _need_lib():
+    try:
+        _lib.load_library()
+    except _lib.SpisUnavailable as e:  # pragma: no cover - the build is part of the suite's set-up
+        pytest.skip(str(e))
 
 
 def test_zero_cache_evicted_with_object():
@@ -31,13 +41,33 @@ def test_zero_cache_evicted_with_object():
         del N
 
 
-def test_zero_cache_sees_in_place_change_at_sampled_entry():
+@pytest.mark.parametrize("where", [0, 1, 4097, -1])
+def test_zero_cache_sees_any_in_place_change(where):
+    """Every entry is covered, not a sample: entries 1 and 4097 fell between round 3's 256 sampled
+    positions at this size."""
     M = _mat(1, zero=True)
     assert device.is_zero_matrix(M)
-    M.data[0] = 1.0  # entry 0 is always sampled
+    M.data[where] = 1.0
     assert not device.is_zero_matrix(M)
-    M.data[0] = 0.0
+    M.data[where] = 0.0
     assert device.is_zero_matrix(M)
+
+
+def test_deferred_check_reports_a_stale_entry():
+    """With a check list (solvers._run), a large cached entry is verified on the verifier thread;
+    an in-place edit makes the pending check fail and drops the entry."""
+    M = _mat(3, zero=True, n=40_000)
+    assert device._nbytes(M) >= device._ASYNC_MIN_BYTES
+    assert device.is_zero_matrix(M)
+    checks = []
+    assert device.is_zero_matrix(M, checks) and len(checks) == 1
+    assert checks[0].ok()
+    M.data[M.nnz // 2 + 1] = 2.0
+    checks = []
+    assert device.is_zero_matrix(M, checks)  # the stale cached verdict, checked beside the work
+    assert not checks[0].ok()
+    assert device._matrix_key(M) not in device._ZERO_CACHE
+    assert not device.is_zero_matrix(M)
 
 
 def test_invalidate_forgets_entries():
@@ -50,9 +80,33 @@ def test_invalidate_forgets_entries():
     assert not device._ZERO_CACHE
 
 
-def test_fingerprint_samples_every_size():
+def test_content_digest_sees_every_entry():
     for n in (1, 7, 5000, 100_000):
         A = sps.csr_matrix(sps.diags([np.arange(1.0, n + 1)], [0]) + sps.eye(n, k=1))
-        f = device.fingerprint(A)
-        A.data[:] += 1.0
-        assert device.fingerprint(A) != f
+        f = device.content_digest(A)
+        assert device.content_digest(A.copy()) == f
+        for i in {0, A.nnz // 3, A.nnz - 1}:
+            B = A.copy()
+            B.data[i] = np.nextafter(B.data[i], np.inf)  # one ulp of one entry
+            assert device.content_digest(B) != f
+        B = A.copy()
+        B.indices[-1] = (B.indices[-1] + 1) % n if n > 1 else 0
+        if n > 1:
+            assert device.content_digest(B) != f
+
+
+def test_host_hash_independent_of_threads():
+    import ctypes as C
+
+    L = _lib.load_library()
+    a = np.random.default_rng(0).random(3 << 20)  # 24 MiB: several pieces per thread
+    outs = set()
+    for t in (1, 2, 3, 8):
+        h = C.c_uint64()
+        _lib.check(L.spis_host_hash(C.c_void_p(a.ctypes.data), a.nbytes, t, C.byref(h)), "spis_host_hash")
+        outs.add(h.value)
+    assert len(outs) == 1
+    h2 = C.c_uint64()
+    a[12345] = np.nextafter(a[12345], 2.0)
+    _lib.check(L.spis_host_hash(C.c_void_p(a.ctypes.data), a.nbytes, 4, C.byref(h2)), "spis_host_hash")
+    assert h2.value not in outs

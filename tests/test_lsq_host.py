@@ -282,3 +282,33 @@ def test_kkt_checker_sign_at_rounding_floor(lsq):
     res = np.zeros(k + 1)
     res[0] = beta
     assert np.sum((res - H @ y) ** 2) <= 1e-20 * beta ** 2
+
+
+@pytest.mark.parametrize("case", ["kkt_c5_cycle8", "kkt_swe_m30_final_step"])
+def test_kkt_initial_multipliers_on_scaled_jacobian(lsq, case):
+    """the SQP's starting multipliers are the least-squares fit
+    (J_s J_s') lam = -J_s grad f on the constraint Jacobian scaled to unit rows at y0, the same
+    scaled constraints the SQP iterates on.  Round 3 formed J from the unscaled term1 plus the
+    scaled term2 (neither Jacobian), which brought back the ~1e9 mass multiplier the scaling
+    removes (C5 cycle 8: |term1| ~ 1e-11)."""
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "kkt_cases", case + ".npz"))
+    H, beta, y0 = z["H"], float(z["beta"]), z["y0"]
+    t0, t1, t2 = z["t0"], z["t1"], z["t2"]
+    p, m = H.shape[1], len(t0)
+    L = lsq
+    L.lsq_kkt_init_multipliers.argtypes = [C.c_int, PD, C.c_double, C.c_int, PD, PD, PD, PD, PD]
+    lam = np.zeros(m)
+    Hc = np.asfortranarray(H)
+    assert L.lsq_kkt_init_multipliers(p, Hc.ctypes.data_as(PD), beta, m, _p(t0), _p(t1.ravel()), _p(t2.ravel()),
+                                      _p(y0), lam.ctypes.data_as(PD)) == 0
+    rhs = np.zeros(p + 1)
+    rhs[0] = beta
+    grad = -2 * H.T @ (rhs - H @ y0)
+    J = np.stack([t1[i] + (t2[i] + t2[i].T) @ y0 for i in range(m)])
+    Js = J / np.linalg.norm(J, axis=1)[:, None]
+    ref = np.linalg.solve(Js @ Js.T, -Js @ grad)
+    # grad f is formed from R, g on the host side and from H here: equal to its terms' rounding
+    gscale = 2 * (np.abs(H.T) @ (np.abs(H) @ np.abs(y0) + np.abs(rhs))).max()
+    np.testing.assert_allclose(lam, ref, rtol=1e-8, atol=1e-12 * gscale)
+    # unit-gradient constraints: multipliers of the objective's own scale, not the 1e9 of round 3
+    assert np.abs(lam).max() <= 10 * np.linalg.norm(grad)

@@ -17,7 +17,7 @@ os.makedirs(out, exist_ok=True)
 dic, _ = sa.linforms(M=30)
 cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
 k = 25
-for pipe in ("off", "stride", "xcd", "stride2", "xcd2", "sell", "xcd_natural"):
+for pipe in ("off", "stride", "xcd", "xcd_natural"):
     set_option("spmv_pipe", pipe)
     x, d = solvers.cgmres(dic["A"], dic["b"], np.zeros_like(dic["b"]), k, tol=1e-19, conlist=cons)
     xs = d["x"]

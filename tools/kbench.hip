@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../structurepreservingiterativesolvers_amd/csrc/kernels.hip"
+#include "spmv_variants.hip"
 #include "../structurepreservingiterativesolvers_amd/csrc/slab_order.h"
 #include "../structurepreservingiterativesolvers_amd/csrc/col16.h"
 
@@ -560,7 +561,7 @@ int main(int argc, char** argv) {
         if (i >= 5)
           hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
                              dpr + 4096);
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, dmeta,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, dmeta,
                            nbd, 1, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
       }
       // the same on the solver's default table (kPipeCap = 2048-nnz blocks, resident grid): 5 warm,
@@ -570,13 +571,13 @@ int main(int argc, char** argv) {
       int2* dmeta2;
       CK(hipMalloc(&dmeta2, 8 * meta2.size()));
       CK(hipMemcpy(dmeta2, meta2.data(), 8 * meta2.size(), hipMemcpyHostToDevice));
-      const int g2 = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
+      const int g2 = resident_grid(spmv_pipe_var_kernel<kPipeCap, 4>);
       printf("pmc mode: kPipeCap dual on %d blocks, grid %d\n", nb, g2);
       for (int i = 0; i < 10; ++i) {
         if (i >= 5)
           hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2, reinterpret_cast<const double2*>(bx),
                              dpr + 4096);
-        hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva, dmeta2, nb, 1, dx,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva, dmeta2, nb, 1, dx,
                            dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
       }
       // and on the solver's default order (slab-ordered (start, end) pairs, walk 2): 5 warm, 5 cold
@@ -590,7 +591,7 @@ int main(int argc, char** argv) {
           if (i >= 5)
             hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
                                reinterpret_cast<const double2*>(bx), dpr + 4096);
-          hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva,
+          hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4>), dim3(g2), dim3(kBlock), 0, s, drp, dci, dva,
                              dpairs, nb, 2, dx, dy, (double*)nullptr, dpr, dx2, dQ, dw, dpart, (const uint16_t*)nullptr, (const int4*)nullptr);
         }
       }
@@ -658,8 +659,8 @@ int main(int argc, char** argv) {
     double* bx;
     CK(hipMalloc(&bx, 8 * big));
     CK(hipMemset(bx, 0, 8 * big));
-    const int g2 = resident_grid(spmv_pipe_kernel<2048, 4>);
-    const int g4 = resident_grid(spmv_pipe_kernel<4096, 4, false, 2>);
+    const int g2 = resident_grid(spmv_pipe_var_kernel<2048, 4>);
+    const int g4 = resident_grid(spmv_pipe_var_kernel<4096, 4, false, 2>);
     printf("blocks %d / %d, resident grids %d / %d\n", nb2, nb4, g2, g4);
     auto run = [&](const char* name, auto&& launch) {
       for (int cold = 0; cold < 2; ++cold) {
@@ -684,7 +685,7 @@ int main(int argc, char** argv) {
     for (int g : {g2, g2 * 4 / 3 / 8 * 8}) {
       snprintf(nm, sizeof nm, "cap 2048 grid %d", g);
       run(nm, [&] {
-        hipExtLaunchKernelGGL((spmv_pipe_kernel<2048, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva, t2,
+        hipExtLaunchKernelGGL((spmv_pipe_var_kernel<2048, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva, t2,
                               nb2, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr,
                               (const int4*)nullptr);
       });
@@ -692,13 +693,13 @@ int main(int argc, char** argv) {
     for (int g : {g4, 512}) {
       snprintf(nm, sizeof nm, "cap 4096 WPE2 grid %d", g);
       run(nm, [&] {
-        hipExtLaunchKernelGGL((spmv_pipe_kernel<4096, 4, false, 2>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci,
+        hipExtLaunchKernelGGL((spmv_pipe_var_kernel<4096, 4, false, 2>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci,
                               dva, t4, nb4, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb,
                               (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "cap 4096 WPE2 BUF grid %d", g);
       run(nm, [&] {
-        hipExtLaunchKernelGGL((spmv_pipe_kernel<4096, 4, false, 2, false, true>), dim3(g), dim3(kBlock), 0, s, e0, e1,
+        hipExtLaunchKernelGGL((spmv_pipe_var_kernel<4096, 4, false, 2, false, true>), dim3(g), dim3(kBlock), 0, s, e0, e1,
                               0, drp, dci, dva, t4, nb4, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb,
                               (const uint16_t*)nullptr, (const int4*)nullptr);
       });
@@ -764,9 +765,9 @@ int main(int argc, char** argv) {
     double* bx;
     CK(hipMalloc(&bx, 8 * big));
     CK(hipMemset(bx, 0, 8 * big));
-    const int gr = resident_grid(spmv_pipe_kernel<kPipeCap, 4>);
-    printf("blocks %d, resident grid %d (NT %d, WPE2 %d)\n", nb, gr, resident_grid(spmv_pipe_kernel<kPipeCap, 4, true>),
-           resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 2>));
+    const int gr = resident_grid(spmv_pipe_var_kernel<kPipeCap, 4>);
+    printf("blocks %d, resident grid %d (NT %d, WPE2 %d)\n", nb, gr, resident_grid(spmv_pipe_var_kernel<kPipeCap, 4, true>),
+           resident_grid(spmv_pipe_var_kernel<kPipeCap, 4, false, 2>));
     auto run = [&](const char* name, auto&& launch) {
       for (int cold = 0; cold < 2; ++cold) {
         double tot = 0;
@@ -789,7 +790,7 @@ int main(int argc, char** argv) {
 #define SLABRUN(LABEL, NTV, WPEV, MT, WALK, G)                                                                  \
   snprintf(nm, sizeof nm, "%s grid=%d", LABEL, G);                                                             \
   run(nm, [&] {                                                                                                \
-    hipExtLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, \
+    hipExtLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, \
                           dci, dva, MT, nb, WALK, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);             \
   })
     SLABRUN("natural", false, 1, mn, 1, gr);
@@ -799,7 +800,7 @@ int main(int argc, char** argv) {
     SLABRUN("slab WPE2", false, 2, ms, 2, gr);
     SLABRUN("slab WPE2", false, 2, ms, 2, 1024);
 #undef SLABRUN
-    const int gc = resident_grid(spmv_pipe_kernel<kPipeCap, 4, false, 1, true>);
+    const int gc = resident_grid(spmv_pipe_var_kernel<kPipeCap, 4, false, 1, true>);
     printf("C16 resident grid %d\n", gc);
     const double SD16 = SD - 2.0 * nnz;
     auto run16 = [&](const char* name, const int2* mt, int walk, const int4* bb, int G) {
@@ -809,7 +810,7 @@ int main(int argc, char** argv) {
         for (int r = 0; r < reps + 3; ++r) {
           if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
                                        reinterpret_cast<const double2*>(bx), pb + 8192);
-          hipExtLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, false, 1, true>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0,
+          hipExtLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, false, 1, true>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0,
                                 drp, dci, dva, mt, nb, walk, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, dc16, bb);
           CK(hipEventSynchronize(e1));
           float ms_;
@@ -825,11 +826,11 @@ int main(int argc, char** argv) {
     run16("C16 slab", ms, 2, dbs, gc);
     {  // rows bit-equal to the 32-bit columns
       std::vector<double> w1(n), w2(n);
-      hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4>), dim3(gr), dim3(kBlock), 0, s, drp, dci, dva, ms, nb, 2, dx, db,
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4>), dim3(gr), dim3(kBlock), 0, s, drp, dci, dva, ms, nb, 2, dx, db,
                          (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       CK(hipStreamSynchronize(s));
       CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
-      hipLaunchKernelGGL((spmv_pipe_kernel<kPipeCap, 4, false, 1, true>), dim3(gc), dim3(kBlock), 0, s, drp, dci, dva, ms,
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, false, 1, true>), dim3(gc), dim3(kBlock), 0, s, drp, dci, dva, ms,
                          nb, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, dc16, dbs);
       CK(hipStreamSynchronize(s));
       CK(hipMemcpy(w2.data(), dw, 8 * n, hipMemcpyDeviceToHost));
@@ -896,12 +897,12 @@ int main(int argc, char** argv) {
 #define CAPRUN(CAPV, MT, NB, G)                                                                                \
   snprintf(nm, sizeof nm, "dual cap%d grid=%d", CAPV, G);                                                      \
   run(nm, SD, [&] {                                                                                            \
-    hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
+    hipExtLaunchKernelGGL((spmv_pipe_var_kernel<CAPV, 4, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
                           dva, MT, NB, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                      \
   });                                                                                                          \
   snprintf(nm, sizeof nm, "K1 dot cap%d grid=%d", CAPV, G);                                                    \
   run(nm, S, [&] {                                                                                             \
-    hipExtLaunchKernelGGL((spmv_pipe_kernel<CAPV, 1, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
+    hipExtLaunchKernelGGL((spmv_pipe_var_kernel<CAPV, 1, false, 1>), dim3(G), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, \
                           dva, MT, NB, 1, dx, dQ, dw, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                                     \
   })
     for (int g : {1280, 2048}) { CAPRUN(512, m5, nb5, g); }
@@ -909,9 +910,9 @@ int main(int argc, char** argv) {
     for (int g : {512, 768, 1024, 1280}) { CAPRUN(2048, m2, nb2, g); }
 #undef CAPRUN
     {  // rows bit-equal across capacities (each row sum is left to right in every table)
-      hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, m1,
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, m1,
                          nb1, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
-      hipLaunchKernelGGL((spmv_pipe_kernel<2048, 4, false, 1>), dim3(768), dim3(kBlock), 0, s, drp, dci, dva, m2,
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<2048, 4, false, 1>), dim3(768), dim3(kBlock), 0, s, drp, dci, dva, m2,
                          nb2, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw2, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       CK(hipStreamSynchronize(s));
       std::vector<double> w1(n), w2(n);
@@ -998,7 +999,7 @@ int main(int argc, char** argv) {
 #define VAR(NAME, CAPV, NTV, WPEV, G)                                                                         \
   snprintf(nm, sizeof nm, "dual pipe walk=1 %s grid=%d", NAME, G);                                            \
   timeit(nm, 50, SD, [&] {                                                                                    \
-    hipLaunchKernelGGL((spmv_pipe_kernel<CAPV, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, drp, dci, dva, mt, \
+    hipLaunchKernelGGL((spmv_pipe_var_kernel<CAPV, 4, NTV, WPEV>), dim3(G), dim3(kBlock), 0, s, drp, dci, dva, mt, \
                        nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);                                  \
   })
       VAR("nt", 1024, true, 1, 1280);
@@ -1015,7 +1016,7 @@ int main(int argc, char** argv) {
         });
       }
       {  // pipe2 bit identity vs pipe at the same grid / walk
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
         hipLaunchKernelGGL((spmv_pipe2_kernel<1024, 4>), dim3(1024), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pc, dx2, dQ, dw2, pd);
@@ -1066,7 +1067,7 @@ int main(int argc, char** argv) {
         for (int g : {1024, 1280, 2560}) {
           snprintf(nm, sizeof nm, "dual pipe walk=1 grid=%d", g);
           cold(nm, SD, [&] {
-            hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
+            hipExtLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
                                   dci, dva, mt, nb, 1, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
           });
         }
@@ -1093,7 +1094,7 @@ int main(int argc, char** argv) {
         for (int g : {1024, 1280}) {
           snprintf(nm, sizeof nm, "K1 dot pipe walk=1 grid=%d", g);
           cold(nm, S, [&] {
-            hipExtLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
+            hipExtLaunchKernelGGL((spmv_pipe_var_kernel<1024, 1, false, 1>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp,
                                   dci, dva, mt, nb, 1, dx, dQ, dw, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
           });
           snprintf(nm, sizeof nm, "K1 dot pipe2 walk=1 grid=%d", g);
@@ -1107,24 +1108,24 @@ int main(int argc, char** argv) {
       }
       snprintf(nm, sizeof nm, "dual pipe walk=1 x2=x1 grid=1280");
       timeit(nm, 50, SD, [&] {
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "dual pipe walk=1 q0=b grid=1280");
       timeit(nm, 50, SD, [&] {
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 4, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pa, dx2, db, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "single pipe walk=1 ResNorm grid=1280");
       timeit(nm, 50, S, [&] {
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
       snprintf(nm, sizeof nm, "2x single pipe walk=1 (ResNorm + Dot) grid=1280");
       timeit(nm, 50, SD, [&] {
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 2, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx, db, (double*)nullptr, pa, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
-        hipLaunchKernelGGL((spmv_pipe_kernel<1024, 1, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
+        hipLaunchKernelGGL((spmv_pipe_var_kernel<1024, 1, false, 1>), dim3(1280), dim3(kBlock), 0, s, drp, dci, dva, mt,
                            nb, 1, dx2, dQ, dw, pb, dx, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
       });
 #undef VAR

@@ -16,24 +16,17 @@ from structurepreservingiterativesolvers_amd.device import get_context, set_opti
 from structurepreservingiterativesolvers_amd.swe import assembly  # noqa: E402
 
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 913
-modes = sys.argv[2:] or ["xcd", "stride", "xcd2", "stride2", "xcd_natural"]
+modes = sys.argv[2:] or ["xcd", "stride", "xcd_natural"]
 dic, _ = assembly.linforms(M=M)
 A = dic["A"]
 n, nnz = A.shape[0], A.nnz
 ctx = get_context(0)
 print(f"M={M} N={n:,} nnz={nnz:,}", flush=True)
 keys = [int(k) for k in os.environ.get("SPMV_SWEEP_KEYS", "1").split(",")]  # SPIS_OPT_SLAB_KEY values
-w4s = [int(k) for k in os.environ.get("SPMV_SWEEP_W4", "0").split(",")]  # SPIS_OPT_SPMV_W4 values
-tms = [int(k) for k in os.environ.get("SPMV_SWEEP_TM", "0").split(",")]  # SPIS_OPT_C16_TM values
-nts = [bool(int(k)) for k in os.environ.get("SPMV_SWEEP_NT", "0,1").split(",")]
-configs = [(m, nt, c16, key, w4, tm) for m in modes for nt in nts for c16 in (0, 2) for key in keys for w4 in w4s
-           for tm in tms if not (m.endswith("2") and (c16 or nt)) and not (tm and not c16)]
-for mode, nt, c16, key, w4, tm in configs:
+configs = [(m, c16, key) for m in modes for c16 in (0, 2) for key in keys]
+for mode, c16, key in configs:
     set_option("slab_key", key)
-    set_option("spmv_w4", w4)
-    set_option("c16_tm", tm)
     set_option("spmv_pipe", mode)
-    set_option("spmv_nt", nt)
     set_option("col16", {0: False, 2: True}[c16])
     from structurepreservingiterativesolvers_amd.device import DeviceMatrix
 
@@ -46,12 +39,9 @@ for mode, nt, c16, key, w4, tm in configs:
             v = C.c_double()
             _lib.check(ctx.L.spis_spmv_bench(ctx.handle, Ad.handle, kind, cold, 20, C.byref(v)), "bench")
             res.append(v.value)
-        print(f"{mode:12s} key={key} w4={w4} tm={tm} nt={int(nt)} col16={c16} {name:8s} warm {res[0]:8.1f} us {byt / res[0] / 1e3:7.0f} GB/s | "
+        print(f"{mode:12s} key={key} col16={c16} {name:8s} warm {res[0]:8.1f} us {byt / res[0] / 1e3:7.0f} GB/s | "
               f"cold {res[1]:8.1f} us {byt / res[1] / 1e3:7.0f} GB/s ({byt / res[1] / 1e3 / 8000:.3f})", flush=True)
     del Ad
 set_option("spmv_pipe", "auto")
 set_option("col16", "auto")
-set_option("spmv_nt", False)
 set_option("slab_key", True)
-set_option("spmv_w4", False)
-set_option("c16_tm", False)
