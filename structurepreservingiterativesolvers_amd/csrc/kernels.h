@@ -76,22 +76,14 @@ hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, co
 // K1d: residual SpMV of x1 (||A x1 - b||^2 partials -> part1) and Arnoldi SpMV of x2 (w = A x2,
 // q0.w partials -> part2) reading the matrix once; both bit-identical to launch_spmv's.  A must
 // carry the kDualCap row-block table; grid <= kSpmvGrid (the partial arrays' length)
-// the dual's optional extra epilogue dots: q1 . w and q2 . w partials (grid of each) for the MGS
-// chain that follows, which then starts with its first two exchanges done (K2q, chain j >= 3)
-struct DualDots {
-  const double* q1;
-  const double* q2;
-  double* part3;
-  double* part4;
-};
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
-                            hipStream_t s, const LaunchEv* ev = nullptr, const DualDots* dd = nullptr);
+                            hipStream_t s, const LaunchEv* ev = nullptr);
 // K1p / K1dp (A.blk_meta on a kPipeCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
 // part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi)
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev = nullptr, const DualDots* dd = nullptr);
+                            int grid, hipStream_t s, const LaunchEv* ev = nullptr);
 // y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,
@@ -119,10 +111,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator = false,
                             bool nt = false, double* gsub = nullptr, const double* yx_host = nullptr, int px = 0,
-                            const double* x0 = nullptr, double* xo = nullptr, const double* xd1 = nullptr,
-                            const double* xd2 = nullptr);
-// (xd1, xd2: K2q only, j >= 3 — the partials, n_in of each, of q_1 . w and q_2 . w from the dual
-// SpMV that produced w (DualDots); the chain then starts with h_1 and h_2 formed by its gatherer)
+                            const double* x0 = nullptr, double* xo = nullptr);
 // (nt: the chain's basis loads are nontemporal — the matrix stays Infinity-Cache resident)
 // gsub != nullptr selects K2q, the pipelined chain (dot products one MGS step early by the
 // distributive law; gsub[m] = q_m . q_{m-1}, written by chain m, read by the later chains of the
@@ -153,9 +142,17 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
 // nt: nontemporal basis loads (the matrix stays Infinity-Cache resident between SpMVs, as K2q's)
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
                            hipStream_t s, const LaunchEv* ev = nullptr, bool nt = false);
-// one workgroup: from those 2 nv - 1 dots (reduced, d), Gram row nv - 1 into G (kCgsMax x
-// kCgsMax), h_l = q_l . w - sum_{m<l} h_m G(l, m) in l order -> coef (device) and h_out (H column)
-hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s);
+// K2w's update: every workgroup first forms the coefficients from those 2 nv - 1 dots (reduced, d):
+// Gram row nv - 1 into G (kCgsMax x kCgsMax, by workgroup 0), h_l = q_l . w - sum_{m<l} h_m G(l, m)
+// in l order (h_out: the H column, by workgroup 0), then w -= Q h with the ||w'||^2 partials, and
+// with px > 0 the fused GEMV as launch_cgs_update; rpart (nullable): workgroup 0 also reduces a true
+// residual's r_in partials and publishes it as launch_finalize(rpart, r_in, r_out, 0, .., flag, seq)
+hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* d,
+                              double* G, double* h_out, double* part, int grid, hipStream_t s, bool nt = false,
+                              int px = 0, const double* yx = nullptr, const double* x0 = nullptr,
+                              double* xo = nullptr, int64_t n_gx = 0, const double* rpart = nullptr, int r_in = 0,
+                              double* r_out = nullptr, unsigned long long* flag = nullptr,
+                              const unsigned long long* seq = nullptr);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s, int zero_to = 0);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM

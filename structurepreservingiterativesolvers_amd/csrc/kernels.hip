@@ -306,15 +306,6 @@ struct PipeStage {
                           // stay in registers)
 };
 
-// MODE 5 (the dual SpMV for an MGS chain that takes its first two dots from it): w's dots with q1
-// and q2, per workgroup in the same order as q0's (part2)
-struct PipeXD {
-  const double* q1 = nullptr;
-  const double* q2 = nullptr;
-  double* part3 = nullptr;
-  double* part4 = nullptr;
-};
-
 // C16: column = base[k] + offset of a 16-bit entry (k = the top 2 bits)
 __device__ __forceinline__ int col16_decode(unsigned v, int b0, int b1, int b2, int b3) {
   const unsigned k = v >> 14;
@@ -382,27 +373,25 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 }
 
 // x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
-// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half (MODE 4); MODE 5 = 4 + q1.w and q2.w
-// partials (xd.part3, xd.part4) for the MGS chain that follows (K2q's E_1, E_2)
+// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half (MODE 4)
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
 // (variants measured and not adopted — nontemporal stream, 4 waves per SIMD, buffer descriptors,
 // thread-major columns, two-deep pipeline, SELL-64 — live in tools/spmv_variants.hip)
 template <int CAP, int MODE, bool C16 = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 5 ? 3 : 1, C16 ? 3 : 8))) void spmv_pipe_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ? 3 : 8))) void spmv_pipe_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base, PipeXD xd) {
-  constexpr bool DUAL = MODE >= 4;
-  constexpr bool XD = MODE == 5;
+    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
+  constexpr bool DUAL = MODE == 4;
   constexpr int kPer = PipeStage<CAP>::kPer;
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
   // of 16 entries (swe's edge rows) would otherwise put a wave's lanes 256 B apart, all in one
   // LDS bank group; the pad staggers them
   __shared__ typename std::conditional<DUAL, double2, double>::type s_p[CAP + CAP / 16];
   __shared__ double s_wave[4];
-  double pt1 = 0.0, pt2 = 0.0, pt3 = 0.0, pt4 = 0.0;
+  double pt1 = 0.0, pt2 = 0.0;
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
   const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
@@ -430,10 +419,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
           y2[r0] = s2;
           pt2 += aux2[r0] * s2;
         }
-        if (XD) {
-          pt3 += xd.q1[r0] * s2;
-          pt4 += xd.q2[r0] * s2;
-        }
         if (MODE == kEpiPlain) y1[r0] = s1;
         if (MODE == kEpiDot) { y1[r0] = s1; pt1 += aux1[r0] * s1; }
         if (MODE == kEpiResNorm) { const double t = s1 - aux1[r0]; pt1 += t * t; }
@@ -451,13 +436,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
       const int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
       g1[u] = x1[c];
       if (DUAL) g2[u] = x2[c];
-    }
-    // MODE 5: the row's q1 / q2 entries go out with the gathers (waited for with them, before the
-    // next block's loads are issued), not with the stage: in the stage they spilled
-    double xq1 = 0.0, xq2 = 0.0;
-    if (XD && cur.r0 + static_cast<int>(threadIdx.x) < cur.r1) {
-      xq1 = xd.q1[cur.r0 + threadIdx.x];
-      xq2 = xd.q2[cur.r0 + threadIdx.x];
     }
     nxt.nnz = 0;
     if (nb < b1) pipe_load<CAP, MODE, C16>(nxt, meta, nb, ms, rp, ci, c16, base, va, aux1, aux2);
@@ -535,10 +513,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
         y2[r] = s2;
         pt2 += cur.a2 * s2;
       }
-      if (XD) {
-        pt3 += xq1 * s2;
-        pt4 += xq2 * s2;
-      }
       if (MODE == kEpiPlain) y1[r] = s1;
       if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
       if (MODE == kEpiResNorm) { const double t = s1 - cur.a1; pt1 += t * t; }
@@ -555,51 +529,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
   }
   if (MODE != kEpiPlain) {
     const double tot1 = block_sum(pt1, s_wave);
-    double tot2 = 0.0, tot3 = 0.0, tot4 = 0.0;
+    double tot2 = 0.0;
     if (DUAL) tot2 = block_sum(pt2, s_wave);
-    if (XD) {
-      tot3 = block_sum(pt3, s_wave);
-      tot4 = block_sum(pt4, s_wave);
-    }
     if (threadIdx.x == 0) {
       part1[blockIdx.x] = tot1;
       if (DUAL) part2[blockIdx.x] = tot2;
-      if (XD) {
-        xd.part3[blockIdx.x] = tot3;
-        xd.part4[blockIdx.x] = tot4;
-      }
     }
   }
 }
 
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev, const DualDots* dd) {
+                            int grid, hipStream_t s, const LaunchEv* ev) {
   dim3 g(grid), b(kBlock);
-  PipeXD xd;
-  if (dd != nullptr) {
-    if (mode != 4 || dd->q1 == nullptr || dd->q2 == nullptr || dd->part3 == nullptr || dd->part4 == nullptr)
-      return hipErrorInvalidValue;
-    xd.q1 = dd->q1;
-    xd.q2 = dd->q2;
-    xd.part3 = dd->part3;
-    xd.part4 = dd->part4;
-    mode = 5;
-  }
 #define SPIS_PIPE(M)                                                                                            \
   if (A.col16 != nullptr)                                                                                       \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
-             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, xd);               \
+             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);               \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
-             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, xd)
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
     case 2: SPIS_PIPE(2); break;
     case 3: SPIS_PIPE(3); break;
-    case 4: SPIS_PIPE(4); break;
-    default: SPIS_PIPE(5); break;
+    default: SPIS_PIPE(4); break;
   }
 #undef SPIS_PIPE
   return hipGetLastError();
@@ -607,10 +562,9 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
 
 hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b, double* part1,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
-                            hipStream_t s, const LaunchEv* ev, const DualDots* dd) {
+                            hipStream_t s, const LaunchEv* ev) {
   if (A.blk_meta != nullptr)
-    return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev, dd);
-  if (dd != nullptr) return hipErrorInvalidValue;  // the unpipelined dual has no extra dots
+    return launch_spmv_pipe(A, 4, x1, b, nullptr, part1, x2, q0, w, part2, grid, s, ev);
   if (A.swz)
     launch_k(spmv_dual_kernel<kDualCap, 1>, dim3(grid), dim3(kBlock), 0, s, ev, A.indptr, A.indices, A.vals,
              A.blk_row, A.n_blk, x1, b, part1, x2, w, q0, part2);
@@ -1076,15 +1030,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo, const double* __restrict__ xd1,
-    const double* __restrict__ xd2, int n_xd) {
+    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
 #pragma clang fp contract(off)
   static_assert(LAG >= 1 && LAG <= 2 && NS >= LAG + 3, "ring: q_{i-1}, the dotted q_{i+LAG}, one loading");
-  // pre: E_1 and E_2's dots q_1.w, q_2.w came from the dual SpMV that produced w (MODE 5: per
-  // SpMV workgroup, n_xd partials each): the gatherer forms h_1, h_2 at once and the data
-  // workgroups neither compute nor publish them (j >= 3: neither is the newest vector's, which
-  // carries the Gram entries G(j, .))
-  const bool pre = LAG == 2 && xd1 != nullptr && j >= 3;
   constexpr int DT = DW * 64;  // data threads
   constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
   __shared__ double2 s_acc[FX ? PER * DT : 1];
@@ -1185,15 +1133,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         return all_ok;
       };
       double hm = 0.0;
-      bool ok = true;
-      if (pre && m <= 2) {  // a_m from the SpMV's partials: each lane its strided share, in order
-        const double* xp = m == 1 ? xd1 : xd2;
-        double acc = 0.0;
-        for (int t = lane; t < n_xd; t += 64) acc += xp[t];
-        hm = wave_sum_dpp(acc);
-      } else {
-        ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &hm);
-      }
+      bool ok = sweep(aslots + static_cast<size_t>(m & 3) * 2 * kChainMaxWG, &hm);
       if (m <= j) {
         // h_m = a_m - sum_{l = max(0, m-LAG)}^{m-1} h_l G(m, l), l ascending
         double gv[LAG];
@@ -1388,12 +1328,11 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     }
     // q_{i+NS-1} into the slot q_{i-1} just left
     if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
-    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well); pre: E_1 and
-    // E_2 are the gatherer's already
-    if (i == 0 && !pre) {
+    // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
+    if (i == 0) {
       if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
     }
-    if (i + LAG <= j && !(pre && i == 0)) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
+    if (i + LAG <= j) dots(std::integral_constant<int, (R + LAG) % NS>{}, i + LAG);
     // x += yx_i q_i (K4's order; x0 is added after the last coefficient), after this step's
     // partials are published: its LDS read-modify-write overlaps the exchange instead of
     // delaying the dots (q_i stays in slot R until the next step's update)
@@ -1629,8 +1568,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt,
-                            double* gsub, const double* yx_host, int px, const double* x0, double* xo,
-                            const double* xd1, const double* xd2) {
+                            double* gsub, const double* yx_host, int px, const double* x0, double* xo) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
   // K2q counts (n + 1) / 2 pairs (an odd n's last pair padded): its fallback test must too
@@ -1675,8 +1613,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
 #define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
   launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
-           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo,     \
-           xd1, xd2, n_in)
+           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo)
 #define SPIS_LAG_PER(FX_, NT_, LAG_)          \
   switch (per) {                              \
     case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \
@@ -1837,21 +1774,86 @@ __global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double
 // through LDS in wave order, then + x0; rows [n, n_gx) (x's ghost rows, from the basis vectors'
 // ghost entries) by the same arithmetic one row per thread, so a rank's ghost copy of x equals its
 // owner's bitwise and x needs no halo exchange
-template <int DOT, bool NT = false, bool FX = false>
+// K2w's coefficients, formed by every update workgroup before its pass (COEF; the separate
+// one-workgroup launch and its gap are gone): from the 2 nv - 1 reduced dots d, Gram row nv - 1
+// (to G by workgroup 0: rows < nv - 1 were written by the earlier steps of this solve), then
+// h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l order -> s_c, and workgroup 0 writes the
+// host H column.  The Gram triangle is staged in LDS (packed: row i at i (i - 1) / 2), and the
+// forward substitution runs column by column on one wave: lane i holds t_i and, once h_l = t_l is
+// broadcast, subtracts h_l G(i, l) — for every i the same subtractions in the same l order as the
+// row-by-row recurrence, so every workgroup forms the same bits.  (Thread 0 running the recurrence
+// with h[] in private memory took 17 us per step: the dynamically indexed array lived in scratch.)
+struct CoefArg {
+  const double* d;  // nullptr: coef holds the coefficients already
+  double* G;        // kCgsMax x kCgsMax, row-major
+  double* h_out;    // the host H column (nullable)
+  // (nullable) a true residual's partials, reduced and published by workgroup 0 as finalize_kernel
+  // does (the residual that rode the dots' all-reduce; one launch fewer per Arnoldi step)
+  const double* rpart;
+  int r_in;
+  double* r_out;
+  unsigned long long* flag;
+  const unsigned long long* seq;
+};
+constexpr int kGramTri = kCgsMax * (kCgsMax - 1) / 2;
+
+__device__ __forceinline__ void icwy_coefficients(const CoefArg ca, int nv, double* s_c, double* s_gt, double* s_d) {
+#pragma clang fp contract(off)
+  static_assert(kCgsMax <= 64, "one lane per coefficient");
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const bool writer = blockIdx.x == 0;
+  for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = ca.d[i];
+  for (int i = 1 + wid; i < nv - 1; i += kBlock / 64)
+    if (lane < i) s_gt[i * (i - 1) / 2 + lane] = ca.G[static_cast<int64_t>(i) * kCgsMax + lane];
+  __syncthreads();
+  const int nr = (nv - 1) * (nv - 2) / 2;  // the newest row, to LDS and (workgroup 0) to G
+  for (int l = threadIdx.x; l < nv - 1; l += kBlock) {
+    s_gt[nr + l] = s_d[nv + l];
+    if (writer) ca.G[static_cast<int64_t>(nv - 1) * kCgsMax + l] = s_d[nv + l];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    const double* gi = s_gt + (i > 0 ? i * (i - 1) / 2 : 0);
+    double t = i < nv ? s_d[i] : 0.0;
+    for (int l = 0; l + 1 < nv; ++l) {
+      const double hl = __shfl(t, l, 64);  // h_l: t_l is final once columns 0 .. l-1 are applied
+      if (i > l && i < nv) t -= hl * gi[l];
+    }
+    if (i < nv) {
+      s_c[i] = t;
+      if (writer && ca.h_out != nullptr) ca.h_out[i] = t;
+    }
+  }
+  __syncthreads();
+}
+
+template <int DOT, bool NT = false, bool FX = false, bool COEF = false>
 __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* __restrict__ w,
                                                             const double* __restrict__ Q, int64_t pitch, int nv,
                                                             const double* __restrict__ coef,
                                                             double* __restrict__ part, int px, YArg yx,
                                                             const double* __restrict__ x0, double* __restrict__ xo,
-                                                            int64_t n_gx) {
+                                                            int64_t n_gx, CoefArg ca) {
   __shared__ double s_c[kCgsMax];
   __shared__ double s_sum[4][4][64];  // [wave][element slot][lane]
   __shared__ double s_x[FX ? 4 : 1][4][64];
   __shared__ double s_wave[4];
+  __shared__ double s_gt[COEF ? kGramTri : 1];
+  __shared__ double s_d[COEF ? 2 * kCgsMax : 1];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x < nv) s_c[threadIdx.x] = coef[threadIdx.x];
-  __syncthreads();
+  if (COEF) {
+    icwy_coefficients(ca, nv, s_c, s_gt, s_d);
+    if (ca.rpart != nullptr && blockIdx.x == 0) {
+      const double t = sum_partials(ca.rpart, ca.r_in, s_wave);
+      if (threadIdx.x == 0) publish(ca.r_out, t, ca.flag, ca.seq);
+    }
+  } else {
+    if (threadIdx.x < nv) s_c[threadIdx.x] = coef[threadIdx.x];
+    __syncthreads();
+  }
   double acc[kCgsPerWave];
 #pragma unroll
   for (int m = 0; m < kCgsPerWave; ++m) acc[m] = 0.0;
@@ -2021,9 +2023,27 @@ hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t p
   return hipGetLastError();
 }
 
-hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
-                             bool dot, double* part, int grid, hipStream_t s, bool nt, int px, const double* yx,
-                             const double* x0, double* xo, int64_t n_gx) {
+template <bool NT, bool FX, bool COEF>
+static void launch_update0(int grid, hipStream_t s, int64_t n, double* w, const double* Q, int64_t pitch, int nv,
+                           const double* coef, double* part, int px, const YArg& ya, const double* x0, double* xo,
+                           int64_t n_gx, const CoefArg& ca) {
+  hipLaunchKernelGGL((cgs_update_kernel<0, NT, FX, COEF>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
+                     part, px, ya, x0, xo, n_gx, ca);
+}
+
+template <bool NT, bool FX>
+static void launch_update0c(bool cf, int grid, hipStream_t s, int64_t n, double* w, const double* Q, int64_t pitch,
+                            int nv, const double* coef, double* part, int px, const YArg& ya, const double* x0,
+                            double* xo, int64_t n_gx, const CoefArg& ca) {
+  if (cf)
+    launch_update0<NT, FX, true>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+  else
+    launch_update0<NT, FX, false>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+}
+
+static hipError_t cgs_update_any(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
+                                 bool dot, double* part, int grid, hipStream_t s, bool nt, int px, const double* yx,
+                                 const double* x0, double* xo, int64_t n_gx, const CoefArg& ca) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
   YArg ya;
   const bool fx = px > 0;
@@ -2032,22 +2052,36 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
       return hipErrorInvalidValue;
     for (int i = 0; i < px; ++i) ya.v[i] = yx[i];
   }
+  const bool cf = ca.d != nullptr;
+  if (cf && (dot || ca.G == nullptr)) return hipErrorInvalidValue;
   if (dot)
     hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
-                       x0, xo, n_gx);
+                       x0, xo, n_gx, ca);
   else if (fx && nt)
-    hipLaunchKernelGGL((cgs_update_kernel<0, true, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
-                       part, px, ya, x0, xo, n_gx);
+    launch_update0c<true, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
   else if (fx)
-    hipLaunchKernelGGL((cgs_update_kernel<0, false, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
-                       part, px, ya, x0, xo, n_gx);
+    launch_update0c<false, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
   else if (nt)
-    hipLaunchKernelGGL((cgs_update_kernel<0, true>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part,
-                       0, ya, x0, xo, n_gx);
+    launch_update0c<true, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca);
   else
-    hipLaunchKernelGGL(cgs_update_kernel<0>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
-                       x0, xo, n_gx);
+    launch_update0c<false, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca);
   return hipGetLastError();
+}
+
+hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
+                             bool dot, double* part, int grid, hipStream_t s, bool nt, int px, const double* yx,
+                             const double* x0, double* xo, int64_t n_gx) {
+  return cgs_update_any(n, w, Q, pitch, nv, coef, dot, part, grid, s, nt, px, yx, x0, xo, n_gx,
+                        CoefArg{nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr});
+}
+
+hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* d,
+                              double* G, double* h_out, double* part, int grid, hipStream_t s, bool nt, int px,
+                              const double* yx, const double* x0, double* xo, int64_t n_gx, const double* rpart,
+                              int r_in, double* r_out, unsigned long long* flag, const unsigned long long* seq) {
+  if (d == nullptr || (rpart != nullptr && (r_in < 1 || r_out == nullptr))) return hipErrorInvalidValue;
+  return cgs_update_any(n, w, Q, pitch, nv, nullptr, false, part, grid, s, nt, px, yx, x0, xo, n_gx,
+                        CoefArg{d, G, h_out, rpart, r_in, r_out, flag, seq});
 }
 
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
@@ -2135,43 +2169,6 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
   }
 }
 
-// one workgroup: the 2 nv - 1 dots (already reduced: one value each), the newest Gram row into G
-// (row-major kCgsMax x kCgsMax; rows < nv - 1 were written by the earlier steps of this solve),
-// then h_l = ((q_l . w - h_0 G(l, 0)) - h_1 G(l, 1)) - ... in l order -> coef (device, cgs_update's
-// input) and h_out (the host H column).  The Gram triangle is staged in LDS, and the forward
-// substitution runs column by column on one wave: lane i holds t_i and, once h_l = t_l is
-// broadcast, subtracts h_l G(i, l) — for every i the same subtractions in the same m order as the
-// row-by-row recurrence, so the same bits.  (Thread 0 running the recurrence with h[] in private
-// memory took 17 us per step: the dynamically indexed array lived in scratch.)
-__global__ __launch_bounds__(kBlock) void icwy_coef_kernel(const double* __restrict__ d, int nv,
-                                                           double* __restrict__ G, double* __restrict__ coef,
-                                                           double* __restrict__ h_out) {
-#pragma clang fp contract(off)
-  static_assert(kCgsMax <= 64, "one lane per coefficient");
-  __shared__ double s_g[kCgsMax * kCgsMax];
-  __shared__ double s_d[2 * kCgsMax];
-  for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = d[i];
-  for (int i = threadIdx.x; i < (nv - 1) * kCgsMax; i += kBlock) s_g[i] = G[i];
-  __syncthreads();
-  for (int i = threadIdx.x; i < nv - 1; i += kBlock) {  // the newest row, to LDS and to G
-    s_g[(nv - 1) * kCgsMax + i] = s_d[nv + i];
-    G[static_cast<int64_t>(nv - 1) * kCgsMax + i] = s_d[nv + i];
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const int i = threadIdx.x;
-    double t = i < nv ? s_d[i] : 0.0;
-    for (int l = 0; l + 1 < nv; ++l) {
-      const double hl = __shfl(t, l, 64);  // h_l: t_l is final once columns 0 .. l-1 are applied
-      if (i > l && i < nv) t -= hl * s_g[i * kCgsMax + l];
-    }
-    if (i < nv) {
-      coef[i] = t;
-      h_out[i] = t;
-    }
-  }
-}
-
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
                            hipStream_t s, const LaunchEv* ev, bool nt) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
@@ -2179,12 +2176,6 @@ hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t 
     launch_k(icwy_dot_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
   else
     launch_k(icwy_dot_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
-  return hipGetLastError();
-}
-
-hipError_t launch_icwy_coef(const double* d, int nv, double* G, double* coef, double* h_out, hipStream_t s) {
-  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(icwy_coef_kernel, dim3(1), dim3(kBlock), 0, s, d, nv, G, coef, h_out);
   return hipGetLastError();
 }
 

@@ -101,8 +101,6 @@ struct spis_context {
   double* partA = nullptr;  // reduction partials, ping
   double* partB = nullptr;  // reduction partials, pong
   double* partR = nullptr;  // true-residual partials
-  double* partC = nullptr;  // q1.w partials of a dual SpMV feeding a K2q chain (DualDots)
-  double* partD = nullptr;  // q2.w partials
   double* dscal = nullptr;  // small device scalars (kMaxK + 8)
   double* pinned = nullptr;  // pinned, device-mapped host staging (kernels write h / partials here)
   double* pinned_dev = nullptr;  // the same memory as seen from the device
@@ -512,8 +510,6 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     const int np = std::max(kSpmvGrid, kRedGrid);
     HIP_TRY(hipMalloc(&c->partA, sizeof(double) * np));
     HIP_TRY(hipMalloc(&c->partB, sizeof(double) * np));
-    HIP_TRY(hipMalloc(&c->partC, sizeof(double) * np));
-    HIP_TRY(hipMalloc(&c->partD, sizeof(double) * np));
     // partR lives behind the one-reduce MGS's dot vector (icwy_d): on several GPUs the residual
     // partials then ride in the same all-reduce as the dots (arnoldi_post_icwy)
     HIP_TRY(hipMalloc(&c->dscal, sizeof(double) * (kMaxK + 8)));
@@ -586,8 +582,6 @@ extern "C" int spis_context_destroy(spis_context* c) {
     for (auto& kv : c->live_blocks) (void)hipFree(kv.first);
     (void)hipFree(c->partA);
     (void)hipFree(c->partB);
-    (void)hipFree(c->partC);
-    (void)hipFree(c->partD);
     (void)hipFree(c->dscal);
     (void)hipFree(c->cgs_part);
     (void)hipFree(c->cgs_c);
@@ -1855,24 +1849,9 @@ struct Solver {
   }
 
   double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
-  // the dual SpMV feeding A_ja's chain also forms q_1.w and q_2.w (MODE 5, DualDots) when that
-  // chain is a K2q one that can start from them (single GPU, pipelined SpMV table, ja >= 3): the
-  // chain's first two exchanges are then done before it starts
-  int xd_for = -1;  // the Arnoldi step whose chain the last dual SpMV computed E_1, E_2 for
-  bool xd_ok(int ja) const {
-    return ja >= 3 && c->mgs_chain == 3 && !c->cgs2 && !fixed_grid(c) && k2q_fits() && !icwy_on() &&
-           A->dual_view().blk_meta != nullptr;
-  }
   int launch_dual(int j, int ja, const double* bvec, const LaunchEv* le) {
-    const CsrView v = A->dual_view();
-    if (xd_ok(ja)) {
-      const DualDots dd{Qv(1), Qv(2), c->partC, c->partD};
-      HIP_TRY(launch_spmv_dual(v, xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream, le, &dd));
-      xd_for = ja;
-    } else {
-      HIP_TRY(launch_spmv_dual(v, xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream, le));
-      xd_for = -1;
-    }
+    HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream,
+                             le));
     return SPIS_OK;
   }
   // rows the update GEMV computes.  Several GPUs: n + n_ghost.  Every basis vector z_l's ghost
@@ -1986,11 +1965,9 @@ struct Solver {
       const LaunchEv both{e_first.start, e_last.stop};
       if (lag_chain()) arm_hcol(j);
       const int px = (gsub && yx) ? jx + 1 : 0;
-      const bool xd = gsub != nullptr && xd_for == j;  // E_1, E_2 from the dual SpMV (DualDots)
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
                                c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub, yx, px,
-                               ws->x0, px > 0 ? xbuf(jx) : nullptr, xd ? c->partC : nullptr,
-                               xd ? c->partD : nullptr));
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr));
       return SPIS_OK;
     }
     if (yx) return fail(SPIS_ERR_STATE, "fused update GEMV without the pipelined chain");
@@ -2024,36 +2001,33 @@ struct Solver {
     if (icwy_lag()) arm_hcol(j);
     // U_{j-2}'s residual (L mode): partials all-reduced, then reduced and published.  On several
     // GPUs partR sits right behind the dot vector d, so one all-reduce carries both (3 collectives
-    // per Arnoldi step instead of 4); the residual is then published after the dot pass
-    // (one rank takes the same order, the all-reduce being the identity: the self-halo test covers it)
+    // per Arnoldi step instead of 4).  Either way the residual is reduced and published by the
+    // update kernel's workgroup 0, after the dot pass (no finalize launch: the host's next need is
+    // H[:, j], published at the end of this step; one rank takes the merged order, the all-reduce
+    // being the identity: the self-halo test covers it)
     const bool merged = xpart != nullptr && xpart == c->partR && c->comm != nullptr;
-    if (xpart && !merged) {
-      ST_TRY(allreduce(c, const_cast<double*>(xpart), gs));
-      HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
-    }
+    if (xpart && !merged) ST_TRY(allreduce(c, const_cast<double*>(xpart), gs));
     const int nv = j + 1;
     double* hcol = c->pinned_dev + hoff(j);
     const int gc = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 63) / 64)));
     ProfEv pm(c, SPIS_PROF_MGS);
     const LaunchEv e_first = pm.first(), e_last = pm.last();
     double* d = c->icwy_d;
-    double* coef = c->cgs_c;
     const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
     HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt));
     // (merged: the slack between the dots and partR is zeroed, since the all-reduce sums it too)
     HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s, merged ? kIcwyROff : 0));
     if (merged) {
-      ST_TRY(allreduce(c, d, kIcwyROff + gs));  // [d | slack | partR]
-      HIP_TRY(launch_finalize(xpart, gs, x_out, 0, s, nullptr, flag, seq));
+      ST_TRY(allreduce(c, d, kIcwyROff + gs));  // [d | slack | partR]; partR reduced by the update
     } else {
       ST_TRY(allreduce(c, d, 2 * nv - 1));
     }
-    HIP_TRY(launch_icwy_coef(d, nv, c->icwy_G, coef, hcol, s));
-    // L mode: U_jx's GEMV in the same pass (x_jx = Z y + x0 over the local and ghost rows)
+    // the coefficients h (and H[0..j, j]) in the update's prologue; L mode: U_jx's GEMV in the same
+    // pass (x_jx = Z y + x0 over the local and ghost rows)
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
     if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
-    HIP_TRY(launch_cgs_update(n, ws->w, Qv(0), ws->pitch, nv, coef, false, c->partB, gc, s, nt, px, yx, ws->x0,
-                              px > 0 ? xbuf(jx) : nullptr, n_gx()));
+    HIP_TRY(launch_icwy_update(n, ws->w, Qv(0), ws->pitch, nv, d, c->icwy_G, hcol, c->partB, gc, s, nt, px, yx,
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr, n_gx(), xpart, gs, x_out, flag, seq));
     // ||w'||^2: the gc partials all-reduced element-wise (8 KB, latency-bound like one double) and
     // summed in fixed order by every normalize workgroup: no finalize launch in between
     ST_TRY(allreduce(c, c->partB, gc));
@@ -2095,7 +2069,6 @@ struct Solver {
       ProfEv ps(c, SPIS_PROF_SPMV);
       const LaunchEv le = ps.both();
       HIP_TRY(launch_spmv(A->dual_view(), kEpiDot, Zv(j), ws->w, Qv(0), c->partA, gs, c->stream, &le));
-      xd_for = -1;
     }
     return with_chain ? arnoldi_post(j) : SPIS_OK;
   }

@@ -192,7 +192,7 @@ def test_one_reduce_mgs_equals_mgs():
     dots q_l.w and the Gram rows G(l, m) = q_l.q_m is MGS's h (solvers.py:193-195) in exact
     arithmetic; in floating point, on an MGS basis, the two agree to roundoff and the updated
     vector is orthogonal to the basis as MGS's is.  A NumPy restatement of the formula (the
-    order of the correction terms as icwy_coef_kernel)."""
+    order of the correction terms as the update kernel's coefficient prologue, icwy_coefficients)."""
     rng = np.random.default_rng(5)
     n, k = 4000, 30
     A = np.diag(np.linspace(1, 10, n)) + 0.01 * rng.normal(size=(n, n)) / np.sqrt(n)
@@ -312,7 +312,7 @@ def _solve_worker(rank, world, port, out_q):
             if xj is not None:
                 res_hist.append(float(np.sqrt(red[-1])))
             h = np.zeros(j + 1)
-            for l in range(j + 1):  # icwy_coef: corrections in l order
+            for l in range(j + 1):  # icwy_coefficients: corrections in l order
                 t = d[l]
                 for m in range(l):
                     t -= h[m] * G[l, m]

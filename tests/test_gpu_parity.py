@@ -918,7 +918,7 @@ def test_full_size_lkdv_c2_vs_oracle(spis):
         assert np.linalg.norm(xs[i] - xrs[i]) <= tol_i * np.linalg.norm(xrs[i]), (i, tol_i)
     r0 = np.linalg.norm(dic["b"] - A @ x0)
     for i in range(len(rr)):
-        assert abs(r[i] - rr[i]) <= 1e-10 * r0 + 1e-8 * rr[i] + 10 * renv[i + 1] + 2 * rsl[i + 1], (i, r[i], rr[i])
+        assert abs(r[i] - rr[i]) <= 1e-10 * r0 + 1e-8 * rr[i] + 10 * renv[i] + 2 * rsl[i + 1], (i, r[i], rr[i])
     _assert_invariants(cons, x)
     np.testing.assert_allclose(d["res"][-1], np.linalg.norm(A @ x - dic["b"]), rtol=1e-10)
 

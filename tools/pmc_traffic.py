@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 BENCH_SPMV = 22  # spis_spmv_bench launches per (kind, cold): 2 untimed + 20 (bench.py)
 MGS_KERNELS = ("mgs_chain_lag_kernel", "mgs_chain_big_kernel", "mgs_chain_kernel", "icwy_dot_kernel",
-               "icwy_coef_kernel", "cgs_finalize_kernel", "cgs_update_kernel", "normalize_kernel", "mgs_step_kernel")
+               "cgs_finalize_kernel", "cgs_update_kernel", "normalize_kernel", "mgs_step_kernel")
 
 
 def _rows(path, counter):
