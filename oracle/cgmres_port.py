@@ -180,8 +180,12 @@ def _slsqp(func, y0, jac, cons, ftol):
                         options={"ftol": ftol, "maxiter": 1e3})
 
 
-def cgmres(A, b, x0, k, tol=1e-8, contol=10, conlist=[], pre=None, timing=None, trace=None):
-    """``solvers.py:131-323`` (constrained FGMRES)."""
+def cgmres(A, b, x0, k, tol=1e-8, contol=10, conlist=[], pre=None, timing=None, trace=None, diag=None):
+    """``solvers.py:131-323`` (constrained FGMRES).
+
+    diag (test diagnostics, optional dict): per constrained step j, the signed checker value of
+    SLSQP's solution, each reduced constraint's magnitude at it (|term0| + |term1 y| + |y term2 y|:
+    the scale its rounding lives on) and SLSQP's message; no effect on the computation."""
     ctol = 1e-12
     if timing:
         stamps = {"start": _time.time(), "start_iter": [], "end_iter": [],
@@ -224,6 +228,11 @@ def cgmres(A, b, x0, k, tol=1e-8, contol=10, conlist=[], pre=None, timing=None, 
                     if np.isnan(max(sol.x)):
                         raise ValueError
                 safety = True
+                if diag is not None:
+                    ct = [ConstraintTerms(c, x0, Z) for c in conlist]
+                    diag[j] = {"violation": constraint_checker(sol.x, eq), "message": sol.message,
+                               "scales": [abs(t.term0) + abs(t.term1 @ sol.x) + abs(sol.x @ t.term2 @ sol.x)
+                                          if t.reduced else float("nan") for t in ct]}
                 if not timing:
                     if constraint_checker(sol.x, eq) > ctol:
                         safety = False

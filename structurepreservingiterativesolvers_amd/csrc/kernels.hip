@@ -39,18 +39,26 @@ __device__ __forceinline__ double block_sum(double v, double* s_wave) {
   return t;
 }
 
-// One thread hands a value to the host: value store, system-scope release, then the flag (the
-// host spins on flag >= seq, then reads the value).  A single writer with a release between the
-// two stores is what makes the value visible first; the release's L2 write-back stalls only this
-// wave.  Without a flag, a plain store (the caller synchronises through an event).
+// One 8-B system-scope store into mapped host memory: a host spinning on the slot sees the value
+// whole, and needs no fence or separate flag.  The host arms every such slot with a
+// signalling-NaN sentinel no kernel writes before the launch that fills it (spis.cpp kHSentinel),
+// so the value is its own flag.  (Round 3 stored the value, released with __threadfence_system()
+// and then stored a sequence flag: the fence's L2 write-back stalled the publishing wave by
+// microseconds, on the critical path of every chain and K2w update that carries a residual.)
+__device__ __forceinline__ void pin_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// a residual handed to the host: flag != nullptr marks a host-spun slot (pin_store; flag and seq
+// are no longer written); without a flag, a plain store (the caller synchronises through an event)
 __device__ __forceinline__ void publish(double* out, double v, unsigned long long* flag,
                                         const unsigned long long* seq) {
-  *out = v;
-  if (flag != nullptr) {
-    const unsigned long long sq = *seq;  // written by the host before the launch (graph replays)
-    __threadfence_system();
-    __hip_atomic_store(flag, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  (void)seq;
+  if (flag != nullptr)
+    pin_store(out, v);
+  else
+    *out = v;
 }
 
 // every workgroup reduces the same partial array in the same order -> the same scalar
@@ -859,7 +867,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
   }
   if (tid == 0) s_fail = 0;
   double h = chain_sum_partials(part_in, n_in, s_wave);
-  if (blockIdx.x == 0 && tid == 0) hcol[0] = h;
+  if (blockIdx.x == 0 && tid == 0) pin_store(hcol, h);
   if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
     const double t = chain_sum_partials(xpart, n_x, s_wave);
     if (tid == 0) publish(x_out, t, flag, seq);
@@ -970,7 +978,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
     if (s_fail) break;  // uniform: a workgroup never arrived; the host reports it
     if (!last) {
       h = hn;
-      if (blockIdx.x == 0 && tid == 0) hcol[i + 1] = hn;
+      if (blockIdx.x == 0 && tid == 0) pin_store(hcol + i + 1, hn);
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         U[k] = D[k];
@@ -980,7 +988,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void mgs_chain_kernel(
       dt = pt;
     } else {  // K3: h_{j+1,j} = ||y||, q_{j+1} = y / h (zeros on breakdown, as normalize_kernel)
       const double hh = sqrt(hn);
-      if (blockIdx.x == 0 && tid == 0) hcol[j + 1] = hh;
+      if (blockIdx.x == 0 && tid == 0) pin_store(hcol + j + 1, hh);
       double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
@@ -1092,9 +1100,9 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   if (agg) {  // ---- the gatherer: one wave sums, forms h_m and publishes it
     if (tid >= 64) return;
     const int lane = tid;
-    // the whole column H[:, j] is written by this lane; H[j+1, j] last, behind a system-scope
-    // release, so a host that sees it (the solver's L mode, spis.cpp) sees the column
-    if (lane == 0) hcol[0] = h0;
+    // the whole column H[:, j] is written by this lane, each entry one system-scope store into a
+    // slot the host armed (the solver's L mode, spis.cpp, waits for every slot of the column)
+    if (lane == 0) pin_store(hcol, h0);
     double hl[LAG];  // h_{m-LAG} .. h_{m-1} (hl[LAG-1] = h_{m-1})
 #pragma unroll
     for (int l = 0; l < LAG; ++l) hl[l] = 0.0;
@@ -1165,14 +1173,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
         unsigned long long* hs = hslots + 2 * (m & 3);
         chain_store(hs, tag, static_cast<unsigned>(bits));
         chain_store(hs + 1, tag, static_cast<unsigned>(bits >> 32));
-        if (m <= j) {
-          hcol[m] = hm;
-        } else {
-          __threadfence_system();
-          __hip_atomic_store(reinterpret_cast<unsigned long long*>(hcol + m),
-                             static_cast<unsigned long long>(__double_as_longlong(sqrt(hm))), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        pin_store(hcol + m, m <= j ? hm : sqrt(hm));  // every slot armed: no order needed
       }
       if (lane == 0) CHAIN_TR(2, 2 + m);
       if (!ok) return;
@@ -1470,7 +1471,7 @@ __global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
   double yt = tail ? w[n - 1] : 0.0;
   if (tid == 0) s_fail = 0;
   double h = chain_sum_partials(part_in, n_in, s_wave);
-  if (blockIdx.x == 0 && tid == 0) hcol[0] = h;
+  if (blockIdx.x == 0 && tid == 0) pin_store(hcol, h);
   if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
     const double t = chain_sum_partials(xpart, n_x, s_wave);
     if (tid == 0) publish(x_out, t, flag, seq);
@@ -1546,10 +1547,10 @@ __global__ __launch_bounds__(kBigThreads, 1) void mgs_chain_big_kernel(
     if (s_fail) break;  // uniform: a workgroup never arrived; the host reports it
     if (!last) {
       h = hn;
-      if (blockIdx.x == 0 && tid == 0) hcol[i + 1] = hn;
+      if (blockIdx.x == 0 && tid == 0) pin_store(hcol + i + 1, hn);
     } else {  // K3: h_{j+1,j} = ||y||, q_{j+1} = y / h (zeros on breakdown)
       const double hh = sqrt(hn);
-      if (blockIdx.x == 0 && tid == 0) hcol[j + 1] = hh;
+      if (blockIdx.x == 0 && tid == 0) pin_store(hcol + j + 1, hh);
       const __amdgpu_buffer_rsrc_t rq = vec_rsrc(Q + static_cast<int64_t>(j + 1) * pitch, vbytes);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
@@ -1673,10 +1674,7 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
   for (int u = 0; u < kMgsPer; ++u)
     if (base + u * kBlock < npair) yv[u] = y2[base + u * kBlock];
   const double h = sqrt(sum_partials(part_in, n_in, s_wave));
-  if (blockIdx.x == 0 && threadIdx.x == 0)  // one 8-B system-scope store: a host spinning on the
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(h_out),  // slot sees it whole
-                       static_cast<unsigned long long>(__double_as_longlong(h)), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (blockIdx.x == 0 && threadIdx.x == 0) pin_store(h_out, h);  // a host spinning on the slot sees it whole
   // breakdown (h == 0): cgmres/gmres stop (solvers.py:199-202); cgmres_p carries on with the
   // q[j+1] row it never wrote, i.e. zeros (solvers.py:172,376-377) — reproduce that here
   while (base - threadIdx.x < npair) {
@@ -1823,7 +1821,7 @@ __device__ __forceinline__ void icwy_coefficients(const CoefArg ca, int nv, doub
     }
     if (i < nv) {
       s_c[i] = t;
-      if (writer && ca.h_out != nullptr) ca.h_out[i] = t;
+      if (writer && ca.h_out != nullptr) pin_store(ca.h_out + i, t);
     }
   }
   __syncthreads();

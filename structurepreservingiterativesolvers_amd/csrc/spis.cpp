@@ -1843,9 +1843,11 @@ struct Solver {
   const unsigned long long* seq_dev(int j) const {
     return reinterpret_cast<const unsigned long long*>(c->pinned_dev + seq_off(j));
   }
-  void next_seq(int j) {  // the kernel that publishes U_j reads its seq from pinned memory
+  void next_seq(int j) {  // before the launch that publishes U_j's residual: arm its slot
     upd_seq[j & 1] = ++c->seq;
     *reinterpret_cast<volatile unsigned long long*>(c->pinned + seq_off(j)) = upd_seq[j & 1];
+    // the host read U_{j-2}'s residual from this slot before U_j's producer is enqueued
+    *reinterpret_cast<volatile uint64_t*>(c->pinned + roff(j)) = kHSentinel;
   }
 
   double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
@@ -1889,12 +1891,16 @@ struct Solver {
     return c->comm ? c->dist_mgs == 1 : (c->mgs_chain == 4 || (c->mgs_chain == 3 && !c->cgs2 && !k2q_fits()));
   }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
-  void arm_hcol(int j) {  // before A_j's chain is enqueued
-    *reinterpret_cast<volatile uint64_t*>(c->pinned + hoff(j) + j + 1) = kHSentinel;
+  void arm_hcol(int j) {  // before A_j's chain is enqueued: every slot of H[:, j] (pin_store)
+    for (int i = 0; i <= j + 1; ++i) *reinterpret_cast<volatile uint64_t*>(c->pinned + hoff(j) + i) = kHSentinel;
   }
   // true once H[:, j] is complete; false if the stream drained without it (a failed chain)
   int wait_hcol(int j, bool* ok) const {
-    return wait_slot(reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + j + 1), ok);
+    // H[j+1, j] is written last in stream order; each entry is its own flag (no ordering between
+    // the kernels' system-scope stores), so every slot is checked
+    ST_TRY(wait_slot(reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + j + 1), ok));
+    for (int i = 0; i <= j && *ok; ++i) ST_TRY(wait_slot(reinterpret_cast<const uint64_t*>(c->pinned + hoff(j) + i), ok));
+    return SPIS_OK;
   }
   // spin until a pinned 8-B slot leaves kHSentinel; false if the stream drained first
   int wait_slot(const uint64_t* w, bool* ok) const {
@@ -2192,24 +2198,14 @@ struct Solver {
     return arnoldi_post(ja, c->partR, c->pinned_dev + roff(j), flag_dev(), seq_dev(j));
   }
 
-  // host wait for U_j (which also covers every earlier launch on the stream)
+  // host wait for U_j's residual (which also covers every earlier launch on the stream: its
+  // producer starts after them).  The slot was armed by next_seq(j) and is written whole by one
+  // system-scope store (kernels.hip pin_store)
   int wait_update(int j) const {
-    const unsigned long long want = upd_seq[j & 1];
-    const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(c->pinned + flag_off());
-    // a failed launch must not leave the host spinning forever, but hipStreamQuery enqueues a
-    // marker packet (~5 us of GPU time before the next kernel, seen after every MGS chain when it
-    // ran every 1024 spins): query only once the wait has lasted 20 ms
-    const double t0 = now_s();
-    for (unsigned spin = 0;; ++spin) {
-      if (__atomic_load_n(fl, __ATOMIC_ACQUIRE) >= want) return SPIS_OK;
-      if ((spin & 4095) == 4095 && now_s() - t0 > 0.02) {
-        const hipError_t e = hipStreamQuery(c->stream);
-        if (e != hipSuccess && e != hipErrorNotReady) return fail(SPIS_ERR_HIP, "stream: %s", hipGetErrorString(e));
-        if (e == hipSuccess && __atomic_load_n(fl, __ATOMIC_ACQUIRE) < want)
-          return fail(SPIS_ERR_STATE, "update %d drained without publishing its residual", j);
-      }
-      __builtin_ia32_pause();
-    }
+    bool ok = false;
+    ST_TRY(wait_slot(reinterpret_cast<const uint64_t*>(c->pinned + roff(j)), &ok));
+    if (!ok) return fail(SPIS_ERR_STATE, "update %d drained without publishing its residual", j);
+    return SPIS_OK;
   }
 
   double residual(int j) const {  // ||A x_j - b||, reduced on the device
