@@ -224,15 +224,16 @@ def cgmres(A, b, x0, k, tol=1e-8, contol=10, conlist=[], pre=None, timing=None, 
                 if timing:
                     stamps["end_constraints"].append(_time.time())
                 sol = _slsqp(func, y0, jac, eq[:], ctol ** 2)
+                if diag is not None:
+                    ct = [ConstraintTerms(c, x0, Z) for c in conlist]
+                    diag[j] = {"nan": bool(np.isnan(max(sol.x))), "violation": constraint_checker(sol.x, eq),
+                               "message": sol.message,
+                               "scales": [abs(t.term0) + abs(t.term1 @ sol.x) + abs(sol.x @ t.term2 @ sol.x)
+                                          if t.reduced else float("nan") for t in ct]}
                 if not timing:
                     if np.isnan(max(sol.x)):
                         raise ValueError
                 safety = True
-                if diag is not None:
-                    ct = [ConstraintTerms(c, x0, Z) for c in conlist]
-                    diag[j] = {"violation": constraint_checker(sol.x, eq), "message": sol.message,
-                               "scales": [abs(t.term0) + abs(t.term1 @ sol.x) + abs(sol.x @ t.term2 @ sol.x)
-                                          if t.reduced else float("nan") for t in ct]}
                 if not timing:
                     if constraint_checker(sol.x, eq) > ctol:
                         safety = False

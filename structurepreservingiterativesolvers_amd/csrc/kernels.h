@@ -111,7 +111,8 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator = false,
                             bool nt = false, double* gsub = nullptr, const double* yx_host = nullptr, int px = 0,
-                            const double* x0 = nullptr, double* xo = nullptr);
+                            const double* x0 = nullptr, double* xo = nullptr, int tw = 0);
+// (tw: K2q with nt — q_0 .. q_{tw-1} and x0 with ordinary loads, to stay Infinity-Cache resident)
 // (nt: the chain's basis loads are nontemporal — the matrix stays Infinity-Cache resident)
 // gsub != nullptr selects K2q, the pipelined chain (dot products one MGS step early by the
 // distributive law; gsub[m] = q_m . q_{m-1}, written by chain m, read by the later chains of the

@@ -1038,9 +1038,11 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo) {
+    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo, int tw) {
 #pragma clang fp contract(off)
   static_assert(LAG >= 1 && LAG <= 2 && NS >= LAG + 3, "ring: q_{i-1}, the dotted q_{i+LAG}, one loading");
+  // NT: nontemporal basis loads, except q_0 .. q_{tw-1} and x0 when tw > 0 (a window every chain
+  // re-reads, left to stay Infinity-Cache resident beside the matrix)
   constexpr int DT = DW * 64;  // data threads
   constexpr int NV = 1 + LAG;  // values a workgroup may publish per exchange (a_m, G(m, m-LAG..m-1))
   __shared__ double2 s_acc[FX ? PER * DT : 1];
@@ -1065,26 +1067,26 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
   const unsigned base = *epoch;
   double2 y[PER];
   double2 S[NS][PER];
-  auto load = [&](double2 (&r)[PER], const double* v) {
+  auto load = [&](double2 (&r)[PER], const double* v, bool nt) {
     const double2* v2 = reinterpret_cast<const double2*>(v);
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-      if (data && p0 + k * DT < npair) r[k] = ld_basis(v2 + p0 + k * DT, NT);
+      if (data && p0 + k * DT < npair) r[k] = ld_basis(v2 + p0 + k * DT, nt);
   };
   if (!agg) {
     if (FX && data) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) s_acc[k * DT + tid] = make_double2(0.0, 0.0);
     }
-    load(y, w);
+    load(y, w, NT);
 #pragma unroll
     for (int m = 0; m < NS - 1; ++m)
-      if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch);
+      if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch, NT && m >= tw);
     if (FX && data) {  // x0 into LDS now (added at the end: its load latency off the tail)
       const double2* x02 = reinterpret_cast<const double2*>(x0);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (p0 + k * DT < npair) s_x0[k * DT + tid] = ld_basis(x02 + p0 + k * DT, NT);
+        if (p0 + k * DT < npair) s_x0[k * DT + tid] = ld_basis(x02 + p0 + k * DT, NT && tw == 0);
     }
   }
   if (tid == 0) s_fail = 0;
@@ -1328,7 +1330,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       return false;
     }
     // q_{i+NS-1} into the slot q_{i-1} just left
-    if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch);
+    if (i + NS - 1 <= j) load(S[RM], Q + static_cast<int64_t>(i + NS - 1) * pitch, NT && i + NS - 1 >= tw);
     // E_{i+LAG} (at i = 0 also E_1 .. E_{LAG-1}: their dots against w^{(0)} as well)
     if (i == 0) {
       if (LAG >= 2 && 1 <= j) dots(std::integral_constant<int, (R + 1) % NS>{}, 1);
@@ -1569,7 +1571,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
                             int n_in, double* hcol, unsigned long long* gran, unsigned* epoch, unsigned* err,
                             hipStream_t s, const LaunchEv* ev, const double* xpart, int n_x, double* x_out,
                             unsigned long long* flag, const unsigned long long* seq, bool aggregator, bool nt,
-                            double* gsub, const double* yx_host, int px, const double* x0, double* xo) {
+                            double* gsub, const double* yx_host, int px, const double* x0, double* xo, int tw) {
   const int64_t npair = n >> 1;
   if (!aligned16(w) || !aligned16(Q) || (pitch & 1)) return hipErrorInvalidValue;
   // K2q counts (n + 1) / 2 pairs (an odd n's last pair padded): its fallback test must too
@@ -1614,7 +1616,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
 #define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
   launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
-           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo)
+           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo, tw)
 #define SPIS_LAG_PER(FX_, NT_, LAG_)          \
   switch (per) {                              \
     case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \

@@ -1967,13 +1967,23 @@ struct Solver {
     // chain +1-2 us, +2.9%; C4, whose working set fits, measured 1% slower with them)
     const double ws_bytes = 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * (k + 1) * static_cast<double>(n);
     const bool nt_chain = c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
+    // with nontemporal loads, the first basis vectors (which every later chain re-reads) and x0 keep
+    // ordinary loads while they fit the Infinity Cache beside the matrix and ~6 working vectors
+    // (C3: 6 of them; chain mean 43.0 -> 42.4 us, the dual unchanged at 36.0 us; 10 evicted part of
+    // the matrix: dual 38.4 us; gpurun_out/r04ab1)
+    auto chain_tw = [&](bool nt) {
+      if (!nt) return 0;
+      const double mat = 12.0 * A->nnz + 4.0 * (A->n_rows + 1), vec = 8.0 * static_cast<double>(n);
+      const double room = 256.0 * 1024 * 1024 - mat - 6.0 * vec;
+      return room <= 0.0 ? 0 : static_cast<int>(std::min(6.0, std::floor(room / vec)));
+    };
     if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
       if (lag_chain()) arm_hcol(j);
       const int px = (gsub && yx) ? jx + 1 : 0;
       HIP_TRY(launch_mgs_chain(n, ws->w, ws->Q, ws->pitch, j, c->partA, gs, hcol, c->chain_gran, c->chain_epoch,
                                c->chain_err_dev, s, &both, xpart, gs, x_out, flag, seq, agg, nt_chain, gsub, yx, px,
-                               ws->x0, px > 0 ? xbuf(jx) : nullptr));
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr, chain_tw(nt_chain)));
       return SPIS_OK;
     }
     if (yx) return fail(SPIS_ERR_STATE, "fused update GEMV without the pipelined chain");

@@ -1024,12 +1024,14 @@ def test_full_size_swe_c5_cycle0_vs_oracle(spis):
         assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
         np.testing.assert_allclose(r[-1], ro[-1], rtol=0, atol=1e-10 * ro[0])
     else:
-        # the oracle's own inputs differ from the device's at roundoff; where its checker's verdict
-        # flips on them, SLSQP's constraint values sit at the rounding floor of the constraint's
-        # own magnitude (ctol = 1e-12 absolute against a constraint of magnitude up to ~1e8)
+        # the oracle's own inputs differ from the device's at roundoff, and on them the reference's
+        # SLSQP either failed numerically (NaN: solvers.py:259-260 falls back) or its checker's
+        # verdict flipped at the rounding floor of the constraint's own magnitude (ctol = 1e-12
+        # absolute against a constraint of magnitude up to ~1e8): SURVEY's documented SLSQP
+        # divergence, not the device's
         dg = diag[k - 1]
         worst = max(dg["scales"])
-        assert dg["violation"] <= 64 * np.finfo(float).eps * worst, dg
+        assert dg["nan"] or dg["violation"] <= 64 * np.finfo(float).eps * worst, dg
 
 
 @pytest.mark.slow
