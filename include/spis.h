@@ -227,6 +227,13 @@ int spis_matrix_destroy(spis_matrix* A);
 /* info[0]=n_rows info[1]=n_cols info[2]=nnz info[3]=row blocks info[4]=long-row blocks
  * info[5]=n_ghost info[6]=all values zero (1/0) */
 int spis_matrix_info(spis_matrix* A, int64_t info[8]);
+/* Several GPUs: declares A (a rank's rows, as uploaded with a halo plan) a row block of a global
+ * matrix: col_gid[n_cols] is the global index of each local column (the owned columns first, in
+ * the rows' order, then the ghosts) and symmetric != 0 says the global matrix equals its transpose
+ * exactly.  The constraint Gram then pairs (r, c) with (c, r) by global index (K7t) on every rank
+ * instead of gathering both (K7m).  Replaces nothing in the reference: the global matrix of
+ * constraint_container (solvers.py:22-36) is one object there. */
+int spis_matrix_set_global(spis_matrix* A, const int64_t* col_gid, int32_t symmetric);
 
 /* ---- device ILU preconditioner (pre.solve of a SuperLU spilu object) -------- */
 /* Replaces the host call pre.solve(vec) of solvers.py:152-154 (used at :190) for

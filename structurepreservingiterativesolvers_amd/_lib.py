@@ -130,6 +130,7 @@ SIGNATURES = [
     ("spis_csr_upload", C.c_int, [_VP, _I64, _I64, _I64, _PI32, _PI32, _PD, C.POINTER(HaloDesc), C.POINTER(_VP)]),
     ("spis_matrix_destroy", C.c_int, [_VP]),
     ("spis_matrix_info", C.c_int, [_VP, _PI64]),
+    ("spis_matrix_set_global", C.c_int, [_VP, _PI64, _I32]),
     ("spis_ilu_create", C.c_int, [_VP, _I64, _PI32, _PI32, _PD, _PI32, _PI32, _PD, _PI32, _PI32, C.POINTER(_VP)]),
     ("spis_ilu_apply", C.c_int, [_VP, _VP, _VP]),
     ("spis_ilu_info", C.c_int, [_VP, _PI64]),

@@ -194,6 +194,11 @@ struct spis_matrix {
   double* sym_val = nullptr;
   unsigned long long* sym_mask = nullptr;
   int32_t sym_nblk = 0;
+  // spis_matrix_set_global: each local column's global index and whether the global matrix is
+  // symmetric (several GPUs: a rank's rows of a symmetric matrix are not square, so K7t pairs
+  // entries by global index)
+  std::vector<int64_t> gid;
+  int gsym = -1;
   // halo plan
   int32_t n_ghost = 0;
   std::vector<int32_t> nbr, scnt, rcnt, soff, roff;
@@ -1113,6 +1118,28 @@ extern "C" int spis_ilu_destroy(spis_ilu* P) {
   })
 }
 
+// several GPUs: the global index of each of A's local columns (owned columns first, in the rows'
+// order, then the ghosts) and whether the global matrix is exactly symmetric; K7t then pairs a
+// rank's entries (r, c) by global index (distributed.py computes both from the global matrix)
+extern "C" int spis_matrix_set_global(spis_matrix* M, const int64_t* col_gid, int32_t symmetric) {
+  ABI_GUARD({
+    if (!M || !col_gid) return fail(SPIS_ERR_ARG, "null argument");
+    if (M->n_rows > M->n_cols) return fail(SPIS_ERR_ARG, "spis_matrix_set_global: more rows than columns");
+    M->gid.assign(col_gid, col_gid + M->n_cols);
+    M->gsym = symmetric ? 1 : 0;
+    if (M->sym_state == 1) {  // the table was built without the global numbering
+      (void)hipFree(M->sym_col);
+      (void)hipFree(M->sym_val);
+      (void)hipFree(M->sym_mask);
+      M->sym_col = nullptr;
+      M->sym_val = nullptr;
+      M->sym_mask = nullptr;
+    }
+    M->sym_state = -1;
+    return SPIS_OK;
+  })
+}
+
 extern "C" int spis_matrix_info(spis_matrix* M, int64_t info[8]) {
   if (!M || !info) return fail(SPIS_ERR_ARG, "null argument");
   info[0] = M->n_rows;
@@ -1300,7 +1327,10 @@ static int ensure_symtab(spis_context* c, spis_matrix* M, SymTabView* out, bool*
   if (M->sym_state < 0) {
     M->sym_state = 0;
     const int64_t n = M->n_rows, nnz = M->nnz;
-    if (M->n_cols != n) {
+    // a rank's rows of a globally symmetric matrix (spis_matrix_set_global): entries are paired
+    // by global index, the local numbering (owned, then ghosts) stays the Ut row index
+    const bool global = !M->gid.empty() && M->gsym == 1 && static_cast<int64_t>(M->gid.size()) == M->n_cols;
+    if (M->n_cols != n && !global) {
       *ok = false;
       return SPIS_OK;
     }
@@ -1312,32 +1342,37 @@ static int ensure_symtab(spis_context* c, spis_matrix* M, SymTabView* out, bool*
       HIP_TRY(hipMemcpy(ci.data(), M->indices, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
       HIP_TRY(hipMemcpy(va.data(), M->vals, sizeof(double) * nnz, hipMemcpyDeviceToHost));
     }
-    // exact symmetry: every row's (col, value) multiset equals the transpose's
-    std::vector<int64_t> tp(n + 1, 0);
-    for (int64_t e = 0; e < nnz; ++e) ++tp[ci[e] + 1];
-    for (int64_t r = 0; r < n; ++r) tp[r + 1] += tp[r];
-    std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
-    std::vector<std::pair<int32_t, double>> te(std::max<int64_t>(nnz, 1));
-    for (int64_t r = 0; r < n; ++r)
-      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) te[fill[ci[e]]++] = {static_cast<int32_t>(r), va[e]};
+    // exact symmetry: every row's (col, value) multiset equals the transpose's (the caller
+    // declared it for a rank's rows of a global matrix)
     bool sym = true;
-    std::vector<std::pair<int32_t, double>> row;
-    for (int64_t r = 0; r < n && sym; ++r) {
-      if (tp[r + 1] - tp[r] != rp[r + 1] - rp[r]) {
-        sym = false;
-        break;
+    if (!global) {
+      std::vector<int64_t> tp(n + 1, 0);
+      for (int64_t e = 0; e < nnz; ++e) ++tp[ci[e] + 1];
+      for (int64_t r = 0; r < n; ++r) tp[r + 1] += tp[r];
+      std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
+      std::vector<std::pair<int32_t, double>> te(std::max<int64_t>(nnz, 1));
+      for (int64_t r = 0; r < n; ++r)
+        for (int32_t e = rp[r]; e < rp[r + 1]; ++e) te[fill[ci[e]]++] = {static_cast<int32_t>(r), va[e]};
+      std::vector<std::pair<int32_t, double>> row;
+      for (int64_t r = 0; r < n && sym; ++r) {
+        if (tp[r + 1] - tp[r] != rp[r + 1] - rp[r]) {
+          sym = false;
+          break;
+        }
+        row.clear();
+        for (int32_t e = rp[r]; e < rp[r + 1]; ++e) row.push_back({ci[e], va[e]});
+        auto lt = [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
+          return x.first != y.first ? x.first < y.first : x.second < y.second;
+        };
+        std::sort(row.begin(), row.end(), lt);
+        std::vector<std::pair<int32_t, double>> trow(te.begin() + tp[r], te.begin() + tp[r + 1]);
+        std::sort(trow.begin(), trow.end(), lt);
+        for (size_t i = 0; i < row.size() && sym; ++i)
+          sym = row[i].first == trow[i].first && row[i].second == trow[i].second;
       }
-      row.clear();
-      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) row.push_back({ci[e], va[e]});
-      auto lt = [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
-        return x.first != y.first ? x.first < y.first : x.second < y.second;
-      };
-      std::sort(row.begin(), row.end(), lt);
-      std::vector<std::pair<int32_t, double>> trow(te.begin() + tp[r], te.begin() + tp[r + 1]);
-      std::sort(trow.begin(), trow.end(), lt);
-      for (size_t i = 0; i < row.size() && sym; ++i)
-        sym = row[i].first == trow[i].first && row[i].second == trow[i].second;
     }
+    // the pairing key: the global index (identity on one GPU)
+    auto key = [&](int64_t col) { return global ? M->gid[col] : col; };
     if (sym) {
       // segments of 4-row groups: slot 0 = each row's own U row (value M_rr / 2, duplicates summed),
       // then its entries with c > r in CSR order, padded (col = the row itself, value 0)
@@ -1368,9 +1403,11 @@ static int ensure_symtab(spis_context* c, spis_matrix* M, SymTabView* out, bool*
           diag[g] = 0.0;
           const int64_t r = 4 * q + g;
           if (r >= n) continue;
+          const int64_t kr = key(r);  // a row's global index is its owned column's
           for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
-            if (ci[e] == r) diag[g] += va[e];
-            else if (ci[e] > r) {
+            const int64_t kc = key(ci[e]);
+            if (kc == kr) diag[g] += va[e];
+            else if (kc > kr) {
               up[g].push_back(ci[e]);
               upv[g].push_back(va[e]);
             }
@@ -1483,8 +1520,9 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   // 3: K7m for every matrix.  Both read Ut in the MFMA column order.  1 (and p + 1 > 32): K7 on the CSR.
   const int eg = c->con_gram;
   const bool mfma = np1 <= 32 && eg >= 2;
-  // K7t's symmetric pairing needs both (r, c) and (c, r) in one rank's rows: single GPU only
-  const bool tsym = mfma && eg == 2 && !c->comm;
+  // K7t pairs (r, c) with (c, r): on several GPUs by global index, for the matrices declared
+  // symmetric with their global numbering (spis_matrix_set_global); the others take K7m
+  const bool tsym = mfma && eg == 2;
   std::vector<Launch> plan;
   for (int ci = 0; ci < m; ++ci) {
     if (cons[ci].M == nullptr || cons[ci].M->all_zero) continue;
@@ -1499,6 +1537,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
     HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart,
                                        c->cg_G + 64 * 64, st));
+    if (nv > 0) ST_TRY(allreduce_on(c, c->cg_G + 64 * 64, static_cast<int64_t>(nv) * np1, st));  // local rows' sums
     if (nv > 0)
       HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + 64 * 64, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
     v_done = true;

@@ -154,6 +154,30 @@ def halo_plan(op: LocalOperator, part: FieldPartition, rank: int, allgather) -> 
     return HaloPlan(neighbors, send_counts, send_idx, recv_counts, len(op.ghosts_new))
 
 
+def is_exactly_symmetric(M) -> bool:
+    """M equals its transpose entry by entry (values included): K7t's pairing condition."""
+    M = sps.csr_matrix(M)
+    if M.shape[0] != M.shape[1]:
+        return False
+    D = (M - M.T).tocsr()
+    D.eliminate_zeros()
+    return D.nnz == 0
+
+
+def local_global_ids(op: LocalOperator, part: FieldPartition, rank: int):
+    """Global (partition-ordered) index of each local column: owned columns first, in the rows'
+    order, then the ghosts."""
+    lo = part.starts[rank]
+    n_local = op.csr.shape[0]
+    return np.concatenate([np.arange(lo, lo + n_local, dtype=np.int64), op.ghosts_new.astype(np.int64)])
+
+
+def set_global_numbering(Md, op: LocalOperator, part: FieldPartition, rank: int, symmetric: bool):
+    gid = np.ascontiguousarray(local_global_ids(op, part, rank))
+    _lib.check(Md.ctx.L.spis_matrix_set_global(Md.handle, gid.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                1 if symmetric else 0), "spis_matrix_set_global")
+
+
 def emulate_spmv(op: LocalOperator, plan: HaloPlan, x_local, exchange):
     """NumPy reference of the distributed SpMV data path (for CPU tests):
     ``exchange(send_bufs_by_neighbor) -> recv_bufs_by_neighbor``."""
@@ -247,11 +271,16 @@ class DistributedSystem:
         return DeviceVector.from_host(self.part.to_local(v_global, self.rank), ctx=self.comm.ctx)
 
     def matrix(self, M_global):
+        """A further global operator (a constraint matrix) on this partition.  Its local columns'
+        global indices and whether M_global is exactly symmetric go to the library
+        (spis_matrix_set_global), so the constraint Gram pairs (r, c) with (c, r) across ranks."""
         from .device import DeviceMatrix
 
         op = local_operator(M_global, self.part, self.rank)
         plan = halo_plan(op, self.part, self.rank, self.comm.allgather)
-        return DeviceMatrix(self.comm.ctx, op.csr, halo=plan)
+        Md = DeviceMatrix(self.comm.ctx, op.csr, halo=plan)
+        set_global_numbering(Md, op, self.part, self.rank, is_exactly_symmetric(M_global))
+        return Md
 
     def gather(self, x_local):
         """All local pieces -> the global vector in the reference ordering (every rank)."""

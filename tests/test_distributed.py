@@ -138,6 +138,43 @@ def test_local_operator_ghosts_are_neighbours_only():
         assert op.csr.indices.dtype == np.int32
 
 
+@pytest.mark.parametrize("nparts", [1, 2, 4])
+def test_symmetric_gram_pairs_by_global_index(nparts):
+    """K7t on several GPUs (spis_matrix_set_global): each rank forms H_r = sum over its rows r of
+    U_r W_r^T with W_r = M_rr U_r / 2 + sum_{gid(c) > gid(r)} M_rc U_c over its local columns
+    (ghosts included, at their Ut rows), and the all-reduced H + H^T is U^T M U: every pair (r, c)
+    is taken by exactly one rank, the owner of the row with the smaller global index.  NumPy
+    model of the kernel's pairing on the product's partition and global numbering."""
+    from structurepreservingiterativesolvers_amd.distributed import is_exactly_symmetric, local_global_ids
+    from structurepreservingiterativesolvers_amd.swe import assembly
+
+    M = 12
+    dic = assembly.linforms(M=M)[0]
+    L = dic["L"].tocsr()
+    assert is_exactly_symmetric(L) and not is_exactly_symmetric(dic["A"])
+    part = FieldPartition(swe_fields(M), nparts)
+    n = L.shape[0]
+    U = np.random.default_rng(4).normal(size=(n, 5))   # reference ordering
+    Un = U[part.perm]                                   # partition (new) ordering
+    G = np.zeros((5, 5))
+    for r in range(nparts):
+        op = local_operator(L, part, r)
+        gid = local_global_ids(op, part, r)
+        Ut = Un[gid]  # the local rows, then the ghosts' rows (the halo exchange's result)
+        H = np.zeros((5, 5))
+        for i in range(op.csr.shape[0]):
+            w = np.zeros(5)
+            for e in range(op.csr.indptr[i], op.csr.indptr[i + 1]):
+                c = op.csr.indices[e]
+                if gid[c] == gid[i]:
+                    w += 0.5 * op.csr.data[e] * Ut[c]
+                elif gid[c] > gid[i]:
+                    w += op.csr.data[e] * Ut[c]
+            H += np.outer(Ut[i], w)
+        G += H + H.T
+    np.testing.assert_allclose(G, U.T @ (L @ U), rtol=1e-12, atol=1e-12 * np.abs(U.T @ (L @ U)).max())
+
+
 @pytest.mark.parametrize("nparts", [2, 4])
 def test_lkdvrk_stage_field_partition_nearest_neighbour(nparts):
     """Config C4's row split (lkdvRK GL(3), stage x field blocks): the block-stage operator

@@ -1159,7 +1159,8 @@ def test_full_size_swe_vs_oracle(spis):
     assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
 
 
-@pytest.mark.parametrize("dist_mgs,gram", [("one_reduce", "fused"), ("per_step", "fused"), ("one_reduce", "generic")])
+@pytest.mark.parametrize("dist_mgs,gram", [("one_reduce", "fused"), ("per_step", "fused"), ("one_reduce", "generic"),
+                                           ("one_reduce", "fused_sym")])
 def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
     """The RCCL data path on one GPU: a 1-rank communicator (fixed-size partial arrays +
     ncclAllReduce) and an operator whose last ~20% columns are declared ghosts received from
@@ -1167,7 +1168,9 @@ def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
     all-reduces per Arnoldi step, SPIS_OPT_DIST_MGS 1, the default) or one all-reduce per
     projection; constraints through K7m on the local rows with the ghost Ut rows exchanged
     through the matrix's halo plan and G all-reduced (fused), or the generic per-column halo
-    path.  Must reproduce the single-GPU solve."""
+    path; fused_sym: the energy matrix declared symmetric with its global numbering
+    (spis_matrix_set_global), so K7t pairs its entries by global index, ghosts included.  Must
+    reproduce the single-GPU solve."""
     import ctypes as C
 
     from structurepreservingiterativesolvers_amd import _lib, solvers
@@ -1204,8 +1207,17 @@ def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
     assert Ad.n_ghost > 0
     bd = DeviceVector.from_host(dic["b"], ctx=ctx)
     x0d = DeviceVector.from_host(x0, ctx=ctx)
+    Ld = self_halo(dic["L"])
+    if gram == "fused_sym":
+        from structurepreservingiterativesolvers_amd.distributed import is_exactly_symmetric
+
+        Lc = dic["L"].tocsr()
+        cut = int(0.8 * n)
+        gid = np.concatenate([np.arange(n), np.unique(Lc.indices[Lc.indices >= cut])]).astype(np.int64)
+        assert is_exactly_symmetric(Lc) and len(gid) == Ld.shape[1]
+        _lib.check(ctx.L.spis_matrix_set_global(Ld.handle, gid.ctypes.data_as(C.POINTER(C.c_int64)), 1), "global")
     cons = [_DevCon(None, DeviceVector.from_host(dic["omega"], ctx=ctx), -dic["m0"]),
-            _DevCon(self_halo(dic["L"]), None, -dic["e0"])]
+            _DevCon(Ld, None, -dic["e0"])]
     r = solvers._run(_lib.CGMRES, Ad, bd, x0d, 20, 1e-19, 10, cons, None, None)
     x = r["final"].numpy()
     assert r["steps"] == ds["steps"]
