@@ -80,7 +80,8 @@ hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b,
                             const double* x2, double* w, const double* q0, double* part2, int grid,
                             hipStream_t s, const LaunchEv* ev = nullptr);
 // K1p / K1dp (A.blk_meta on a kPipeCap table): mode 0-3 = launch_spmv's epilogue (x1, aux1, y1,
-// part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi)
+// part1); mode 4 = the dual (x1, aux1 = b, part1: residual; x2, aux2 = q0, y2 = w, part2: Arnoldi);
+// mode 6 = two true residuals (x1, x2 against aux1 = aux2 = b: ||.||^2 partials, nothing stored)
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
                             int grid, hipStream_t s, const LaunchEv* ev = nullptr);
@@ -208,6 +209,9 @@ hipError_t launch_dot(int64_t n, const double* x, const double* y, double* part_
 hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s,
                            const LaunchEv* ev = nullptr, unsigned long long* flag = nullptr,
                            const unsigned long long* seq = nullptr);
+// both reductions of a paired residual SpMV in one launch, each published as launch_finalize's
+hipError_t launch_finalize2(const double* part1, const double* part2, int n_in, double* out1, double* out2,
+                            hipStream_t s, unsigned long long* flag);
 hipError_t launch_axpy(int64_t n, double h, const double* x, double* y, hipStream_t s);
 hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
 // streaming read of n doubles (16-B aligned, n even): evicts L2 and the Infinity Cache

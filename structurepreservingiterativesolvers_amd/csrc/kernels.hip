@@ -381,7 +381,8 @@ __device__ __forceinline__ void block_walk(int n_blk, int walk, int& b0, int& b1
 }
 
 // x1/aux1/y1/part1: the single SpMV (MODE 0-3) or the residual half of the dual (aux1 = b);
-// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half (MODE 4)
+// x2/aux2 (= q0)/y2 (= w)/part2: the dual's Arnoldi half (MODE 4); MODE 6: two true residuals
+// (x1 and x2 against aux1 = aux2 = b, ||.||^2 partials to part1 / part2, nothing stored)
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
 // (variants measured and not adopted — nontemporal stream, 4 waves per SIMD, buffer descriptors,
 // thread-major columns, two-deep pipeline, SELL-64 — live in tools/spmv_variants.hip)
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
     double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
-  constexpr bool DUAL = MODE == 4;
+  constexpr bool DUAL = MODE == 4 || MODE == 6;
   constexpr int kPer = PipeStage<CAP>::kPer;
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
   // of 16 entries (swe's edge rows) would otherwise put a wave's lanes 256 B apart, all in one
@@ -424,8 +425,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
         if (DUAL) {
           const double t = s1 - aux1[r0];
           pt1 += t * t;
-          y2[r0] = s2;
-          pt2 += aux2[r0] * s2;
+          if (MODE == 6) {
+            const double t2 = s2 - aux2[r0];
+            pt2 += t2 * t2;
+          } else {
+            y2[r0] = s2;
+            pt2 += aux2[r0] * s2;
+          }
         }
         if (MODE == kEpiPlain) y1[r0] = s1;
         if (MODE == kEpiDot) { y1[r0] = s1; pt1 += aux1[r0] * s1; }
@@ -518,8 +524,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
       if (DUAL) {
         const double t = s1 - cur.a1;
         pt1 += t * t;
-        y2[r] = s2;
-        pt2 += cur.a2 * s2;
+        if (MODE == 6) {
+          const double t2 = s2 - cur.a2;
+          pt2 += t2 * t2;
+        } else {
+          y2[r] = s2;
+          pt2 += cur.a2 * s2;
+        }
       }
       if (MODE == kEpiPlain) y1[r] = s1;
       if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
@@ -562,7 +573,8 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
     case 1: SPIS_PIPE(1); break;
     case 2: SPIS_PIPE(2); break;
     case 3: SPIS_PIPE(3); break;
-    default: SPIS_PIPE(4); break;
+    case 4: SPIS_PIPE(4); break;
+    default: SPIS_PIPE(6); break;
   }
 #undef SPIS_PIPE
   return hipGetLastError();
@@ -2344,6 +2356,22 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restri
   __shared__ double s_wave[4];
   const double t = sum_partials(part, n_in, s_wave);
   if (threadIdx.x == 0) publish(out, op == 1 ? sqrt(t) : t, flag, seq);
+}
+
+// two reductions in one launch (the paired residuals): workgroup i reduces part_i into out_i
+__global__ __launch_bounds__(kBlock) void finalize2_kernel(const double* __restrict__ part1,
+                                                           const double* __restrict__ part2, int n_in,
+                                                           double* __restrict__ out1, double* __restrict__ out2,
+                                                           unsigned long long* __restrict__ flag) {
+  __shared__ double s_wave[4];
+  const double t = sum_partials(blockIdx.x == 0 ? part1 : part2, n_in, s_wave);
+  if (threadIdx.x == 0) publish(blockIdx.x == 0 ? out1 : out2, t, flag, nullptr);
+}
+
+hipError_t launch_finalize2(const double* part1, const double* part2, int n_in, double* out1, double* out2,
+                            hipStream_t s, unsigned long long* flag) {
+  hipLaunchKernelGGL(finalize2_kernel, dim3(2), dim3(kBlock), 0, s, part1, part2, n_in, out1, out2, flag);
+  return hipGetLastError();
 }
 
 hipError_t launch_finalize(const double* part, int n_in, double* out, int op, hipStream_t s, const LaunchEv* ev,

@@ -2176,6 +2176,23 @@ struct Solver {
     return SPIS_OK;
   }
 
+  // U_j1's and U_j2's true-residual SpMVs in one launch (the matrix read once; the last two
+  // iterates of a solve, which have no Arnoldi SpMV to pair with), both published
+  bool res2_ok() const { return !c->comm && A->dual_view().blk_meta != nullptr; }
+  int enqueue_residual2(int j1, int j2) {
+    {
+      ProfEv ps(c, SPIS_PROF_SPMV_RES);
+      const LaunchEv le = ps.both();
+      HIP_TRY(launch_spmv_pipe(A->dual_view(), 6, xbuf(j1), b, nullptr, c->partR, xbuf(j2), b, nullptr, c->partB, gs,
+                               c->stream, &le));
+    }
+    next_seq(j1);
+    next_seq(j2);
+    HIP_TRY(launch_finalize2(c->partR, c->partB, gs, c->pinned_dev + roff(j1), c->pinned_dev + roff(j2), c->stream,
+                             flag_dev()));
+    return SPIS_OK;
+  }
+
   // U_j = update_gemv (x_j = Z y + x0, halo) -> true-residual SpMV -> update_finish (host signal)
   int update_gemv(int j, int p, const double* y, hipStream_t s_gemv = nullptr) {  // :287
     hipStream_t s = s_gemv ? s_gemv : c->stream;
@@ -2380,6 +2397,11 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // recomputes x_j after c_{j+1}), and enqueues [U_j res | a_{j+2}] (res + finalize at the end).
     std::vector<double> yspec(k);
     int last_x = -1;  // iteration whose x_j is x[-1]
+    // L mode: U_{k-2}'s residual held back and read with U_{k-1}'s in one SpMV (the matrix read
+    // once) when it cannot stop the run: CGMRES with safety not True at k-2 (solvers.py:296-297)
+    // or CGMRES_P; the record order stays res_{k-2}, res_{k-1}
+    int deferred = -1;
+    bool deferred_queued = false;
     int gram_queued = -1;  // iteration whose constraint reduction is already on the stream
     int spec_kkt = -1;     // iteration whose KKT solve already ran (ycon, spec_kr)
     KKTResult spec_kr;
@@ -2449,9 +2471,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           spec_kkt = j;
         }
       }
-      ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : S.wait_update(j - 1));
+      ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : (deferred == j - 1 ? SPIS_OK : S.wait_update(j - 1)));
       prof_drain(c);
-      if (pending >= 0) {  // finish iteration j-1: true residual + stop test (solvers.py:290-297)
+      if (pending >= 0 && pending != deferred) {  // finish iteration j-1: true residual + stop test (:290-297)
         out->res_host[n_res++] = S.residual(pending);
         if (stamps) stamps[k + pending] = now_s();
         pending = -1;
@@ -2585,7 +2607,15 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           // the forced constrained last step's reduction first (its inputs, q_0 .. q_{k-1} and
           // x0, are complete): the host's KKT then runs while the GPU computes this residual
           if (j + 1 == k - 1 && gram_early_ok(j + 1)) ST_TRY(queue_gram(j + 1));
-          ST_TRY(S.enqueue_residual(j));
+          const bool may_stop = o->method == SPIS_GMRES || (o->method == SPIS_CGMRES && safety == kSafetyTrue);
+          if (j == k - 2 && !may_stop && !o->timing && S.res2_ok()) {
+            deferred = j;  // paired with U_{k-1}'s below
+          } else if (deferred == j - 1 && deferred >= 0) {
+            ST_TRY(S.enqueue_residual2(j - 1, j));
+            deferred_queued = true;
+          } else {
+            ST_TRY(S.enqueue_residual(j));
+          }
         }
       } else if (j + 2 < k && c->fuse_spmv) {
         if (stamps) stamps[j + 2] = now_s();
@@ -2607,7 +2637,13 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
       else HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));
     }
-    if (pending >= 0) {
+    if (deferred >= 0) {  // U_{k-2}'s residual, on its own if the run ended before U_{k-1}
+      if (!deferred_queued) ST_TRY(S.enqueue_residual(deferred));
+      ST_TRY(S.wait_update(deferred));
+      out->res_host[n_res++] = S.residual(deferred);
+      if (stamps) stamps[k + deferred] = now_s();
+    }
+    if (pending >= 0 && pending != deferred) {
       ST_TRY(S.wait_update(pending));
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
