@@ -474,6 +474,30 @@ def test_nontemporal_chain_loads_bit_identical(spis):
             assert np.array_equal(a, bb)
 
 
+def test_paired_last_residuals_bit_identical(spis):
+    """The last two true residuals of a CGMRES solve run as one SpMV (spmv_pipe_kernel MODE 6)
+    unless the run's timing mode asks for per-iteration stamps; the pairing must not change a bit
+    of the residual history, the iterates or the branch sequence (the partials group as in two
+    single launches)."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=20)
+    cons = swe_ls.constraints(dic, np.zeros_like(dic["b"]))
+    A, b = dic["A"], dic["b"]
+    x0 = np.zeros_like(b)
+    runs = []
+    for timing in (None, True):
+        x, d = solvers.cgmres(A, b, x0, 25, tol=1e-19, conlist=cons, timing=timing)
+        runs.append((x, np.asarray(d["res"]), d["x"].trace, np.concatenate(d["x"].y)))
+    (x1, r1, t1, y1), (x2, r2, t2, y2) = runs
+    assert t1 == t2
+    assert np.array_equal(r1, r2)
+    assert np.array_equal(y1, y2)
+    assert np.array_equal(x1, x2)
+
+
 def test_fused_dual_spmv_bit_identical(spis):
     """SPIS_OPT_FUSE_SPMV: the true-residual SpMV of U_j fused with the Arnoldi SpMV of A_{j+2}
     (matrix read once) gives bit-identical iterates, residuals, LS solutions and basis, in the
