@@ -741,7 +741,7 @@ def test_restarted_cgmres_vs_oracle_loop(spis):
     x0 = np.zeros(n)
     cons = swe_ls.constraints(dic, x0)
     D, c3 = sa.extra_constraint(n, dic["z0"], seed=2)
-    cons.append(swe_ls._Constraint(D, None, c3))
+    cons.append(swe_ls._Constraint(D, np.zeros(n), c3))  # v as the bench (and the reference's class form) has it
     k, cycles = 12, 3
     x, d = solvers.cgmres_restarted(dic["A"], dic["b"], x0, k, cycles, tol=1e-19, conlist=cons,
                                     keep_iterates=True)
@@ -1020,7 +1020,7 @@ def test_full_size_swe_c5_cycle0_vs_oracle(spis):
     x0 = np.zeros(n)
     cons = swe_ls.constraints(dic, x0)
     D, c3 = sa.extra_constraint(n, dic["z0"], seed=2)
-    cons.append(swe_ls._Constraint(D, None, c3))
+    cons.append(swe_ls._Constraint(D, np.zeros(n), c3))  # v as the bench (and the reference's class form) has it
     k = 30
     x, d = solvers.cgmres(dic["A"], dic["b"], x0, k, tol=1e-19, conlist=device_constraints(cons))
     xs = {j: np.asarray(d["x"][j]) for j in (1, 10, 20, 29)}
@@ -1080,7 +1080,7 @@ def test_full_size_swe_c5_restarted_properties(spis):
     x0 = np.zeros(n)
     cons = swe_ls.constraints(dic, x0)
     D, c3 = sa.extra_constraint(n, dic["z0"], seed=2)
-    cons.append(swe_ls._Constraint(D, None, c3))
+    cons.append(swe_ls._Constraint(D, np.zeros(n), c3))  # v as the bench (and the reference's class form) has it
     k = 30
     x, d = solvers.cgmres_restarted(dic["A"], dic["b"], x0, k, 10, tol=1e-19, conlist=device_constraints(cons),
                                     keep_iterates=True)

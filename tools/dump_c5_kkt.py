@@ -31,7 +31,7 @@ n = dic["A"].shape[0]
 x0 = np.zeros(n)
 cons = ls.constraints(dic, x0)
 D, c3 = assembly.extra_constraint(n, dic["z0"], seed=2)
-cons.append(ls._Constraint(D, None, c3))
+cons.append(ls._Constraint(D, np.zeros(n), c3))
 print(f"assembled M={M} N={n} in {time.time() - t:.1f}s", flush=True)
 ctx = get_context(0)
 bd = DeviceVector.from_host(dic["b"], ctx=ctx)
