@@ -23,6 +23,7 @@ import argparse
 import collections
 import csv
 import json
+import math
 import os
 import statistics
 import subprocess
@@ -56,7 +57,10 @@ def reduce(cfg, fetch_csv, write_csv, out):
     if not cal_f or not cal_w:
         raise SystemExit("calibration launches missing from the counter files")
     fc = GIB / (statistics.median(cal_f) * 1024)  # counters in KiB
-    wc = GIB / (max(cal_w) * 1024)
+    # the calibration fill is the 1 GiB eviction memset; the solver's own workspace
+    # memsets are fills too (2.4 GB at C5), so pick the launch nearest 1 GiB, not the max
+    wcal = min(cal_w, key=lambda v: abs(math.log(max(v, 1.0) * 1024 / GIB)))
+    wc = GIB / (wcal * 1024)
     wmap = {d: v for d, _, v in w}
     byte = {d: v * 1024 * fc + wmap.get(d, 0.0) * 1024 * wc for d, _, v in f}
     names = {d: k for d, k, _ in f}
