@@ -141,9 +141,15 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
                              int64_t n_gx = 0);
 // K2w (multi-GPU MGS, one reduction for the projections): partials of q_l . w (l < nv) and of
 // q_l . q_{nv-1} (l < nv - 1) -> part rows [0, nv) and [nv, 2 nv - 1), grid columns each
-// nt: nontemporal basis loads (the matrix stays Infinity-Cache resident between SpMVs, as K2q's)
+// nt: nontemporal basis loads (the matrix stays Infinity-Cache resident between SpMVs, as K2q's),
+// except for the first tw basis vectors.  slots != nullptr (the fold): no part rows; the launch's
+// last workgroups reduce the partials (published as tagged halves in slots, 2 (2 kCgsMax - 1)
+// kRedGrid words; tag: a fresh nonzero value per launch) into d[0, 2 nv - 1) bitwise as
+// launch_cgs_finalize(part, grid, 2 nv - 1, d, .., zero_to) would; a timed-out wait sets *err
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
-                           hipStream_t s, const LaunchEv* ev = nullptr, bool nt = false);
+                           hipStream_t s, const LaunchEv* ev = nullptr, bool nt = false, int tw = 0,
+                           unsigned long long* slots = nullptr, unsigned tag = 0, double* d = nullptr,
+                           int zero_to = 0, unsigned* err = nullptr);
 // K2w's update: every workgroup first forms the coefficients from those 2 nv - 1 dots (reduced, d):
 // Gram row nv - 1 into G (kCgsMax x kCgsMax, by workgroup 0), h_l = q_l . w - sum_{m<l} h_m G(l, m)
 // in l order (h_out: the H column, by workgroup 0), then w -= Q h with the ||w'||^2 partials, and
@@ -154,7 +160,7 @@ hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pit
                               int px = 0, const double* yx = nullptr, const double* x0 = nullptr,
                               double* xo = nullptr, int64_t n_gx = 0, const double* rpart = nullptr, int r_in = 0,
                               double* r_out = nullptr, unsigned long long* flag = nullptr,
-                              const unsigned long long* seq = nullptr);
+                              const unsigned long long* seq = nullptr, int tw = 0);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s, int zero_to = 0);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM

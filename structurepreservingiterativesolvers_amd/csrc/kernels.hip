@@ -1847,7 +1847,7 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
                                                             const double* __restrict__ coef,
                                                             double* __restrict__ part, int px, YArg yx,
                                                             const double* __restrict__ x0, double* __restrict__ xo,
-                                                            int64_t n_gx, CoefArg ca) {
+                                                            int64_t n_gx, CoefArg ca, int tw) {
   __shared__ double s_c[kCgsMax];
   __shared__ double s_sum[4][4][64];  // [wave][element slot][lane]
   __shared__ double s_x[FX ? 4 : 1][4][64];
@@ -1881,12 +1881,22 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     double2 qa[kCgsPerWave], qb[kCgsPerWave];
     double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
     double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+    // w (and, for the GEMV's wave, x0) issued with the basis loads: loaded after the barrier, they
+    // were a full memory latency per chunk during which the workgroup's other waves sat at the
+    // second barrier
+    const double2 wa = *reinterpret_cast<const double2*>(w + e);
+    const double2 wb = *reinterpret_cast<const double2*>(w + e + 128);
+    double2 ba = make_double2(0.0, 0.0), bb = make_double2(0.0, 0.0);
+    if (FX && wid == 1) {
+      ba = *reinterpret_cast<const double2*>(x0 + e);
+      bb = *reinterpret_cast<const double2*>(x0 + e + 128);
+    }
 #pragma unroll
     for (int m = 0; m < kCgsPerWave; ++m) {
       if (wid + 4 * m < nv) {
         const double* qv = Qw + m * step;
-        qa[m] = ld_basis(reinterpret_cast<const double2*>(qv + e), NT);
-        qb[m] = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT);
+        qa[m] = ld_basis(reinterpret_cast<const double2*>(qv + e), NT && wid + 4 * m >= tw);
+        qb[m] = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT && wid + 4 * m >= tw);
         const double cm = s_c[wid + 4 * m];
         p0 += cm * qa[m].x;
         p1 += cm * qa[m].y;
@@ -1904,8 +1914,6 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
         qb[m] = make_double2(0.0, 0.0);
       }
     }
-    const double2 wa = *reinterpret_cast<const double2*>(w + e);
-    const double2 wb = *reinterpret_cast<const double2*>(w + e + 128);
     s_sum[wid][0][lane] = p0;
     s_sum[wid][1][lane] = p1;
     s_sum[wid][2][lane] = p2;
@@ -1934,8 +1942,6 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
-      const double2 ba = *reinterpret_cast<const double2*>(x0 + e);
-      const double2 bb = *reinterpret_cast<const double2*>(x0 + e + 128);
       *reinterpret_cast<double2*>(xo + e) = make_double2(xs[0] + ba.x, xs[1] + ba.y);
       *reinterpret_cast<double2*>(xo + e + 128) = make_double2(xs[2] + bb.x, xs[3] + bb.y);
     }
@@ -2038,24 +2044,24 @@ hipError_t launch_cgs_dot(int64_t n, const double* w, const double* Q, int64_t p
 template <bool NT, bool FX, bool COEF>
 static void launch_update0(int grid, hipStream_t s, int64_t n, double* w, const double* Q, int64_t pitch, int nv,
                            const double* coef, double* part, int px, const YArg& ya, const double* x0, double* xo,
-                           int64_t n_gx, const CoefArg& ca) {
+                           int64_t n_gx, const CoefArg& ca, int tw) {
   hipLaunchKernelGGL((cgs_update_kernel<0, NT, FX, COEF>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
-                     part, px, ya, x0, xo, n_gx, ca);
+                     part, px, ya, x0, xo, n_gx, ca, tw);
 }
 
 template <bool NT, bool FX>
 static void launch_update0c(bool cf, int grid, hipStream_t s, int64_t n, double* w, const double* Q, int64_t pitch,
                             int nv, const double* coef, double* part, int px, const YArg& ya, const double* x0,
-                            double* xo, int64_t n_gx, const CoefArg& ca) {
+                            double* xo, int64_t n_gx, const CoefArg& ca, int tw) {
   if (cf)
-    launch_update0<NT, FX, true>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+    launch_update0<NT, FX, true>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca, tw);
   else
-    launch_update0<NT, FX, false>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+    launch_update0<NT, FX, false>(grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca, tw);
 }
 
 static hipError_t cgs_update_any(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* coef,
                                  bool dot, double* part, int grid, hipStream_t s, bool nt, int px, const double* yx,
-                                 const double* x0, double* xo, int64_t n_gx, const CoefArg& ca) {
+                                 const double* x0, double* xo, int64_t n_gx, const CoefArg& ca, int tw = 0) {
   if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
   YArg ya;
   const bool fx = px > 0;
@@ -2068,15 +2074,15 @@ static hipError_t cgs_update_any(int64_t n, double* w, const double* Q, int64_t 
   if (cf && (dot || ca.G == nullptr)) return hipErrorInvalidValue;
   if (dot)
     hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
-                       x0, xo, n_gx, ca);
+                       x0, xo, n_gx, ca, 0);
   else if (fx && nt)
-    launch_update0c<true, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+    launch_update0c<true, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca, tw);
   else if (fx)
-    launch_update0c<false, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca);
+    launch_update0c<false, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca, tw);
   else if (nt)
-    launch_update0c<true, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca);
+    launch_update0c<true, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca, tw);
   else
-    launch_update0c<false, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca);
+    launch_update0c<false, false>(cf, grid, s, n, w, Q, pitch, nv, coef, part, 0, ya, x0, xo, n_gx, ca, tw);
   return hipGetLastError();
 }
 
@@ -2090,10 +2096,11 @@ hipError_t launch_cgs_update(int64_t n, double* w, const double* Q, int64_t pitc
 hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pitch, int nv, const double* d,
                               double* G, double* h_out, double* part, int grid, hipStream_t s, bool nt, int px,
                               const double* yx, const double* x0, double* xo, int64_t n_gx, const double* rpart,
-                              int r_in, double* r_out, unsigned long long* flag, const unsigned long long* seq) {
+                              int r_in, double* r_out, unsigned long long* flag, const unsigned long long* seq,
+                              int tw) {
   if (d == nullptr || (rpart != nullptr && (r_in < 1 || r_out == nullptr))) return hipErrorInvalidValue;
   return cgs_update_any(n, w, Q, pitch, nv, nullptr, false, part, grid, s, nt, px, yx, x0, xo, n_gx,
-                        CoefArg{d, G, h_out, rpart, r_in, r_out, flag, seq});
+                        CoefArg{d, G, h_out, rpart, r_in, r_out, flag, seq}, tw);
 }
 
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
@@ -2111,11 +2118,23 @@ hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, 
 // then cgs_update subtracts Q h with the ||w'||^2 partials (the second all-reduce) and K3
 // normalises.  Two reductions per Arnoldi step instead of MGS's j + 2; exact arithmetic is MGS's.
 // ---------------------------------------------------------------------------------------------
-template <bool NT>
+// The fold (FOLD, the default): the launch also reduces its own partials into d, so no finalize
+// launch (4.9 us + its gap per Arnoldi step at C3) sits between the dots and the update.  Each
+// workgroup publishes its partial of value i as two tagged 32-bit halves (chain_store: agent-scope
+// relaxed stores, each slot its own flag, no fence, the K2q exchange's protocol); the LAST
+// min(grid, 2 nv - 1) workgroups of the grid, dispatched after every producer, then each reduce
+// value r, r + nred, ... in sum_partials' order (thread t: partials t, t + 256, ... then
+// block_sum), so d is bitwise cgs_finalize's.  tag: a per-launch host counter (never 0), so the
+// slots need no reset; a spin bounded by kChainWaitTicks sets *err instead of hanging.
+// tw: basis vectors l < tw load with ordinary loads (they stay in the Infinity Cache, as K2q's).
+template <bool NT, bool FOLD>
 __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const double* __restrict__ w,
                                                           const double* __restrict__ Q, int64_t pitch, int nv,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part, int tw,
+                                                          unsigned long long* __restrict__ slots, unsigned tag,
+                                                          double* __restrict__ d, int zero_to, unsigned* err) {
   // rows [0, nv): q_l . w ; rows [nv, 2 nv - 1): q_l . q_{nv-1}, l < nv - 1
+  __shared__ double s_wave[4];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double acc[kCgsPerWave], acg[kCgsPerWave];
@@ -2138,8 +2157,8 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
       const int i = wid + 4 * m;
       if (i < nv) {
         const double* qv = Qw + m * step;
-        const double2 qa = ld_basis(reinterpret_cast<const double2*>(qv + e), NT);
-        const double2 qb = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT);
+        const double2 qa = ld_basis(reinterpret_cast<const double2*>(qv + e), NT && i >= tw);
+        const double2 qb = ld_basis(reinterpret_cast<const double2*>(qv + e + 128), NT && i >= tw);
         acc[m] += qa.x * wa.x;
         acc[m] += qa.y * wa.y;
         acc[m] += qb.x * wb.x;
@@ -2167,27 +2186,86 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
       }
     }
   }
+  const int gc = static_cast<int>(gridDim.x);
+  auto put = [&](int i, double t) {
+    if (FOLD) {
+      const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(t));
+      unsigned long long* sl = slots + 2 * (static_cast<int64_t>(i) * gc + blockIdx.x);
+      chain_store(sl, tag, static_cast<unsigned>(u));
+      chain_store(sl + 1, tag, static_cast<unsigned>(u >> 32));
+    } else {
+      part[static_cast<int64_t>(i) * gc + blockIdx.x] = t;
+    }
+  };
 #pragma unroll
   for (int m = 0; m < kCgsPerWave; ++m) {
     const int i = wid + 4 * m;
     if (i < nv) {
       const double t = wave_sum(acc[m]);
-      if (lane == 0) part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] = t;
+      if (lane == 0) put(i, t);
     }
     if (i < nv - 1) {
       const double t = wave_sum(acg[m]);
-      if (lane == 0) part[static_cast<int64_t>(nv + i) * gridDim.x + blockIdx.x] = t;
+      if (lane == 0) put(nv + i, t);
     }
   }
+  if (!FOLD) return;
+  const int nval = 2 * nv - 1;
+  const int nred = min(gc, nval);
+  const int r = static_cast<int>(blockIdx.x) - (gc - nred);
+  if (r < 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = r; i < nval; i += nred) {
+    const unsigned long long* sl = slots + 2 * static_cast<int64_t>(i) * gc;
+    constexpr int kPer = kRedGrid / kBlock;  // partials per thread (gc <= kRedGrid)
+    unsigned long long g[2 * kPer];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int b = threadIdx.x + k * kBlock;
+        if (b < gc) {
+          g[2 * k] = chain_load(sl + 2 * b);
+          g[2 * k + 1] = chain_load(sl + 2 * b + 1);
+          ok &= static_cast<unsigned>(g[2 * k] >> 32) == tag && static_cast<unsigned>(g[2 * k + 1] >> 32) == tag;
+        }
+      }
+      if (__all(ok)) break;
+      if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+    }
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (threadIdx.x + k * kBlock < gc)
+        v += __longlong_as_double(static_cast<long long>((g[2 * k + 1] << 32) | (g[2 * k] & 0xffffffffull)));
+    const double tot = block_sum(v, s_wave);
+    if (threadIdx.x == 0) d[i] = tot;
+  }
+  if (r == 0)
+    for (int z = nval + static_cast<int>(threadIdx.x); z < zero_to; z += kBlock) d[z] = 0.0;
 }
 
 hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t pitch, int nv, double* part, int grid,
-                           hipStream_t s, const LaunchEv* ev, bool nt) {
-  if (nv < 1 || nv > kCgsMax) return hipErrorInvalidValue;
-  if (nt)
-    launch_k(icwy_dot_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+                           hipStream_t s, const LaunchEv* ev, bool nt, int tw, unsigned long long* slots,
+                           unsigned tag, double* d, int zero_to, unsigned* err) {
+  if (nv < 1 || nv > kCgsMax || grid < 1 || grid > kRedGrid) return hipErrorInvalidValue;
+  const bool fold = slots != nullptr;
+  if (fold && (tag == 0 || d == nullptr || err == nullptr)) return hipErrorInvalidValue;
+  if (fold && nt)
+    launch_k(icwy_dot_kernel<true, true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part, tw, slots,
+             tag, d, zero_to, err);
+  else if (fold)
+    launch_k(icwy_dot_kernel<false, true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part, tw, slots,
+             tag, d, zero_to, err);
+  else if (nt)
+    launch_k(icwy_dot_kernel<true, false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part, tw, slots,
+             tag, d, zero_to, err);
   else
-    launch_k(icwy_dot_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part);
+    launch_k(icwy_dot_kernel<false, false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part, tw, slots,
+             tag, d, zero_to, err);
   return hipGetLastError();
 }
 

@@ -134,6 +134,8 @@ struct spis_context {
   int dist_mgs = 1;
   double* icwy_part = nullptr;      // 2 kCgsMax x kRedGrid partials
   double* icwy_d = nullptr;         // the 2 nv - 1 reduced dots, then (at kIcwyROff) partR
+  unsigned long long* icwy_slots = nullptr;  // K2w fold: tagged partial halves (launch_icwy_dot)
+  unsigned icwy_tag = 0;                     // the last fold's tag (never 0 on a launch)
   double* icwy_G = nullptr;         // kCgsMax x kCgsMax Gram rows G(l, m) = q_l . q_m, m < l
   double* ut_send = nullptr;        // several GPUs: the Ut rows a constraint matrix's halo sends
   size_t ut_send_len = 0;
@@ -522,6 +524,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
     HIP_TRY(hipMalloc(&c->icwy_part, sizeof(double) * 2 * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->icwy_d, sizeof(double) * (kIcwyROff + np)));
+    HIP_TRY(hipMalloc(&c->icwy_slots, sizeof(unsigned long long) * 2 * (2 * kCgsMax - 1) * kRedGrid));
+    HIP_TRY(hipMemset(c->icwy_slots, 0, sizeof(unsigned long long) * 2 * (2 * kCgsMax - 1) * kRedGrid));
     HIP_TRY(hipMemset(c->icwy_d, 0, sizeof(double) * (kIcwyROff + np)));
     c->partR = c->icwy_d + kIcwyROff;
     HIP_TRY(hipMalloc(&c->icwy_G, sizeof(double) * kCgsMax * kCgsMax));
@@ -592,6 +596,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->cgs_c);
     (void)hipFree(c->icwy_part);
     (void)hipFree(c->icwy_d);
+    (void)hipFree(c->icwy_slots);
     (void)hipFree(c->icwy_G);
     (void)hipFree(c->ut_send);
     (void)hipFree(c->chain_gran);
@@ -1867,6 +1872,9 @@ struct Solver {
   int gs;  // SpMV partial count
   int gb;  // BLAS-1 partial count
   std::vector<double> hostq, hostz;
+  // A/B switches for the K2w fold and its temporal window (tools/r04_ab.sh)
+  const bool k2w_fold = std::getenv("SPIS_K2W_FOLD") == nullptr || std::atoi(std::getenv("SPIS_K2W_FOLD")) != 0;
+  const int k2w_tw = std::getenv("SPIS_K2W_TW") != nullptr ? std::atoi(std::getenv("SPIS_K2W_TW")) : -1;
 
   double* Qv(int i) const { return ws->Q + static_cast<int64_t>(i) * ws->pitch; }
   double* Zv(int i) const { return ws->Zb + static_cast<int64_t>(i) * ws->pitch; }
@@ -1981,6 +1989,17 @@ struct Solver {
     return exchange(c, A, zj);
   }
 
+  // with nontemporal basis loads, the first basis vectors (which every later step re-reads) and x0
+  // keep ordinary loads while they fit the Infinity Cache beside the matrix and ~6 working vectors
+  // (C3: 6 of them; chain mean 43.0 -> 42.4 us, the dual unchanged at 36.0 us; 10 evicted part of
+  // the matrix: dual 38.4 us; gpurun_out/r04ab1)
+  int chain_tw(bool nt) const {
+    if (!nt) return 0;
+    const double mat = 12.0 * A->nnz + 4.0 * (A->n_rows + 1), vec = 8.0 * static_cast<double>(n);
+    const double room = 256.0 * 1024 * 1024 - mat - 6.0 * vec;
+    return room <= 0.0 ? 0 : static_cast<int>(std::min(6.0, std::floor(room / vec)));
+  }
+
   // (xpart, x_out, done): the first MGS step also reduces the previous update's residual partials
   // into host memory and carries that update's completion event (single GPU, fused path)
   // (yx, jx): K2q only — the chain also computes U_jx's GEMV x_jx = Z[:, :jx+1] yx + x0 (L mode)
@@ -2006,16 +2025,6 @@ struct Solver {
     // chain +1-2 us, +2.9%; C4, whose working set fits, measured 1% slower with them)
     const double ws_bytes = 12.0 * A->nnz + 4.0 * (A->n_rows + 1) + 8.0 * (k + 1) * static_cast<double>(n);
     const bool nt_chain = c->nt_basis == 1 || (c->nt_basis == 2 && ws_bytes > 256.0 * 1024 * 1024);
-    // with nontemporal loads, the first basis vectors (which every later chain re-reads) and x0 keep
-    // ordinary loads while they fit the Infinity Cache beside the matrix and ~6 working vectors
-    // (C3: 6 of them; chain mean 43.0 -> 42.4 us, the dual unchanged at 36.0 us; 10 evicted part of
-    // the matrix: dual 38.4 us; gpurun_out/r04ab1)
-    auto chain_tw = [&](bool nt) {
-      if (!nt) return 0;
-      const double mat = 12.0 * A->nnz + 4.0 * (A->n_rows + 1), vec = 8.0 * static_cast<double>(n);
-      const double room = 256.0 * 1024 * 1024 - mat - 6.0 * vec;
-      return room <= 0.0 ? 0 : static_cast<int>(std::min(6.0, std::floor(room / vec)));
-    };
     if (!fixed_grid(c) && c->mgs_chain && mgs_chain_fits(n, agg)) {  // K2p: the chain in one launch
       const LaunchEv both{e_first.start, e_last.stop};
       if (lag_chain()) arm_hcol(j);
@@ -2069,9 +2078,16 @@ struct Solver {
     const LaunchEv e_first = pm.first(), e_last = pm.last();
     double* d = c->icwy_d;
     const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
-    HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt));
+    const int tw = k2w_tw >= 0 ? k2w_tw : chain_tw(nt);
     // (merged: the slack between the dots and partR is zeroed, since the all-reduce sums it too)
-    HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s, merged ? kIcwyROff : 0));
+    if (k2w_fold) {  // the dots reduced into d by the same launch (no finalize launch)
+      if (++c->icwy_tag == 0) c->icwy_tag = 1;
+      HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, nullptr, gc, s, &e_first, nt, tw, c->icwy_slots,
+                              c->icwy_tag, d, merged ? kIcwyROff : 0, c->chain_err_dev));
+    } else {
+      HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_part, gc, s, &e_first, nt, tw));
+      HIP_TRY(launch_cgs_finalize(c->icwy_part, gc, 2 * nv - 1, d, nullptr, nullptr, s, merged ? kIcwyROff : 0));
+    }
     if (merged) {
       ST_TRY(allreduce(c, d, kIcwyROff + gs));  // [d | slack | partR]; partR reduced by the update
     } else {
@@ -2082,7 +2098,7 @@ struct Solver {
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
     if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
     HIP_TRY(launch_icwy_update(n, ws->w, Qv(0), ws->pitch, nv, d, c->icwy_G, hcol, c->partB, gc, s, nt, px, yx,
-                               ws->x0, px > 0 ? xbuf(jx) : nullptr, n_gx(), xpart, gs, x_out, flag, seq));
+                               ws->x0, px > 0 ? xbuf(jx) : nullptr, n_gx(), xpart, gs, x_out, flag, seq, tw));
     // ||w'||^2: the gc partials all-reduced element-wise (8 KB, latency-bound like one double) and
     // summed in fixed order by every normalize workgroup: no finalize launch in between
     ST_TRY(allreduce(c, c->partB, gc));

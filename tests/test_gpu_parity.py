@@ -1314,3 +1314,38 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
         # orthogonality: MGS's own loss, the same with either grouping of the partial dots
         loss = np.abs(Q @ Q.T - np.eye(k)).max()
         assert loss <= 4 * loss0 + 1e-14, (loss, loss0)
+
+
+@pytest.mark.parametrize("n", [1001, 70_001, 1_002_252])
+def test_k2w_fold_bit_identical(spis, n, monkeypatch):
+    """K2w's folded dot pass (the launch's last workgroups reduce the tagged partials into d, no
+    finalize launch) against the dot pass + cgs_finalize: the same summation order, so the
+    solves are bitwise equal.  n = 1001: 16 workgroups for up to 2 k - 1 = 23 values, so each
+    reducing workgroup takes several; 1,002,252: the full 1024-workgroup grid at C3's size, with
+    the temporal window on and off.  Repeated solves reuse the tag slots (a fresh tag per launch)."""
+    from structurepreservingiterativesolvers_amd import _lib, solvers
+    from structurepreservingiterativesolvers_amd.device import get_context
+
+    ctx = get_context()
+    rng = np.random.default_rng(n)
+    A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
+                   0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
+    b = rng.standard_normal(n)
+    k = 12
+    runs = []
+    _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 4), "spis_set_option")
+    try:
+        for fold, tw in ((0, None), (1, None), (1, None), (1, "0"), (0, "0")):
+            monkeypatch.setenv("SPIS_K2W_FOLD", str(fold))
+            if tw is None:
+                monkeypatch.delenv("SPIS_K2W_TW", raising=False)
+            else:
+                monkeypatch.setenv("SPIS_K2W_TW", tw)
+            x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
+            runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
+    finally:
+        _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 3), "spis_set_option")
+    xa, ra, Qa = runs[0]
+    assert ra[-1] < 1e-3 * ra[0]
+    for xb, rb, Qb in runs[1:]:
+        assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)

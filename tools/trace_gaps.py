@@ -6,7 +6,7 @@ import sys
 KEYS = ['mgs_chain', 'spmv_pipe_kernel<2048, 4', 'spmv_pipe_kernel<2048, 3', 'spmv_pipe_kernel<2048, 1',
         'spmv_pipe_kernel<2048, 2', 'spmv_dual', 'mgs_step', 'spmv_rowblock_kernel<1>', 'spmv_rowblock_kernel<2>', 'spmv_rowblock_kernel<3>',
         'spmv_rowblock_kernel<0>', 'constraint_gram', 'gemv', 'normalize', 'transpose', 'gram_reduce',
-        'copy_kernel', 'fillBuffer', 'copyBuffer', 'dot', 'finalize']
+        'copy_kernel', 'fillBuffer', 'copyBuffer', 'icwy_dot', 'cgs_update', 'cgs_finalize', 'finalize2', 'dot', 'finalize', 'gather']
 
 
 def short(n):
