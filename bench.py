@@ -60,12 +60,16 @@ def mgs_chain_bytes(n, k, chain):
       one-reduce two-pass MGS (chain 4, and chain 3 beyond K2q): 8 N (j + 2) for the dots (w,
           q_0 .. q_j) + 8 N (j + 3) for the update (q_0 .. q_j and w read, w written) + 16 N for
           the update GEMV it carries from j >= 1 + 16 N for the normalise;
+      its one-launch form K2s (chain 3 or 4, N <= 262,144, k <= 32: spis.cpp k2w_small): 8 N
+          (j + 2) (w, q_0 .. q_j read once) + 16 N (w' and q_{j+1} written) + 16 N for the GEMV;
       per-step launches (chain 0): 32 N (j + 1) + 16 N (y, q_i, q_{i+1} read, y written; the
           normalise reads y, writes q)."""
     tot = 0.0
     k2q = (n + 1) // 2 <= 255 * 512 * 4
     for j in range(k):
-        if chain == 4 or (chain == 3 and not k2q):
+        if k2s_used(n, k, chain):
+            b = 8 * n * (j + 2) + 16 * n + (16 * n if j >= 1 else 0)
+        elif chain == 4 or (chain == 3 and not k2q):
             b = 8 * n * (j + 2) + 8 * n * (j + 3) + (16 * n if j >= 1 else 0) + 16 * n
         elif chain == 3:
             b = 8 * n * (j + 3) + (16 * n if j >= 1 else 0)
@@ -77,6 +81,12 @@ def mgs_chain_bytes(n, k, chain):
             b = 32 * n * (j + 1) + 16 * n
         tot += b
     return tot / k
+
+
+def k2s_used(n, k, chain):
+    """One GPU: does the library take K2s, the one-launch one-reduce MGS (spis.cpp k2w_small and
+    arnoldi_post_icwy: chain 3 or 4, k <= 32, N within its 1024 resident 256-row workgroups)?"""
+    return chain in (3, 4) and k <= 32 and n <= 256 * 1024
 
 
 def dual_bytes(n_rows, nnz, col_bytes=4):
@@ -342,6 +352,8 @@ def main():
                   4: "icwy_dot + cgs_update + normalise (K2w: one-reduce two-pass MGS)"}.get(args.chain, "MGS chain")
     if args.chain == 3 and (n + 1) // 2 > 255 * 512 * 4:
         chain_name = "icwy_dot + cgs_update + normalise (K2w: one-reduce two-pass MGS, beyond K2q's capacity)"
+    if args.orthog == "mgs" and k2s_used(n, args.k, args.chain):
+        chain_name = "icwy_onepass_kernel (K2s: one-reduce MGS in one launch, basis slices in registers)"
     roof_mgs = {"kernel": chain_name + ": solvers.py:193-198 (+ the update GEMV of :287)", "bound": "hbm",
                 "achieved": mgs_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": None if mgs_gbs is None else mgs_gbs / HBM_PEAK_GBS,

@@ -161,6 +161,19 @@ hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pit
                               double* xo = nullptr, int64_t n_gx = 0, const double* rpart = nullptr, int r_in = 0,
                               double* r_out = nullptr, unsigned long long* flag = nullptr,
                               const unsigned long long* seq = nullptr, int tw = 0);
+// K2s (one GPU, n <= 256 icwy_onepass_max_grid()): K2w's dot pass, coefficients, update (with the
+// fused GEMV for px > 0 and the residual hand-off as launch_icwy_update), norm and normalise in
+// one launch over register-resident basis slices; h_col: the H column (H[nv, nv-1] included);
+// slots: (2 (2 kCgsMax - 1) + 2) kRedGrid + 4 kCgsMax words; tag: fresh nonzero per launch
+constexpr int64_t kIcwySlotWords = 2 * (2 * kCgsMax - 1) * static_cast<int64_t>(kRedGrid) + 2 * (2 * kCgsMax - 1) +
+                                   2 * static_cast<int64_t>(kRedGrid) + 2;
+int icwy_onepass_max_grid();
+hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pitch, int nv, double* G, double* h_col,
+                               unsigned long long* slots, unsigned tag, unsigned* err, hipStream_t s,
+                               const LaunchEv* ev, int px = 0, const double* yx = nullptr,
+                               const double* x0 = nullptr, double* xo = nullptr, const double* rpart = nullptr,
+                               int r_in = 0, double* r_out = nullptr, unsigned long long* flag = nullptr,
+                               const unsigned long long* seq = nullptr);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s, int zero_to = 0);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM

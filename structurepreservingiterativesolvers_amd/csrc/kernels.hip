@@ -1731,7 +1731,7 @@ hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const dou
 constexpr int kCgsPerWave = kCgsMax / (kBlock / 64);
 constexpr int kCgsChunk = 256;
 
-__device__ __forceinline__ bool aligned16d(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+__host__ __device__ __forceinline__ bool aligned16d(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 __global__ __launch_bounds__(kBlock) void cgs_dot_kernel(int64_t n, const double* __restrict__ w,
                                                          const double* __restrict__ Q, int64_t pitch, int nv,
@@ -1815,7 +1815,8 @@ __device__ __forceinline__ void icwy_coefficients(const CoefArg ca, int nv, doub
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const bool writer = blockIdx.x == 0;
-  for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = ca.d[i];
+  if (ca.d != nullptr)  // (else the caller staged the dots in s_d: K2s)
+    for (int i = threadIdx.x; i < 2 * nv - 1; i += kBlock) s_d[i] = ca.d[i];
   for (int i = 1 + wid; i < nv - 1; i += kBlock / 64)
     if (lane < i) s_gt[i * (i - 1) / 2 + lane] = ca.G[static_cast<int64_t>(i) * kCgsMax + lane];
   __syncthreads();
@@ -2266,6 +2267,296 @@ hipError_t launch_icwy_dot(int64_t n, const double* w, const double* Q, int64_t 
   else
     launch_k(icwy_dot_kernel<false, false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, pitch, nv, part, tw, slots,
              tag, d, zero_to, err);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2s: K2w in ONE launch and ONE pass over the basis, for small N on one GPU.  Each workgroup owns
+// one 256-element chunk (grid = ceil(n / 256), every workgroup resident at once: the host checks
+// the occupancy), and its four waves keep their basis vectors' slices of it in registers from the
+// dots to the update:
+//   1. the dots of icwy_dot (q_l . w, q_l . q_{nv-1}) -> tagged partial slots (as the fold);
+//   2. the last min(grid, 2 nv - 1) workgroups reduce them (sum_partials' order) and publish each
+//      reduced dot as tagged halves; every workgroup polls the 2 nv - 1 of them;
+//   3. icwy_coefficients (every workgroup the same bits; workgroup 0 writes G's row and H[:, j]);
+//   4. cgs_update's arithmetic on the register slices: w' (stored), the fused GEMV, ||w'||^2
+//      partial -> tagged slot;
+//   5. the last workgroup reduces the norm partials and publishes ||w'||^2; every workgroup forms
+//      q_{j+1} = w' / ||w'|| as normalize_kernel does (workgroup 0: H[j+1, j] to the host).
+// For n a multiple of 256 (n <= 262,144) the two-pass launches group every partial and every sum
+// the same way (tests/test_gpu_parity.py: bitwise equal solves at n = 65,536; at 196,608 one
+// step's ||w'|| differs in its last bit, cause not found); otherwise the last chunk's elements are
+// grouped differently (the two-pass kernels take them in a scalar tail): roundoff.
+// Spins are bounded (kChainWaitTicks) and set *err, as the chain's.
+// slots: [P: 2 (2 kCgsMax - 1) kRedGrid][D: 2 (2 kCgsMax - 1)][N: 2 kRedGrid][H: 2] words.
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t kOnePassP = 2 * (2 * kCgsMax - 1) * static_cast<int64_t>(kRedGrid);
+constexpr int64_t kOnePassD = kOnePassP;
+constexpr int64_t kOnePassN = kOnePassD + 2 * (2 * kCgsMax - 1);
+constexpr int64_t kOnePassH = kOnePassN + 2 * kRedGrid;
+
+__device__ __forceinline__ void tag_put(unsigned long long* sl, unsigned tag, double v) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(v));
+  chain_store(sl, tag, static_cast<unsigned>(u));
+  chain_store(sl + 1, tag, static_cast<unsigned>(u >> 32));
+}
+// one lane's tagged double: spins until both halves carry tag (false: timed out, *err set)
+__device__ __forceinline__ bool tag_get(const unsigned long long* sl, unsigned tag, double* v,
+                                        unsigned long long t0, unsigned* err) {
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned long long lo = chain_load(sl), hi = chain_load(sl + 1);
+    if (static_cast<unsigned>(lo >> 32) == tag && static_cast<unsigned>(hi >> 32) == tag) {
+      *v = __longlong_as_double(static_cast<long long>((hi << 32) | (lo & 0xffffffffull)));
+      return true;
+    }
+    if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
+      atomicOr(err, 1u);
+      *v = 0.0;
+      return false;
+    }
+  }
+}
+// the workgroup sums grid (<= kRedGrid) tagged partials (slot pairs at sl + 2 b) in sum_partials'
+// order; each thread's slots are loaded together and re-polled until all carry tag
+__device__ __forceinline__ double tag_sum(const unsigned long long* sl, int grid, unsigned tag, double* s_wave,
+                                          unsigned long long t0, unsigned* err) {
+  constexpr int kPer = kRedGrid / kBlock;
+  unsigned long long g[2 * kPer];
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = threadIdx.x + k * kBlock;
+      if (b < grid) {
+        g[2 * k] = chain_load(sl + 2 * b);
+        g[2 * k + 1] = chain_load(sl + 2 * b + 1);
+        ok &= static_cast<unsigned>(g[2 * k] >> 32) == tag && static_cast<unsigned>(g[2 * k + 1] >> 32) == tag;
+      }
+    }
+    if (__all(ok)) break;
+    if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
+      if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
+      break;
+    }
+  }
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    if (threadIdx.x + k * kBlock < grid)
+      v += __longlong_as_double(static_cast<long long>((g[2 * k + 1] << 32) | (g[2 * k] & 0xffffffffull)));
+  return block_sum(v, s_wave);
+}
+
+template <bool FX>
+__global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, double* __restrict__ w,
+                                                              const double* __restrict__ Q, double* __restrict__ qn,
+                                                              int64_t pitch, int nv, unsigned long long* slots,
+                                                              unsigned tag, unsigned* err, CoefArg ca, int px,
+                                                              YArg yx, const double* __restrict__ x0,
+                                                              double* __restrict__ xo, double* h_out) {
+  __shared__ double s_c[kCgsMax];
+  __shared__ double s_sum[4][4][64];
+  __shared__ double s_x[FX ? 4 : 1][4][64];
+  __shared__ double s_wave[4];
+  __shared__ double s_gt[kGramTri];
+  __shared__ double s_d[2 * kCgsMax];
+  __shared__ double s_h;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grid = static_cast<int>(gridDim.x);
+  const int nval = 2 * nv - 1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kCgsChunk + 2 * lane;  // e, e+1, e+128, e+129
+  auto ld2 = [&](const double* p, int64_t i) -> double2 {
+    if (i + 1 < n) return *reinterpret_cast<const double2*>(p + i);
+    return make_double2(i < n ? p[i] : 0.0, 0.0);
+  };
+  auto st2 = [&](double* p, int64_t i, double a, double b) {
+    if (i + 1 < n)
+      *reinterpret_cast<double2*>(p + i) = make_double2(a, b);
+    else if (i < n)
+      p[i] = a;
+  };
+  const double* Qw = Q + wid * pitch;
+  const int64_t step = 4 * pitch;
+  const double2 wa = ld2(w, e), wb = ld2(w, e + 128);
+  double2 ba = make_double2(0.0, 0.0), bb = make_double2(0.0, 0.0);
+  if (FX && wid == 1) {
+    ba = ld2(x0, e);
+    bb = ld2(x0, e + 128);
+  }
+  double2 qa[kCgsPerWave], qb[kCgsPerWave];
+  {
+    const double* ql = Q + static_cast<int64_t>(nv - 1) * pitch;
+    const double2 la = ld2(ql, e), lb = ld2(ql, e + 128);
+    // 1. the dots, icwy_dot's arithmetic
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nv) {
+        qa[m] = ld2(Qw + m * step, e);
+        qb[m] = ld2(Qw + m * step, e + 128);
+      } else {
+        qa[m] = make_double2(0.0, 0.0);
+        qb[m] = make_double2(0.0, 0.0);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nv) {
+        double acc = 0.0, acg = 0.0;
+        acc += qa[m].x * wa.x;
+        acc += qa[m].y * wa.y;
+        acc += qb[m].x * wb.x;
+        acc += qb[m].y * wb.y;
+        acc = wave_sum(acc);
+        if (lane == 0) tag_put(slots + 2 * (static_cast<int64_t>(i) * grid + blockIdx.x), tag, acc);
+        if (i < nv - 1) {
+          acg += qa[m].x * la.x;
+          acg += qa[m].y * la.y;
+          acg += qb[m].x * lb.x;
+          acg += qb[m].y * lb.y;
+          acg = wave_sum(acg);
+          if (lane == 0) tag_put(slots + 2 * (static_cast<int64_t>(nv + i) * grid + blockIdx.x), tag, acg);
+        }
+      }
+    }
+  }
+  // 2. the last workgroups reduce the dots and publish them; everyone polls
+  const int nred = min(grid, nval);
+  const int r = static_cast<int>(blockIdx.x) - (grid - nred);
+  if (r >= 0)
+    for (int i = r; i < nval; i += nred) {
+      const double tot = tag_sum(slots + 2 * static_cast<int64_t>(i) * grid, grid, tag, s_wave, t0, err);
+      if (threadIdx.x == 0) tag_put(slots + kOnePassD + 2 * i, tag, tot);
+    }
+  if (threadIdx.x < nval) tag_get(slots + kOnePassD + 2 * threadIdx.x, tag, &s_d[threadIdx.x], t0, err);
+  __syncthreads();
+  // 3. the coefficients (d already in s_d: ca.d == nullptr)
+  icwy_coefficients(ca, nv, s_c, s_gt, s_d);
+  if (ca.rpart != nullptr && blockIdx.x == 0) {
+    const double t = sum_partials(ca.rpart, ca.r_in, s_wave);
+    if (threadIdx.x == 0) publish(ca.r_out, t, ca.flag, ca.seq);
+  }
+  // 4. cgs_update's arithmetic on the register slices
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+#pragma unroll
+  for (int m = 0; m < kCgsPerWave; ++m) {
+    if (wid + 4 * m < nv) {
+      const double cm = s_c[wid + 4 * m];
+      p0 += cm * qa[m].x;
+      p1 += cm * qa[m].y;
+      p2 += cm * qb[m].x;
+      p3 += cm * qb[m].y;
+      if (FX && wid + 4 * m < px) {
+        const double ym = yx.v[wid + 4 * m];
+        g0 = fma(ym, qa[m].x, g0);
+        g1 = fma(ym, qa[m].y, g1);
+        g2 = fma(ym, qb[m].x, g2);
+        g3 = fma(ym, qb[m].y, g3);
+      }
+    }
+  }
+  s_sum[wid][0][lane] = p0;
+  s_sum[wid][1][lane] = p1;
+  s_sum[wid][2][lane] = p2;
+  s_sum[wid][3][lane] = p3;
+  if (FX) {
+    s_x[wid][0][lane] = g0;
+    s_x[wid][1][lane] = g1;
+    s_x[wid][2][lane] = g2;
+    s_x[wid][3][lane] = g3;
+  }
+  __syncthreads();
+  double t[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = (((s_sum[0][k][lane] + s_sum[1][k][lane]) + s_sum[2][k][lane]) + s_sum[3][k][lane]);
+  t[0] = wa.x - t[0];
+  t[1] = wa.y - t[1];
+  t[2] = wb.x - t[2];
+  t[3] = wb.y - t[3];
+  // the tail of a chunk past n holds zeros (ld2), so its t are 0 and add nothing below
+  if (wid == 0) {
+    st2(w, e, t[0], t[1]);
+    st2(w, e + 128, t[2], t[3]);
+  }
+  if (FX && wid == 1) {
+    double xs[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
+    st2(xo, e, xs[0] + ba.x, xs[1] + ba.y);
+    st2(xo, e + 128, xs[2] + bb.x, xs[3] + bb.y);
+  }
+  double a0 = 0.0;
+  if (wid == 0) {
+    a0 += t[0] * t[0];
+    a0 += t[1] * t[1];
+    a0 += t[2] * t[2];
+    a0 += t[3] * t[3];
+  }
+  const double part = block_sum(a0, s_wave);
+  if (threadIdx.x == 0) tag_put(slots + kOnePassN + 2 * blockIdx.x, tag, part);
+  // 5. ||w'||^2 by the last workgroup, then q_{j+1} = w' / ||w'|| everywhere
+  if (static_cast<int>(blockIdx.x) == grid - 1) {
+    const double hn = tag_sum(slots + kOnePassN, grid, tag, s_wave, t0, err);
+    if (threadIdx.x == 0) tag_put(slots + kOnePassH, tag, hn);
+  }
+  if (threadIdx.x == 0) {
+    double hn;
+    tag_get(slots + kOnePassH, tag, &hn, t0, err);
+    s_h = sqrt(hn);
+  }
+  __syncthreads();
+  const double h = s_h;
+  if (blockIdx.x == 0 && threadIdx.x == 0) pin_store(h_out, h);
+  if (wid == 0) {
+    st2(qn, e, h == 0.0 ? 0.0 : t[0] / h, h == 0.0 ? 0.0 : t[1] / h);
+    st2(qn, e + 128, h == 0.0 ? 0.0 : t[2] / h, h == 0.0 ? 0.0 : t[3] / h);
+  }
+}
+
+int icwy_onepass_max_grid() {
+  static int cap = -1;
+  if (cap < 0) {
+    int dev = 0, cus = 0, per = 0, per_fx = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, icwy_onepass_kernel<false>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fx, icwy_onepass_kernel<true>, kBlock, 0) != hipSuccess)
+      return 0;
+    // every workgroup must be resident at once.  A kernel running beside it on another stream (the
+    // side-stream GEMV) only delays the last workgroups' placement: it waits on nothing in here
+    cap = std::min<int>(kRedGrid, cus * std::min(per, per_fx));
+  }
+  return cap;
+}
+
+hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pitch, int nv, double* G, double* h_col,
+                               unsigned long long* slots, unsigned tag, unsigned* err, hipStream_t s,
+                               const LaunchEv* ev, int px, const double* yx, const double* x0, double* xo,
+                               const double* rpart, int r_in, double* r_out, unsigned long long* flag,
+                               const unsigned long long* seq) {
+  const int64_t grid = (n + kCgsChunk - 1) / kCgsChunk;
+  if (nv < 1 || nv > kCgsMax || n < 1 || grid > icwy_onepass_max_grid() || tag == 0 || slots == nullptr ||
+      err == nullptr || G == nullptr || h_col == nullptr || !aligned16d(w) || !aligned16d(Q) || pitch % 2 != 0 ||
+      (rpart != nullptr && (r_in < 1 || r_out == nullptr)))
+    return hipErrorInvalidValue;
+  YArg ya;
+  if (px > 0) {
+    if (px > nv || px > kYArg || yx == nullptr || x0 == nullptr || xo == nullptr || !aligned16d(x0) || !aligned16d(xo))
+      return hipErrorInvalidValue;
+    for (int i = 0; i < px; ++i) ya.v[i] = yx[i];
+  }
+  const CoefArg ca{nullptr, G, h_col, rpart, r_in, r_out, flag, seq};
+  double* qn = const_cast<double*>(Q) + static_cast<int64_t>(nv) * pitch;
+  if (px > 0)
+    launch_k(icwy_onepass_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, qn, pitch, nv, slots, tag, err,
+             ca, px, ya, x0, xo, h_col + nv);
+  else
+    launch_k(icwy_onepass_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, qn, pitch, nv, slots, tag, err,
+             ca, 0, ya, x0, xo, h_col + nv);
   return hipGetLastError();
 }
 

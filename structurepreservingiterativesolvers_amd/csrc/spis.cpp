@@ -134,7 +134,7 @@ struct spis_context {
   int dist_mgs = 1;
   double* icwy_part = nullptr;      // 2 kCgsMax x kRedGrid partials
   double* icwy_d = nullptr;         // the 2 nv - 1 reduced dots, then (at kIcwyROff) partR
-  unsigned long long* icwy_slots = nullptr;  // K2w fold: tagged partial halves (launch_icwy_dot)
+  unsigned long long* icwy_slots = nullptr;  // K2w fold / K2s: tagged partial halves (kIcwySlotWords)
   unsigned icwy_tag = 0;                     // the last fold's tag (never 0 on a launch)
   double* icwy_G = nullptr;         // kCgsMax x kCgsMax Gram rows G(l, m) = q_l . q_m, m < l
   double* ut_send = nullptr;        // several GPUs: the Ut rows a constraint matrix's halo sends
@@ -524,8 +524,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMalloc(&c->cgs_c, sizeof(double) * 2 * kCgsMax));
     HIP_TRY(hipMalloc(&c->icwy_part, sizeof(double) * 2 * kCgsMax * kRedGrid));
     HIP_TRY(hipMalloc(&c->icwy_d, sizeof(double) * (kIcwyROff + np)));
-    HIP_TRY(hipMalloc(&c->icwy_slots, sizeof(unsigned long long) * 2 * (2 * kCgsMax - 1) * kRedGrid));
-    HIP_TRY(hipMemset(c->icwy_slots, 0, sizeof(unsigned long long) * 2 * (2 * kCgsMax - 1) * kRedGrid));
+    HIP_TRY(hipMalloc(&c->icwy_slots, sizeof(unsigned long long) * kIcwySlotWords));
+    HIP_TRY(hipMemset(c->icwy_slots, 0, sizeof(unsigned long long) * kIcwySlotWords));
     HIP_TRY(hipMemset(c->icwy_d, 0, sizeof(double) * (kIcwyROff + np)));
     c->partR = c->icwy_d + kIcwyROff;
     HIP_TRY(hipMalloc(&c->icwy_G, sizeof(double) * kCgsMax * kCgsMax));
@@ -1872,9 +1872,13 @@ struct Solver {
   int gs;  // SpMV partial count
   int gb;  // BLAS-1 partial count
   std::vector<double> hostq, hostz;
-  // A/B switches for the K2w fold and its temporal window (tools/r04_ab.sh)
+  // A/B switches (tests and tools/r04_*.sh): the K2w fold, its temporal window, K2s, and the
+  // small-N threshold for K2w at SPIS_OPT_MGS_CHAIN 3 (0: K2q at every N)
   const bool k2w_fold = std::getenv("SPIS_K2W_FOLD") == nullptr || std::atoi(std::getenv("SPIS_K2W_FOLD")) != 0;
   const int k2w_tw = std::getenv("SPIS_K2W_TW") != nullptr ? std::atoi(std::getenv("SPIS_K2W_TW")) : -1;
+  const bool k2w_onepass = std::getenv("SPIS_K2W_ONEPASS") == nullptr || std::atoi(std::getenv("SPIS_K2W_ONEPASS")) != 0;
+  const int64_t k2w_small_n = std::getenv("SPIS_K2W_SMALL_N") != nullptr ? std::atoll(std::getenv("SPIS_K2W_SMALL_N"))
+                                                                         : -1;  // -1: where K2s fits
 
   double* Qv(int i) const { return ws->Q + static_cast<int64_t>(i) * ws->pitch; }
   double* Zv(int i) const { return ws->Zb + static_cast<int64_t>(i) * ws->pitch; }
@@ -1935,7 +1939,18 @@ struct Solver {
   // K2q's capacity: two passes over the basis per step, the second carrying the update GEMV, in
   // place of K2b + a separate GEMV pass (C5: 826 -> 902 it/s; FX does not fit K2b's registers)
   bool icwy_on() const {
-    return c->comm ? c->dist_mgs == 1 : (c->mgs_chain == 4 || (c->mgs_chain == 3 && !c->cgs2 && !k2q_fits()));
+    return c->comm ? c->dist_mgs == 1
+                   : (c->mgs_chain == 4 || (c->mgs_chain == 3 && !c->cgs2 && !k2q_fits()) || k2w_small());
+  }
+  // small N: K2q's per-MGS-step exchanges are latency, not bandwidth; K2s (K2w in one launch over
+  // register-resident basis slices) wins wherever it fits (lkdv, N = 100,002: MGS 29.1 -> 18.0 us,
+  // 22,272 -> 26,485-28,246 it/s; 200,004: +3-7%; 250,002: +6.6%; gpurun_out/r04k2s), while
+  // K2w's two launches lose to K2q from N = 250,000 on (gpurun_out/r04k2ws2): so K2w is taken at
+  // small N only where K2s fits (n <= 256 icwy_onepass_max_grid(), <= 262,144).  Every step must
+  // take it (k <= kCgsMax): a later K2q step would read Gram entries (chain_gsub) it never wrote
+  bool k2w_small() const {
+    const int64_t cap = k2w_small_n >= 0 ? k2w_small_n : 256 * static_cast<int64_t>(icwy_onepass_max_grid());
+    return c->mgs_chain == 3 && !c->cgs2 && k <= kCgsMax && n <= cap;
   }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
   void arm_hcol(int j) {  // before A_j's chain is enqueued: every slot of H[:, j] (pin_store)
@@ -2078,6 +2093,17 @@ struct Solver {
     const LaunchEv e_first = pm.first(), e_last = pm.last();
     double* d = c->icwy_d;
     const bool nt = nt_basis_on();  // the matrix stays Infinity-Cache resident for the next SpMV
+    const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
+    if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
+    // K2s: one GPU, small N: the whole step in one launch, the basis slices held in registers
+    if (!c->comm && k2w_onepass && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
+      if (++c->icwy_tag == 0) c->icwy_tag = 1;
+      const LaunchEv both{e_first.start, e_last.stop};
+      HIP_TRY(launch_icwy_onepass(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_G, hcol, c->icwy_slots, c->icwy_tag,
+                                  c->chain_err_dev, s, &both, px, yx, ws->x0, px > 0 ? xbuf(jx) : nullptr, xpart, gs,
+                                  x_out, flag, seq));
+      return SPIS_OK;
+    }
     const int tw = k2w_tw >= 0 ? k2w_tw : chain_tw(nt);
     // (merged: the slack between the dots and partR is zeroed, since the all-reduce sums it too)
     if (k2w_fold) {  // the dots reduced into d by the same launch (no finalize launch)
@@ -2095,8 +2121,6 @@ struct Solver {
     }
     // the coefficients h (and H[0..j, j]) in the update's prologue; L mode: U_jx's GEMV in the same
     // pass (x_jx = Z y + x0 over the local and ghost rows)
-    const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
-    if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
     HIP_TRY(launch_icwy_update(n, ws->w, Qv(0), ws->pitch, nv, d, c->icwy_G, hcol, c->partB, gc, s, nt, px, yx,
                                ws->x0, px > 0 ? xbuf(jx) : nullptr, n_gx(), xpart, gs, x_out, flag, seq, tw));
     // ||w'||^2: the gc partials all-reduced element-wise (8 KB, latency-bound like one double) and

@@ -17,6 +17,7 @@ Tolerances (fp64):
 * constraint deviation of the CGMRES solution: |c_i(x)| <= 1e-12 * scale.
 """
 import logging
+import os
 import warnings
 
 import numpy as np
@@ -282,11 +283,16 @@ def _run_package(spis, case):
 
 
 @pytest.fixture(params=["aggregator", "pipelined", "one_reduce"])
-def chain_mode(request, spis):
+def chain_mode(request, spis, monkeypatch):
     """The pipelined MGS chain (the default, SPIS_OPT_MGS_CHAIN = 3), the plain one (2), and the
-    one-reduce two-pass MGS with the fused update GEMV (4: the several-GPU kernels on one GPU)."""
+    one-reduce two-pass MGS with the fused update GEMV (4: the several-GPU kernels on one GPU).
+    The default takes the one-reduce MGS in its one-launch form (K2s) for N <= 262,144 (k <= 32):
+    "pipelined" forces K2q there
+    (SPIS_K2W_SMALL_N = 0), so both kernels stay covered at every size."""
     from structurepreservingiterativesolvers_amd.device import set_option
 
+    if request.param == "pipelined":
+        monkeypatch.setenv("SPIS_K2W_SMALL_N", "0")
     set_option("mgs_chain", request.param)
     yield request.param
     set_option("mgs_chain", True)
@@ -501,8 +507,9 @@ def test_paired_last_residuals_bit_identical(spis):
 def test_fused_dual_spmv_bit_identical(spis):
     """SPIS_OPT_FUSE_SPMV: the true-residual SpMV of U_j fused with the Arnoldi SpMV of A_{j+2}
     (matrix read once) gives bit-identical iterates, residuals, LS solutions and basis, in the
-    L-mode schedule (the default chain) and in the plain pipelined one (the aggregator chain,
-    where the update GEMV runs on the side stream)."""
+    L-mode schedule (the pipelined chain K2q) and in the plain pipelined one (the aggregator
+    chain, where the update GEMV runs on the side stream); the default's one-reduce MGS at these
+    small N to roundoff (its fused GEMV sums in another order)."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
     from structurepreservingiterativesolvers_amd.device import get_context
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
@@ -518,7 +525,11 @@ def test_fused_dual_spmv_bit_identical(spis):
         else:
             c = Case("lkdv_m50_cgmres_tol1e-19")
             A, b, cons = c.A, c.b, c.conlist()
-        for chain in (3, 2):
+        for chain, small in ((3, None), (3, "0"), (2, None)):  # (3, "0"): K2q at these small N
+            if small is None:
+                os.environ.pop("SPIS_K2W_SMALL_N", None)
+            else:
+                os.environ["SPIS_K2W_SMALL_N"] = small
             runs = []
             for fuse in (0, 1):
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
@@ -529,8 +540,19 @@ def test_fused_dual_spmv_bit_identical(spis):
                     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, 1), "spis_set_option")
                     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 3), "spis_set_option")
                 runs.append((x, np.asarray(d["res"]), np.concatenate(d["x"].y), d["x"].basis(25), np.asarray(d["x"])))
+            if chain == 3 and small is None:
+                # the default at these N is the one-reduce MGS (K2w), whose L-mode update pass forms
+                # x_j as four wave sums (K2w's GEMV order) while the unfused schedule runs K4's
+                # basis-order GEMV: the basis is bitwise equal, the iterates agree to roundoff
+                (xa, ra, ya, Qa, _), (xb, rb, yb, Qb, _) = runs
+                assert np.array_equal(Qa, Qb), case
+                assert np.linalg.norm(xa - xb) <= 1e-12 * np.linalg.norm(xa), case
+                np.testing.assert_allclose(ra, rb, rtol=1e-9, atol=1e-13 * ra[0])
+                np.testing.assert_allclose(ya, yb, rtol=1e-9, atol=1e-13 * np.abs(ya).max())
+                continue
             for a, bb in zip(runs[0], runs[1]):
-                assert np.array_equal(a, bb), (case, chain)
+                assert np.array_equal(a, bb), (case, chain, small)
+        os.environ.pop("SPIS_K2W_SMALL_N", None)
         outs.append(case)
     assert outs == ["swe", "lkdv"]
 
@@ -1274,7 +1296,7 @@ def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
 
 
 @pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_044_481, 1_048_575, 2_000_001, 3_500_000, 5_000_001, 7_500_001, 10_000_001])
-def test_mgs_chain_matches_per_step_launches(spis, n):
+def test_mgs_chain_matches_per_step_launches(spis, n, monkeypatch):
     """K2p / K2b / K2q (SPIS_OPT_MGS_CHAIN): the persistent MGS chains against one launch per MGS step,
     on sizes that select each register tiling (K2p: PER = 2, 4, 8 double2 per thread; K2b, the
     dedicated-gatherer mode beyond 2^20: PER = 8, 16, 24, 32, 40), the largest N K2p takes (odd: a
@@ -1286,6 +1308,7 @@ def test_mgs_chain_matches_per_step_launches(spis, n):
     from structurepreservingiterativesolvers_amd.device import get_context
 
     ctx = get_context()
+    monkeypatch.setenv("SPIS_K2W_SMALL_N", "0")  # mode 3 is K2q at every n here
     rng = np.random.default_rng(n)
     A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
                    0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
@@ -1349,3 +1372,36 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
     assert ra[-1] < 1e-3 * ra[0]
     for xb, rb, Qb in runs[1:]:
         assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
+
+
+@pytest.mark.parametrize("n", [65_536, 100_002, 196_608, 1001])
+def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
+    """K2s (small N, one GPU: K2w's dots, coefficients, update with the fused GEMV, norm and
+    normalise in one launch over register-resident basis slices) against K2w's launches
+    (SPIS_K2W_ONEPASS = 0): the same grouping of every partial for n a multiple of 256, and at
+    65,536 bitwise equal; at 196,608 one step's ||w'|| (H[10, 9]) comes out one ulp apart (cause
+    not found), otherwise the last chunk is grouped differently: roundoff.  GMRES in L mode, so the fused GEMV
+    and the residual hand-off ride in the launch (the golden suite covers the constrained
+    solves); repeated solves reuse the tag slots."""
+    from structurepreservingiterativesolvers_amd import solvers
+
+    rng = np.random.default_rng(n)
+    A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
+                   0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
+    b = rng.standard_normal(n)
+    k = 12
+    runs = []
+    for onepass in (0, 1, 1):
+        monkeypatch.setenv("SPIS_K2W_ONEPASS", str(onepass))
+        x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
+        runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
+    xa, ra, Qa = runs[0]
+    assert ra[-1] < 1e-3 * ra[0]
+    assert all(np.array_equal(p, q) for p, q in zip(runs[1], runs[2]))  # run to run
+    xb, rb, Qb = runs[1]
+    if n == 65_536:
+        assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
+    else:
+        assert np.linalg.norm(xa - xb) <= 1e-12 * np.linalg.norm(xa)
+        np.testing.assert_allclose(rb, ra, rtol=1e-9, atol=1e-14 * ra[0])
+        np.testing.assert_allclose(Qb, Qa, rtol=0, atol=1e-11)

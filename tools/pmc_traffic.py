@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
 BENCH_SPMV = 22  # spis_spmv_bench launches per (kind, cold): 2 untimed + 20 (bench.py)
-MGS_KERNELS = ("mgs_chain_lag_kernel", "mgs_chain_big_kernel", "mgs_chain_kernel", "icwy_dot_kernel",
+MGS_KERNELS = ("mgs_chain_lag_kernel", "mgs_chain_big_kernel", "mgs_chain_kernel", "icwy_dot_kernel", "icwy_onepass_kernel",
                "cgs_finalize_kernel", "cgs_update_kernel", "normalize_kernel", "mgs_step_kernel")
 
 
@@ -72,7 +72,7 @@ def reduce(cfg, fetch_csv, write_csv, out):
     mgs = [d for d in byte if d <= end_solver and any(m in names[d] for m in MGS_KERNELS)]
     # one Arnoldi step's MGS = its chain launch, or (K2w) its dot / coefficient / update / normalise
     # launches: the count of steps is the count of chain launches or of icwy_dot launches
-    steps = sum(1 for d in mgs if "mgs_chain" in names[d] or "icwy_dot" in names[d])
+    steps = sum(1 for d in mgs if "mgs_chain" in names[d] or "icwy_dot" in names[d] or "icwy_onepass" in names[d])
     # the normalise of r0 (one per solve, after the r0 SpMV, epilogue kEpiR0 = 3) is not MGS
     solves = sum(1 for d in byte if d <= end_solver and ("spmv_pipe_kernel<2048, 3" in names[d]
                                                          or "spmv_rowblock_kernel<3>" in names[d]))

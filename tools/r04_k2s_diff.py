@@ -1,0 +1,44 @@
+"""GPU: where K2s (one-pass) and K2w (two launches) first differ bitwise, per n."""
+import os
+import sys
+
+import numpy as np
+import scipy.sparse as sps
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from structurepreservingiterativesolvers_amd import solvers  # noqa: E402
+
+for n in (196_608,):
+    rng = np.random.default_rng(n)
+    A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
+                   0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
+    b = rng.standard_normal(n)
+    k = 12
+    out = []
+    for onepass in ("0", "1"):
+        os.environ["SPIS_K2W_ONEPASS"] = onepass
+        x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
+        out.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k), [np.asarray(v) for v in d["x"].y],
+                    np.asarray(d["x"].hessenberg(k))))
+    (xa, ra, Qa, ya, Ha), (xb, rb, Qb, yb, Hb) = out
+    print("H[10,9]", Ha[10, 9].hex(), Hb[10, 9].hex(), "H[9,8]", Ha[9, 8].hex(), Hb[9, 8].hex(),
+          "col9 eq", np.array_equal(Ha[:, 9], Hb[:, 9]))
+    print("H[:11,9] row eq", [bool(Ha[i, 9] == Hb[i, 9]) for i in range(11)])
+    r = Qb[10] / Qa[10]
+    rr = r[np.isfinite(r) & (np.abs(Qa[10]) > 1e-300)]
+    print("q10 ratio-1 min/max (ulps)", (rr.min() - 1) / 2.2e-16, (rr.max() - 1) / 2.2e-16)
+    print("q10 ratio quantiles", np.quantile(r[np.isfinite(r)], [0, 0.01, 0.5, 0.99, 1]))
+    print("first/last chunk eq", np.array_equal(Qa[10][:256], Qb[10][:256]), np.array_equal(Qa[10][-256:], Qb[10][-256:]))
+    eqc = [bool(np.array_equal(Qa[10][c * 256:(c + 1) * 256], Qb[10][c * 256:(c + 1) * 256])) for c in range(n // 256)]
+    print("chunks equal:", sum(eqc), "of", len(eqc), "first equal chunk ids", [i for i, e in enumerate(eqc) if e][:10])
+    hd = np.argwhere(Ha != Hb)
+    print("H diffs (row, col)", hd[:6].tolist(), [(Ha[i, j], Hb[i, j]) for i, j in hd[:3]])
+    for i in range(k):
+        if not np.array_equal(Qa[i], Qb[i]):
+            dq = np.abs(Qa[i] - Qb[i])
+            print("q", i, "ndiff", int((dq > 0).sum()), "max", dq.max(), "ratio", np.median(Qb[i][dq > 0] / Qa[i][dq > 0]))
+            break
+    qd = [int(np.argmax(Qa[i] != Qb[i])) if not np.array_equal(Qa[i], Qb[i]) else -1 for i in range(k)]
+    yd = [i for i in range(min(len(ya), len(yb))) if not np.array_equal(ya[i], yb[i])]
+    print(n, "x eq", np.array_equal(xa, xb), "res eq", np.array_equal(ra, rb), "first q diff idx per vec", qd,
+          "y diff steps", yd[:5], "xdiff rows", np.nonzero(xa != xb)[0][:8], flush=True)
