@@ -88,12 +88,15 @@ def _problem(name):
     return dic["A"], [n // 3] * 3, rng.normal(size=n)
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("problem", ["swe", "lkdv", "lkdvrk", "lkdvrk_lifted"])
-def test_two_rank_spmv_and_dot(problem):
+def test_two_rank_spmv_and_dot(problem, world):
+    """The row partition, halo plan and fixed-order dot at 2 and 4 ranks (gloo): the 4-rank case
+    rehearses the several-neighbour halo that the 4- and 8-GPU bench lines take."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, problem, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, problem, q)) for r in range(world)]
     for p in procs:
         p.start()
     y, dots, n_ghost, nbrs = q.get(timeout=240)
@@ -102,12 +105,13 @@ def test_two_rank_spmv_and_dot(problem):
         assert p.exitcode == 0
     A, fields, x = _problem(problem)
     assert np.array_equal(y, A @ x)  # bit-exact: each local row keeps its entry order
-    assert dots[0] == dots[1]
+    assert all(d == dots[0] for d in dots)
     np.testing.assert_allclose(dots[0], x @ (A @ x), rtol=1e-12)
     if problem == "lkdvrk_lifted":  # kron(P'P, L - M): DG mass blocks couple no cells, so no halo
         assert n_ghost == 0 and nbrs == []
     else:
-        assert n_ghost > 0 and nbrs == [1]
+        assert n_ghost > 0 and 1 in nbrs and 0 not in nbrs
+        assert nbrs == sorted(nbrs) and all(0 < q < world for q in nbrs)
 
 
 def test_partition_roundtrip_and_locality():
@@ -407,11 +411,12 @@ def _solve_worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def test_two_rank_constrained_solve_matches_serial_oracle():
-    """The several-GPU design end to end on CPU (2 gloo ranks): both ranks take the same branches
-    as each other and as the serial oracle (20 steps, the final one constrained), hold bitwise
-    identical H, residual histories and LS solutions, and the assembled iterate agrees with the
-    oracle's to roundoff and preserves mass and energy."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_constrained_solve_matches_serial_oracle(world):
+    """The several-GPU design end to end on CPU (2 and 4 gloo ranks): all ranks take the same
+    branches as each other and as the serial oracle (20 steps, the final one constrained), hold
+    bitwise identical H, residual histories and LS solutions, and the assembled iterate agrees
+    with the oracle's to roundoff and preserves mass and energy."""
     from oracle import cgmres_port as port
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly
@@ -419,15 +424,15 @@ def test_two_rank_constrained_solve_matches_serial_oracle():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port_ = _free_port()
-    procs = [ctx.Process(target=_solve_worker, args=(r, 2, port_, q)) for r in range(2)]
+    procs = [ctx.Process(target=_solve_worker, args=(r, world, port_, q)) for r in range(world)]
     for p in procs:
         p.start()
     x, traces, steps, res, Hs = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert traces[0] == traces[1] and steps[0] == steps[1]
-    assert np.array_equal(Hs[0], Hs[1]) and res[0] == res[1]
+    assert all(t == traces[0] for t in traces) and all(st == steps[0] for st in steps)
+    assert all(np.array_equal(h, Hs[0]) for h in Hs) and all(r == res[0] for r in res)
     dic, _ = assembly.linforms(M=12)
     x0 = np.zeros_like(dic["b"])
     trace = []

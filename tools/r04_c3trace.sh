@@ -1,0 +1,8 @@
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=${1:-gpurun_out/r04c3t}
+mkdir -p $O
+timeout -k 10 240 python -u bench.py > $O/c3.json 2> $O/c3.err
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/c3t.json 2> $O/c3t.err
+f=$(find $O/prof -name '*kernel_trace.csv' | head -n 1); cp "$f" $O/trace.csv
+python tools/trace_gaps.py $O/trace.csv > $O/gaps.txt
