@@ -205,6 +205,19 @@ int spis_comm_init(spis_context* ctx, int32_t nranks, int32_t rank, const uint8_
 int spis_comm_allreduce_sum(spis_context* ctx, double* buf_dev, int64_t count);
 int spis_comm_barrier(spis_context* ctx);
 
+/* The same several-rank code path with the collectives done by a host callback instead of RCCL
+ * (operands staged through host memory, the stream drained first).  For rehearsing several ranks
+ * on one GPU, which RCCL refuses; not a production transport.  The callback returns 0 on success.
+ *   SPIS_COLL_ALLREDUCE: buf[0 .. count) summed element-wise over the ranks, in place;
+ *   SPIS_COLL_EXCHANGE:  buf[0 .. count) holds send_counts[i] doubles for neighbors[i] (i in
+ *                        order, concatenated); recv receives recv_counts[i] doubles from each, in
+ *                        the same order. */
+enum { SPIS_COLL_ALLREDUCE = 0, SPIS_COLL_EXCHANGE = 1 };
+typedef int (*spis_host_coll_fn)(void* user, int32_t op, double* buf, int64_t count, int32_t n_neighbors,
+                                 const int32_t* neighbors, const int64_t* send_counts, const int64_t* recv_counts,
+                                 double* recv);
+int spis_comm_init_host(spis_context* ctx, int32_t nranks, int32_t rank, spis_host_coll_fn fn, void* user);
+
 /* ---- matrices ----------------------------------------------------------------
  * Local CSR rows (n_rows x (n_rows + n_ghost)), host arrays, copied to HBM.
  * The matrix is partitioned into row blocks of <= 2048 merge items (rows +

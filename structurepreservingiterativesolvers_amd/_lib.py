@@ -68,6 +68,11 @@ class ConstraintDesc(C.Structure):
 
 
 PRECOND_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64)
+# spis_host_coll_fn (spis_comm_init_host): (user, op, buf, count, n_neighbors, neighbors,
+# send_counts, recv_counts, recv)
+HOST_COLL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.c_int64, C.c_int32,
+                           C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double))
+COLL_ALLREDUCE, COLL_EXCHANGE = 0, 1
 CONLS_FN = C.CFUNCTYPE(
     C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.c_double,
     C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
@@ -127,6 +132,7 @@ SIGNATURES = [
     ("spis_comm_init", C.c_int, [_VP, _I32, _I32, C.POINTER(C.c_uint8)]),
     ("spis_comm_allreduce_sum", C.c_int, [_VP, _VP, _I64]),
     ("spis_comm_barrier", C.c_int, [_VP]),
+    ("spis_comm_init_host", C.c_int, [_VP, _I32, _I32, HOST_COLL_FN, _VP]),
     ("spis_csr_upload", C.c_int, [_VP, _I64, _I64, _I64, _PI32, _PI32, _PD, C.POINTER(HaloDesc), C.POINTER(_VP)]),
     ("spis_matrix_destroy", C.c_int, [_VP]),
     ("spis_matrix_info", C.c_int, [_VP, _PI64]),

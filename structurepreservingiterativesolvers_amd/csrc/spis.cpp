@@ -118,7 +118,14 @@ struct spis_context {
   double* cg_G = nullptr;              // its reduced output (64*64 + 4*64)
   double* cg_vpart = nullptr;          // K7t: the transpose's linear-term partials
   ncclComm_t comm = nullptr;
+  // several ranks through a host callback instead of RCCL (spis_comm_init_host): the same
+  // distributed code path with the collectives staged through host memory, so that several
+  // ranks can share one GPU (RCCL refuses that) when the path is rehearsed on a one-GPU box
+  spis_host_coll_fn host_coll = nullptr;
+  void* host_user = nullptr;
+  std::vector<double> host_stage;  // send | recv staging of a host collective
   int nranks = 1, rank = 0;
+  bool dist_on() const { return comm != nullptr || host_coll != nullptr; }
   std::vector<spis_workspace*> pool;
   // live kernel timing (spis_profile_*): HIP events on this stream around each timed launch
   bool prof = false;
@@ -250,7 +257,7 @@ struct spis_workspace {
 // ------------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------------
-static bool fixed_grid(const spis_context* c) { return c->comm != nullptr; }
+static bool fixed_grid(const spis_context* c) { return c->dist_on(); }
 
 // C16 (SPIS_OPT_COL16): 1 = when val/col exceed the 256 MB Infinity Cache (C5 dual 470 vs
 // 494 us: HBM-bound, 2 B less per nonzero pays; C3, cache-resident: 39.5 vs 37.6 us, the
@@ -344,17 +351,56 @@ static void prof_drain(spis_context* c) {
   c->ev_pending.resize(keep);
 }
 
-// a one-rank communicator's sum is the identity: no collective launch (halo exchanges still run:
-// a one-rank operator may declare ghosts it receives from itself)
-static int allreduce(spis_context* c, double* buf, int64_t count) {
-  if (!c->comm || count <= 0 || c->nranks == 1) return SPIS_OK;
-  NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
+// several ranks through the host callback (spis_comm_init_host): the stream drained, the
+// operands staged through host memory, the callback does the collective (tests: torch.distributed
+// over gloo); ordering across ranks is the callers', exactly as for RCCL
+static int host_allreduce(spis_context* c, double* buf, int64_t count, hipStream_t st) {
+  HIP_TRY(hipStreamSynchronize(st));
+  c->host_stage.resize(static_cast<size_t>(count));
+  HIP_TRY(hipMemcpy(c->host_stage.data(), buf, sizeof(double) * count, hipMemcpyDeviceToHost));
+  if (c->host_coll(c->host_user, SPIS_COLL_ALLREDUCE, c->host_stage.data(), count, 0, nullptr, nullptr, nullptr,
+                   nullptr) != 0)
+    return fail(SPIS_ERR_CALLBACK, "host all-reduce failed");
+  HIP_TRY(hipMemcpy(buf, c->host_stage.data(), sizeof(double) * count, hipMemcpyHostToDevice));
   return SPIS_OK;
 }
 
+// send[soff[i] * w ...] to nbr[i] and recv[roff[i] * w ...] from it, w doubles per halo entry;
+// the receive side is contiguous (ghost rows in neighbour order)
+static int host_exchange(spis_context* c, const spis_matrix* M, const double* send_dev, double* recv_dev, int w,
+                         hipStream_t st) {
+  HIP_TRY(hipStreamSynchronize(st));
+  const int nn = static_cast<int>(M->nbr.size());
+  const int64_t ns = static_cast<int64_t>(M->n_send) * w, nr = static_cast<int64_t>(M->n_ghost) * w;
+  c->host_stage.resize(static_cast<size_t>(ns + nr));
+  std::vector<int64_t> sc(nn), rc(nn);
+  for (int i = 0; i < nn; ++i) {
+    sc[i] = static_cast<int64_t>(M->scnt[i]) * w;
+    rc[i] = static_cast<int64_t>(M->rcnt[i]) * w;
+  }
+  if (ns > 0) HIP_TRY(hipMemcpy(c->host_stage.data(), send_dev, sizeof(double) * ns, hipMemcpyDeviceToHost));
+  if (c->host_coll(c->host_user, SPIS_COLL_EXCHANGE, c->host_stage.data(), ns, nn, M->nbr.data(), sc.data(),
+                   rc.data(), c->host_stage.data() + ns) != 0)
+    return fail(SPIS_ERR_CALLBACK, "host halo exchange failed");
+  if (nr > 0) HIP_TRY(hipMemcpy(recv_dev, c->host_stage.data() + ns, sizeof(double) * nr, hipMemcpyHostToDevice));
+  return SPIS_OK;
+}
+
+// a one-rank communicator's sum is the identity: no collective launch (halo exchanges still run:
+// a one-rank operator may declare ghosts it receives from itself)
+static int allreduce_on(spis_context* c, double* buf, int64_t count, hipStream_t st) {
+  if (!c->dist_on() || count <= 0 || c->nranks == 1) return SPIS_OK;
+  if (c->host_coll) return host_allreduce(c, buf, count, st);
+  NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, st));
+  return SPIS_OK;
+}
+
+static int allreduce(spis_context* c, double* buf, int64_t count) { return allreduce_on(c, buf, count, c->stream); }
+
 static int exchange(spis_context* c, const spis_matrix* M, double* x) {
-  if (!c->comm || M->nbr.empty()) return SPIS_OK;
+  if (!c->dist_on() || M->nbr.empty()) return SPIS_OK;
   HIP_TRY(launch_gather(M->n_send, M->send_idx, x, M->send_buf, c->stream));
+  if (c->host_coll) return host_exchange(c, M, M->send_buf, x + M->n_rows, 1, c->stream);
   NCCL_TRY(ncclGroupStart());
   for (size_t i = 0; i < M->nbr.size(); ++i) {
     if (M->scnt[i] > 0)
@@ -366,16 +412,10 @@ static int exchange(spis_context* c, const spis_matrix* M, double* x) {
   return SPIS_OK;
 }
 
-static int allreduce_on(spis_context* c, double* buf, int64_t count, hipStream_t st) {
-  if (!c->comm || count <= 0 || c->nranks == 1) return SPIS_OK;
-  NCCL_TRY(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, st));
-  return SPIS_OK;
-}
-
 // several GPUs: the ghost rows of a row-major (n_rows + n_ghost, cols) array (Ut of a constraint
 // reduction) from their owners, through M's halo plan (one grouped send/recv of whole rows)
 static int exchange_rows(spis_context* c, const spis_matrix* M, double* U, int cols, hipStream_t st) {
-  if (!c->comm || M->nbr.empty()) return SPIS_OK;
+  if (!c->dist_on() || M->nbr.empty()) return SPIS_OK;
   const size_t need = static_cast<size_t>(std::max<int64_t>(M->n_send, 1)) * cols;
   if (c->ut_send_len < need) {
     if (c->ut_send) HIP_TRY(hipFree(c->ut_send));
@@ -385,6 +425,7 @@ static int exchange_rows(spis_context* c, const spis_matrix* M, double* U, int c
     c->ut_send_len = need;
   }
   HIP_TRY(launch_gather_rows(M->n_send, cols, M->send_idx, U, c->ut_send, st));
+  if (c->host_coll) return host_exchange(c, M, c->ut_send, U + static_cast<size_t>(M->n_rows) * cols, cols, st);
   NCCL_TRY(ncclGroupStart());
   for (size_t i = 0; i < M->nbr.size(); ++i) {
     if (M->scnt[i] > 0)
@@ -432,7 +473,7 @@ static int wait_event(hipEvent_t e) {
 static int spmv_local(spis_context* c, spis_workspace* ws, const spis_matrix* M, const double* x,
                       double* y) {
   const int g = spmv_grid(M->view(), fixed_grid(c));
-  if (c->comm && M->n_ghost > 0) {
+  if (c->dist_on() && M->n_ghost > 0) {
     if (!ws->ext || ws->ext_len < M->n_rows + M->n_ghost) {
       if (ws->ext) HIP_TRY(hipFree(ws->ext));
       ws->ext_len = static_cast<int32_t>(M->n_rows + M->n_ghost);
@@ -727,7 +768,7 @@ extern "C" int spis_spmv_bench(spis_context* c, spis_matrix* A, int32_t kind, in
                                double* us_out) {
   ABI_GUARD({
     if (!c || !A || !us_out || reps < 1 || kind < 0 || kind > 1) return fail(SPIS_ERR_ARG, "bad argument");
-    if (A->ctx != c || A->n_rows != A->n_cols || c->comm) return fail(SPIS_ERR_ARG, "single-GPU square matrix only");
+    if (A->ctx != c || A->n_rows != A->n_cols || c->dist_on()) return fail(SPIS_ERR_ARG, "single-GPU square matrix only");
     HIP_TRY(hipSetDevice(c->device));
     const int64_t n = A->n_rows;
     const int64_t pn = (n + 63) / 64 * 64;
@@ -789,13 +830,25 @@ extern "C" int spis_comm_unique_id(uint8_t id_out[128]) {
 extern "C" int spis_comm_init(spis_context* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
   ABI_GUARD({
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPIS_ERR_ARG, "bad comm args");
-    if (c->comm) return fail(SPIS_ERR_STATE, "context already has a communicator");
+    if (c->dist_on()) return fail(SPIS_ERR_STATE, "context already has a communicator");
     // a 1-rank communicator is created too: it switches the context to the distributed code
     // path (fixed grids, all-reduces, halo exchanges — e.g. to itself), which tests use
     HIP_TRY(hipSetDevice(c->device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, 128);
     NCCL_TRY(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_comm_init_host(spis_context* c, int32_t nranks, int32_t rank, spis_host_coll_fn fn, void* user) {
+  ABI_GUARD({
+    if (!c || !fn || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPIS_ERR_ARG, "bad comm args");
+    if (c->dist_on()) return fail(SPIS_ERR_STATE, "context already has a communicator");
+    c->host_coll = fn;
+    c->host_user = user;
     c->nranks = nranks;
     c->rank = rank;
     return SPIS_OK;
@@ -1496,7 +1549,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   // after the local rows (exchange_rows, per matrix: each has its own halo plan)
   int64_t ut_rows = std::max<int64_t>(n, 1);
   for (int ci = 0; ci < m; ++ci)
-    if (c->comm && cons[ci].M != nullptr) ut_rows = std::max<int64_t>(ut_rows, n + cons[ci].M->n_ghost);
+    if (c->dist_on() && cons[ci].M != nullptr) ut_rows = std::max<int64_t>(ut_rows, n + cons[ci].M->n_ghost);
   if (ws->Ut && (ws->Ut_cols < ut_cols || ws->Ut_rows < ut_rows)) {
     HIP_TRY(hipFree(ws->Ut));
     ws->Ut = nullptr;
@@ -1553,7 +1606,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     const CsrView mv = cons[L.ci].M->view();
     const int nvv = v_done ? 0 : nv;
     spis_matrix* Mc = cons[L.ci].M;
-    if (c->comm) ST_TRY(exchange_rows(c, Mc, ws->Ut, ut_cols, st));
+    if (c->dist_on()) ST_TRY(exchange_rows(c, Mc, ws->Ut, ut_cols, st));
     if (L.sym) {
       HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, c->cg_G, st));
     } else if (mfma) {
@@ -1621,7 +1674,7 @@ static bool fused_con_ok(const spis_context* c, int p, int m, const spis_constra
   int nlin = 0;
   for (int ci = 0; ci < m; ++ci) nlin += cons[ci].v_dev ? 1 : 0;
   // several GPUs: K7m on the local rows, the ghost Ut rows exchanged per matrix, G all-reduced
-  if (c->comm && !(p + 1 <= 32 && c->con_gram >= 2)) return false;
+  if (c->dist_on() && !(p + 1 <= 32 && c->con_gram >= 2)) return false;
   return p + 1 <= 64 && nlin <= 4 && c->con_gram != 0;
 }
 
@@ -1643,7 +1696,7 @@ static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, cons
     if (!mzero) {
       if (con.M->n_rows != n) return fail(SPIS_ERR_ARG, "constraint matrix rows != n");
       if (cc.cols < p) {
-        if (!c->comm || con.M->n_ghost == 0) {
+        if (!c->dist_on() || con.M->n_ghost == 0) {
           HIP_TRY(launch_spmm(con.M->view(), Z + static_cast<int64_t>(cc.cols) * pitch, pitch, p - cc.cols,
                               cc.MZ + static_cast<int64_t>(cc.cols) * ws->pitch_n, ws->pitch_n, c->stream));
         } else {
@@ -1911,7 +1964,7 @@ struct Solver {
   // rows hold its owners' values (exchanged before A_l's SpMV) and x0's were exchanged at the
   // start, so x_j's ghost rows come out bitwise equal to the owners' x_j (same y, same order):
   // no per-iteration halo exchange of x_j before its residual SpMV
-  int64_t n_gx() const { return (c->comm && !A->nbr.empty()) ? n + A->n_ghost : n; }
+  int64_t n_gx() const { return (c->dist_on() && !A->nbr.empty()) ? n + A->n_ghost : n; }
 
   // Speculative update (single GPU, K2q chains): K2q's gatherer writes H[:, j] with H[j+1, j]
   // last, behind a system-scope release, so the host can read the column as soon as A_j's chain
@@ -1939,7 +1992,7 @@ struct Solver {
   // K2q's capacity: two passes over the basis per step, the second carrying the update GEMV, in
   // place of K2b + a separate GEMV pass (C5: 826 -> 902 it/s; FX does not fit K2b's registers)
   bool icwy_on() const {
-    return c->comm ? c->dist_mgs == 1
+    return c->dist_on() ? c->dist_mgs == 1
                    : (c->mgs_chain == 4 || (c->mgs_chain == 3 && !c->cgs2 && !k2q_fits()) || k2w_small());
   }
   // small N: K2q's per-MGS-step exchanges are latency, not bandwidth; K2s (K2w in one launch over
@@ -2084,7 +2137,7 @@ struct Solver {
     // update kernel's workgroup 0, after the dot pass (no finalize launch: the host's next need is
     // H[:, j], published at the end of this step; one rank takes the merged order, the all-reduce
     // being the identity: the self-halo test covers it)
-    const bool merged = xpart != nullptr && xpart == c->partR && c->comm != nullptr;
+    const bool merged = xpart != nullptr && xpart == c->partR && c->dist_on();
     if (xpart && !merged) ST_TRY(allreduce(c, const_cast<double*>(xpart), gs));
     const int nv = j + 1;
     double* hcol = c->pinned_dev + hoff(j);
@@ -2096,7 +2149,7 @@ struct Solver {
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
     if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
     // K2s: one GPU, small N: the whole step in one launch, the basis slices held in registers
-    if (!c->comm && k2w_onepass && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
+    if (!c->dist_on() && k2w_onepass && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
       if (++c->icwy_tag == 0) c->icwy_tag = 1;
       const LaunchEv both{e_first.start, e_last.stop};
       HIP_TRY(launch_icwy_onepass(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_G, hcol, c->icwy_slots, c->icwy_tag,
@@ -2218,7 +2271,7 @@ struct Solver {
 
   // U_j1's and U_j2's true-residual SpMVs in one launch (the matrix read once; the last two
   // iterates of a solve, which have no Arnoldi SpMV to pair with), both published
-  bool res2_ok() const { return !c->comm && A->dual_view().blk_meta != nullptr; }
+  bool res2_ok() const { return !c->dist_on() && A->dual_view().blk_meta != nullptr; }
   int enqueue_residual2(int j1, int j2) {
     {
       ProfEv ps(c, SPIS_PROF_SPMV_RES);
@@ -2244,7 +2297,7 @@ struct Solver {
       if (p <= kYArg) {
         // several GPUs: the GEMV runs every iteration beside the distributed MGS; nontemporal basis
         // loads keep the matrix resident there (single GPU: the GEMV rides in K2q, FX)
-        HIP_TRY(launch_gemv(n_gx(), p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le, c->comm && nt_basis_on()));
+        HIP_TRY(launch_gemv(n_gx(), p, ws->Zb, ws->pitch, y, true, ws->x0, xbuf(j), s, &le, c->dist_on() && nt_basis_on()));
       } else {
         double* yh = c->pinned + yoff();
         for (int a = 0; a < p; ++a) yh[a] = y[a];
@@ -2275,7 +2328,7 @@ struct Solver {
       const LaunchEv le = ps.both();
       HIP_TRY(launch_spmv(A->dual_view(), kEpiResNorm, xbuf(j), nullptr, b, c->partR, gs, c->stream, &le));
     }
-    if (c->comm) return update_comm_finish(j);
+    if (c->dist_on()) return update_comm_finish(j);
     next_seq(j);
     HIP_TRY(launch_finalize(c->partR, gs, c->pinned_dev + roff(j), 0, c->stream, nullptr, flag_dev(), seq_dev(j)));
     return SPIS_OK;
@@ -2290,14 +2343,14 @@ struct Solver {
   int enqueue_update_arnoldi(int j, int p, const double* y, int ja) {
     ST_TRY(enqueue_gemv(j, p, y, true));
     ST_TRY(arnoldi_pre(ja));
-    if (!c->comm) next_seq(j);
+    if (!c->dist_on()) next_seq(j);
     c->prof_iter = j;
     {
       ProfEv pd(c, SPIS_PROF_SPMV_DUAL);
       const LaunchEv le = pd.both();
       ST_TRY(launch_dual(j, ja, b, &le));
     }
-    if (c->comm) {
+    if (c->dist_on()) {
       ST_TRY(update_comm_finish(j));
       return arnoldi_post(ja);
     }
@@ -2336,7 +2389,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     if (c->prof) ++c->prof_phase;
     if (o->pre_matrix && o->pre_matrix->n_rows != n) return fail(SPIS_ERR_ARG, "preconditioner size mismatch");
     if (o->pre_ilu && o->pre_ilu->n != n) return fail(SPIS_ERR_ARG, "ILU preconditioner size mismatch");
-    if (o->pre_ilu && c->comm) return fail(SPIS_ERR_ARG, "the device ILU preconditioner is single-GPU");
+    if (o->pre_ilu && c->dist_on()) return fail(SPIS_ERR_ARG, "the device ILU preconditioner is single-GPU");
     if (o->pre_ilu && o->pre_ilu->ctx != c) return fail(SPIS_ERR_ARG, "ILU preconditioner of another context");
     if (!!o->pre_matrix + !!o->pre_ilu + !!o->pre_fn > 1) return fail(SPIS_ERR_ARG, "more than one preconditioner");
     for (int i = 0; i < (o->conls_fn ? 0 : o->n_constraints); ++i)
@@ -2375,7 +2428,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // x0 into a halo'd buffer only when the SpMV reads ghost entries
     HIP_TRY(launch_copy(n, x0, ws->x0, s));
     const double* xr0 = ws->x0;
-    if (A->n_ghost > 0 || c->comm) {
+    if (A->n_ghost > 0 || c->dist_on()) {
       HIP_TRY(launch_copy(n, x0, ws->xj, s));
       ST_TRY(exchange(c, A, ws->xj));
       xr0 = ws->xj;
@@ -2388,7 +2441,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // beta: the normalize kernel's one system-scope store into pinned memory; the host spins
     // until the slot leaves its sentinel (an event marker here cost ~6 us of GPU idle per solve);
     // several GPUs keep the event (the slot is written after an all-reduce)
-    const bool beta_spin = !c->comm;
+    const bool beta_spin = !c->dist_on();
     if (beta_spin) *reinterpret_cast<volatile uint64_t*>(beta_slot) = Solver::kHSentinel;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
     if (!beta_spin) HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)

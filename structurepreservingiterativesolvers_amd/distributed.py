@@ -195,10 +195,50 @@ def emulate_spmv(op: LocalOperator, plan: HaloPlan, x_local, exchange):
 # ------------------------------------------------------------------------------------------------
 # runtime: RCCL bootstrap + distributed handles
 # ------------------------------------------------------------------------------------------------
-class Comm:
-    """torch.distributed (gloo side channel) + the libspis RCCL communicator."""
+def _host_collective(dist):
+    """spis_host_coll_fn over torch.distributed (gloo): the in-place sum of an all-reduce, and a
+    halo exchange's sends / receives to and from each neighbour (non-blocking, then all waited)."""
+    import torch
 
-    def __init__(self, ctx=None):
+    def coll(_user, op, buf, count, n_nbr, nbr, scnt, rcnt, recv):
+        try:
+            if op == _lib.COLL_ALLREDUCE:
+                if count > 0:
+                    dist.all_reduce(torch.from_numpy(np.ctypeslib.as_array(buf, shape=(count,))))
+                return 0
+            sc = [int(scnt[i]) for i in range(n_nbr)]
+            rc = [int(rcnt[i]) for i in range(n_nbr)]
+            send = np.ctypeslib.as_array(buf, shape=(count,)) if count > 0 else np.zeros(0)
+            rv = np.ctypeslib.as_array(recv, shape=(sum(rc),)) if sum(rc) > 0 else np.zeros(0)
+            reqs, so, ro = [], 0, 0
+            for i in range(n_nbr):
+                peer = int(nbr[i])
+                if sc[i] > 0:
+                    reqs.append(dist.isend(torch.from_numpy(send[so:so + sc[i]]), peer))
+                if rc[i] > 0:
+                    reqs.append(dist.irecv(torch.from_numpy(rv[ro:ro + rc[i]]), peer))
+                so, ro = so + sc[i], ro + rc[i]
+            for r in reqs:
+                r.wait()
+            return 0
+        except Exception:  # noqa: BLE001 — reported to the library as a failed collective
+            import traceback
+
+            traceback.print_exc()
+            return 1
+
+    return _lib.HOST_COLL_FN(coll)
+
+
+class Comm:
+    """torch.distributed (gloo side channel) + the libspis RCCL communicator.
+
+    ``transport="host"`` (or ``SPIS_TRANSPORT=host``) runs the same several-rank code path with the
+    collectives staged through host memory and done over gloo (spis_comm_init_host): several
+    ranks can then share one GPU (``SPIS_DEVICE``), which RCCL refuses.  For rehearsal and tests,
+    not for measurement."""
+
+    def __init__(self, ctx=None, transport=None):
         import torch.distributed as dist
 
         if not dist.is_initialized():
@@ -222,13 +262,21 @@ class Comm:
         dev = int(os.environ["SPIS_DEVICE"]) if "SPIS_DEVICE" in os.environ else local_rank
         self.ctx = ctx or get_context(dev)
         L = self.ctx.L
-        uid = (C.c_uint8 * 128)()
-        if self.rank == 0:
-            _lib.check(L.spis_comm_unique_id(uid), "spis_comm_unique_id")
-        box = [bytes(uid)]
-        dist.broadcast_object_list(box, src=0)
-        uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
-        _lib.check(L.spis_comm_init(self.ctx.handle, self.world, self.rank, uid), "spis_comm_init")
+        self.transport = transport or os.environ.get("SPIS_TRANSPORT", "rccl")
+        if self.transport == "host":
+            self._coll = _host_collective(dist)  # kept alive: the library holds the pointer
+            _lib.check(L.spis_comm_init_host(self.ctx.handle, self.world, self.rank, self._coll, None),
+                       "spis_comm_init_host")
+        elif self.transport == "rccl":
+            uid = (C.c_uint8 * 128)()
+            if self.rank == 0:
+                _lib.check(L.spis_comm_unique_id(uid), "spis_comm_unique_id")
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0)
+            uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
+            _lib.check(L.spis_comm_init(self.ctx.handle, self.world, self.rank, uid), "spis_comm_init")
+        else:
+            raise ValueError(f"unknown transport {self.transport!r} (rccl or host)")
         self.ctx.nranks, self.ctx.rank = self.world, self.rank
 
     def allgather(self, obj):

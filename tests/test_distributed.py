@@ -443,3 +443,54 @@ def test_two_rank_constrained_solve_matches_serial_oracle(world):
     np.testing.assert_allclose(res[0][:-1], dr["res"][:-1], rtol=1e-6, atol=1e-10 * dr["res"][0])
     assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-12 * abs(dic["m0"])
     assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
+
+
+# ---- the host transport's collective callback (spis_comm_init_host) over gloo -----------------
+def _coll_worker(rank, world, port, out_q):
+    import ctypes as C
+
+    from structurepreservingiterativesolvers_amd import _lib
+    from structurepreservingiterativesolvers_amd.distributed import _host_collective
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn = _host_collective(dist)
+        PD = C.POINTER(C.c_double)
+        a = np.arange(5, dtype=np.float64) * (rank + 1)
+        assert fn(None, _lib.COLL_ALLREDUCE, a.ctypes.data_as(PD), 5, 0, None, None, None, None) == 0
+        # a ring exchange: rank r sends r+1 values (r, r, ..) to each other rank, receives q+1 from q
+        peers = [q for q in range(world) if q != rank]
+        send = np.concatenate([np.full(rank + 1, 100.0 * rank + q) for q in peers])
+        recv = np.zeros(sum(q + 1 for q in peers))
+        nbr = (C.c_int32 * len(peers))(*peers)
+        sc = (C.c_int64 * len(peers))(*[rank + 1] * len(peers))
+        rc = (C.c_int64 * len(peers))(*[q + 1 for q in peers])
+        assert fn(None, _lib.COLL_EXCHANGE, send.ctypes.data_as(PD), len(send), len(peers), nbr, sc, rc,
+                  recv.ctypes.data_as(PD)) == 0
+        out_q.put((rank, a, recv, peers))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_transport_collectives(world):
+    """The callback behind spis_comm_init_host (several ranks sharing one GPU in the GPU tests):
+    its all-reduce sums in place, and its exchange delivers each neighbour's block in neighbour
+    order with unequal counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_coll_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    tot = sum(r + 1 for r in range(world))
+    for rank, a, recv, peers in got:
+        assert np.array_equal(a, np.arange(5) * tot)
+        exp = np.concatenate([np.full(p + 1, 100.0 * p + rank) for p in peers])
+        assert np.array_equal(recv, exp)

@@ -1,0 +1,102 @@
+"""Several ranks through libspis's distributed code path on ONE GPU (pytest -m gpu).
+
+RCCL refuses two ranks on one device, so the ranks use the host transport
+(spis_comm_init_host, SPIS_TRANSPORT=host): every all-reduce and halo exchange of the solve is
+staged through host memory and done over gloo, while everything else is the several-GPU path of
+the product — the field-interleaved row partition and halo plans (distributed.py), fixed-size
+partial arrays, K2w's one-reduce MGS with its merged residual all-reduce, the constraint terms
+from local rows with the ghost Ut rows exchanged, K7t pairing the symmetric energy matrix by
+global index, and the replicated host least squares.  Each rank is its own process on GPU 0
+(tests/multirank_worker.py).  Checked against the single-GPU solve and the reference oracle:
+the same branch sequence and steps on every rank, bitwise-identical residual histories across
+ranks, iterates within roundoff of the single-GPU ones, and the invariants preserved
+(solvers.py:131-323)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(tmp_path, world, problem, M, k):
+    out = str(tmp_path / f"{problem}_{world}")
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), SPIS_DEVICE="0", SPIS_TRANSPORT="host", OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "multirank_worker.py"), out,
+                                       problem, str(M), str(k)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=150)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("problem", ["swe", "lkdv"])
+def test_several_ranks_on_one_gpu_match_single_gpu_and_oracle(tmp_path, problem, world):
+    from oracle import cgmres_port as port
+
+    k = 20
+    if problem == "swe":
+        from structurepreservingiterativesolvers_amd.swe import LinearSolver as ls
+        from structurepreservingiterativesolvers_amd.swe import assembly
+
+        M = 20
+    else:
+        from structurepreservingiterativesolvers_amd.lkdv import LinearSolver as ls
+        from structurepreservingiterativesolvers_amd.lkdv import assembly
+
+        M = 400
+    outs = _run_ranks(tmp_path, world, problem, M, k)
+
+    dic, _ = assembly.linforms(M=M)
+    n = dic["A"].shape[0]
+    x0 = np.zeros(n)
+    xs, ds = ls.cgmresWrapper(dic, x0=x0, k=k, tol=1e-19)  # the single-GPU path of libspis
+    trace1 = list(ds["x"].trace)
+    trace = []
+    xr, dr = port.cgmres(dic["A"], dic["b"], x0, k, tol=1e-19, conlist=ls.constraints(dic, x0), trace=trace)
+
+    ref = outs[0]
+    for o in outs:  # every rank: the same branches, steps and (bitwise) residual history
+        assert int(o["steps"]) == int(ref["steps"])
+        assert np.array_equal(o["trace_j"], ref["trace_j"]) and np.array_equal(o["trace_b"], ref["trace_b"])
+        assert np.array_equal(o["res"], ref["res"])
+        assert np.array_equal(o["x"], ref["x"])
+    assert all(int(o["n_ghost"]) > 0 for o in outs)  # the halo exchange is exercised on every rank
+    tr = [(int(j), str(b)) for j, b in zip(ref["trace_j"], ref["trace_b"])]
+    assert tr == trace1 == trace
+    assert int(ref["steps"]) == ds["steps"] == dr["steps"]
+    x = ref["x"]
+    # the reduction order differs from one GPU's (per-rank partials, then the sum over ranks):
+    # roundoff-level agreement, as the 2-rank gloo model (tests/test_distributed.py)
+    assert np.linalg.norm(x - xs) <= 1e-8 * np.linalg.norm(xs)
+    assert np.linalg.norm(x - xr) <= 1e-8 * np.linalg.norm(xr)
+    mid = int(ref["mid"])
+    xm1 = np.asarray(ds["x"][mid])
+    assert np.linalg.norm(ref["x_mid"] - xm1) <= 1e-8 * np.linalg.norm(xm1)
+    np.testing.assert_allclose(ref["res"][:-1], dr["res"][:-1], rtol=1e-6, atol=1e-10 * dr["res"][0])
+    if problem == "swe":
+        assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-12 * abs(dic["m0"])
+        assert abs(0.5 * x @ dic["L"] @ x - dic["e0"]) <= 1e-12 * abs(dic["e0"])
