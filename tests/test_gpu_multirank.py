@@ -89,13 +89,18 @@ def test_several_ranks_on_one_gpu_match_single_gpu_and_oracle(tmp_path, problem,
     assert tr == trace1 == trace
     assert int(ref["steps"]) == ds["steps"] == dr["steps"]
     x = ref["x"]
-    # the reduction order differs from one GPU's (per-rank partials, then the sum over ranks):
-    # roundoff-level agreement, as the 2-rank gloo model (tests/test_distributed.py)
-    assert np.linalg.norm(x - xs) <= 1e-8 * np.linalg.norm(xs)
-    assert np.linalg.norm(x - xr) <= 1e-8 * np.linalg.norm(xr)
+    # the reduction order differs from one GPU's (per-rank partials, then the sum over ranks), so
+    # the iterates agree to roundoff as amplified by the problem: within 1e-8 relative, or within
+    # 10x the single-GPU solve's own distance from the oracle where that is larger (lkdv's
+    # constrained steps amplify roundoff to ~1e-7 relative: tests/test_gpu_parity.py C2)
+    def close(a, b, envelope):
+        return np.linalg.norm(a - b) <= max(1e-8 * np.linalg.norm(b), 10.0 * envelope)
+
+    env = np.linalg.norm(xs - xr)
+    assert close(x, xs, env) and close(x, xr, env)
     mid = int(ref["mid"])
-    xm1 = np.asarray(ds["x"][mid])
-    assert np.linalg.norm(ref["x_mid"] - xm1) <= 1e-8 * np.linalg.norm(xm1)
+    xm1, xmr = np.asarray(ds["x"][mid]), np.asarray(dr["x"][mid])
+    assert close(ref["x_mid"], xm1, np.linalg.norm(xm1 - xmr))
     np.testing.assert_allclose(ref["res"][:-1], dr["res"][:-1], rtol=1e-6, atol=1e-10 * dr["res"][0])
     if problem == "swe":
         assert abs(dic["omega"] @ x - dic["m0"]) <= 1e-12 * abs(dic["m0"])
