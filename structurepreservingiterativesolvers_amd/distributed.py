@@ -516,7 +516,9 @@ def bench_main(args, metric):
                 "orthogonalisation": getattr(args, "orthog", "mgs"),
                 "global_dof": n_glob,
                 "k": args.k,
-                "parallelism": f"row partition x{P}, RCCL allreduce + halo send/recv",
+                "parallelism": f"row partition x{P}, " + ("RCCL allreduce + halo send/recv" if comm.transport == "rccl" else
+                                                          "host-staged gloo collectives (SPIS_TRANSPORT=host: a "
+                                                          "rehearsal of the path, not a measurement)"),
                 "global_iterations_per_s": iters / elapsed,
             },
             "roofline": {
