@@ -26,10 +26,12 @@ processes (tests/test_distributed.py); the RCCL data path runs in
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import gc
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -195,6 +197,20 @@ def emulate_spmv(op: LocalOperator, plan: HaloPlan, x_local, exchange):
 # ------------------------------------------------------------------------------------------------
 # runtime: RCCL bootstrap + distributed handles
 # ------------------------------------------------------------------------------------------------
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """File descriptor 1 points at stderr inside the block (native libraries print there too)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def _host_collective(dist):
     """spis_host_coll_fn over torch.distributed (gloo): the in-place sum of an all-reduce, and a
     halo exchange's sends / receives to and from each neighbour (non-blocking, then all waited)."""
@@ -239,6 +255,12 @@ class Comm:
     not for measurement."""
 
     def __init__(self, ctx=None, transport=None):
+        # gloo reports its peer connections on stdout while the group forms; keep stdout for
+        # bench.py's one JSON line
+        with _stdout_to_stderr():
+            self._init(ctx, transport)
+
+    def _init(self, ctx, transport):
         import torch.distributed as dist
 
         if not dist.is_initialized():
