@@ -494,3 +494,18 @@ def test_host_transport_collectives(world):
         assert np.array_equal(a, np.arange(5) * tot)
         exp = np.concatenate([np.full(p + 1, 100.0 * p + rank) for p in peers])
         assert np.array_equal(recv, exp)
+
+
+def test_gloo_chatter_kept_off_stdout():
+    """Comm forms its gloo group with file descriptor 1 pointed at stderr (native libraries print
+    their peer connections there), so bench.py's stdout carries only the JSON line at N > 1."""
+    import subprocess
+    import sys
+
+    code = ("import os, sys; from structurepreservingiterativesolvers_amd.distributed import _stdout_to_stderr\n"
+            "with _stdout_to_stderr():\n    print('inside'); os.write(1, b'native\\n')\nprint('after')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == "after\n"
+    assert "inside" in r.stderr and "native" in r.stderr
