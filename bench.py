@@ -89,6 +89,26 @@ def k2s_used(n, k, chain):
     return chain in (3, 4) and k <= 32 and n <= 256 * 1024
 
 
+def orthog_label(n, k, chain, orthog):
+    """The arithmetic the run's orthogonalisation actually performs (variants that do
+    not round as MGS does are reported as such): "mgs" for per-step MGS and the K2p chain (MGS's
+    rounding), "mgs-lag2" for K2q (MGS with each dot taken two steps early by the distributive
+    law), "mgs-icwy" for K2w / K2s (MGS's projections in inverse-compact-WY one-reduce form), or
+    "cgs2"."""
+    if orthog == "cgs2":
+        return "cgs2"
+    if k2s_used(n, k, chain) or chain == 4 or (chain == 3 and (n + 1) // 2 > 255 * 512 * 4):
+        return "mgs-icwy"
+    return "mgs-lag2" if chain == 3 else "mgs"
+
+
+def mgs_one_read_bytes(n, k):
+    """Mean bytes of an Arnoldi step's orthogonalisation with the basis read ONCE: w and q_0 ..
+    q_j read, q_{j+1} written (8 N (j + 3)), + 16 N for the update GEMV it carries from j >= 1.
+    The figure a two-pass kernel (K2w: dots, then update) is also quoted against."""
+    return sum(8 * n * (j + 3) + (16 * n if j >= 1 else 0) for j in range(k)) / k
+
+
 def dual_bytes(n_rows, nnz, col_bytes=4):
     """Algorithmic bytes of the fused residual + Arnoldi SpMV: the matrix once, x_j and b read
     (true residual, solvers.py:290), z_{j+2} read and w written (Arnoldi, :191)."""
@@ -358,7 +378,14 @@ def main():
                 "achieved": mgs_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": None if mgs_gbs is None else mgs_gbs / HBM_PEAK_GBS,
                 "algorithmic_bytes_per_launch": mgs_b, "avg_launch_us": 1e3 * mgs_ms,
-                "launches": int(cnt[_lib.PROF_MGS]), "traffic": tr.get("mgs_solver")}
+                "launches": int(cnt[_lib.PROF_MGS]), "traffic": tr.get("mgs_solver"),
+                "orthogonalisation": orthog_label(n, args.k, args.chain, args.orthog)}
+    if roof_mgs["orthogonalisation"] == "mgs-icwy" and mgs_ms > 0:
+        # the one-read figure beside the kernel's own byte model (two passes for K2w)
+        b1 = mgs_one_read_bytes(n, args.k)
+        roof_mgs["one_read_bytes_per_launch"] = b1
+        roof_mgs["achieved_one_read"] = b1 / (mgs_ms * 1e-3) / 1e9
+        roof_mgs["frac_one_read"] = roof_mgs["achieved_one_read"] / HBM_PEAK_GBS
     # the dominant kernel by GPU time per solve (the contract's roofline object); the other beside it
     t_mgs = mgs_ms * k_per_solve(args.k)
     t_spmv = (dual_ms if fused else spmv_ms) * max(args.k - 2, 1)
@@ -400,7 +427,7 @@ def main():
             "workload": wl["desc"] + f", N={n:,} DoF, nnz={A.nnz:,}, CGMRES(k={args.k}, tol={args.tol:g})"
                         + (f" restarted x{wl['cycles']}" if wl["cycles"] > 1 else ""),
             "config": args.config,
-            "orthogonalisation": args.orthog,
+            "orthogonalisation": orthog_label(n, args.k, args.chain, args.orthog),
             "global_dof": n,
             "k": args.k,
             "parallelism": "single GPU",

@@ -34,10 +34,7 @@ inline uint64_t mix(uint64_t h) {  // murmur3's finaliser
 uint64_t piece_digest(const unsigned char* p, int64_t n, uint64_t index) {
   uint64_t a0 = 0x9E3779B97F4A7C15ull ^ index, a1 = 0xC2B2AE3D27D4EB4Full, a2 = 0x165667B19E3779F9ull,
            a3 = 0x27D4EB2F165667C5ull;
-  int64_t i = 0;
-  for (; i + 32 <= n; i += 32) {
-    uint64_t w[4];
-    std::memcpy(w, p + i, 32);
+  auto round = [&](const uint64_t* w) {
     a0 = (a0 ^ w[0]) * 0xff51afd7ed558ccdull;
     a1 = (a1 ^ w[1]) * 0xc4ceb9fe1a85ec53ull;
     a2 = (a2 ^ w[2]) * 0xff51afd7ed558ccdull;
@@ -46,10 +43,20 @@ uint64_t piece_digest(const unsigned char* p, int64_t n, uint64_t index) {
     a1 ^= a1 >> 29;
     a2 ^= a2 >> 29;
     a3 ^= a3 >> 29;
+  };
+  int64_t i = 0;
+  uint64_t w[4];
+  for (; i + 32 <= n; i += 32) {
+    std::memcpy(w, p + i, 32);
+    round(w);
   }
-  uint64_t tail = 0;
-  for (int s = 0; i < n; ++i, s = (s + 8) & 63) tail ^= static_cast<uint64_t>(p[i]) << s;
-  return mix(mix(a0) ^ mix(a1 + 1) ^ mix(a2 + 2) ^ mix(a3 + 3) ^ mix(tail ^ static_cast<uint64_t>(n)));
+  if (i < n) {  // the last < 32 bytes, zero-padded, through the same lanes: every byte keeps its
+                // position (a tail folded by shifts alone let bytes 8 apart commute)
+    std::memset(w, 0, sizeof w);
+    std::memcpy(w, p + i, static_cast<size_t>(n - i));
+    round(w);
+  }
+  return mix(mix(a0) ^ mix(a1 + 1) ^ mix(a2 + 2) ^ mix(a3 + 3) ^ mix(static_cast<uint64_t>(n)));
 }
 
 }  // namespace

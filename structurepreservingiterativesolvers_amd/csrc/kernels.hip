@@ -2233,7 +2233,7 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
       }
       if (__all(ok)) break;
       if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
-        if (lane == 0) atomicOr(err, 1u);
+        if (lane == 0) atomicOr(err, 2u);
         break;
       }
     }
@@ -2310,7 +2310,7 @@ __device__ __forceinline__ bool tag_get(const unsigned long long* sl, unsigned t
       return true;
     }
     if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
-      atomicOr(err, 1u);
+      atomicOr(err, 2u);
       *v = 0.0;
       return false;
     }
@@ -2335,7 +2335,7 @@ __device__ __forceinline__ double tag_sum(const unsigned long long* sl, int grid
     }
     if (__all(ok)) break;
     if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kChainWaitTicks) {
-      if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
+      if ((threadIdx.x & 63) == 0) atomicOr(err, 2u);
       break;
     }
   }

@@ -166,6 +166,7 @@ struct spis_context {
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
   unsigned* chain_err_dev = nullptr;
+  bool icwy_spin_off = false;  // a one-reduce hand-off (K2w fold / K2s) timed out: finalize launches
   std::vector<hipEvent_t> ev_free;
   struct Pending { int kind; hipEvent_t a, b; };
   std::vector<Pending> ev_pending;
@@ -2149,7 +2150,7 @@ struct Solver {
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
     if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
     // K2s: one GPU, small N: the whole step in one launch, the basis slices held in registers
-    if (!c->dist_on() && k2w_onepass && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
+    if (!c->dist_on() && k2w_onepass && !c->icwy_spin_off && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
       if (++c->icwy_tag == 0) c->icwy_tag = 1;
       const LaunchEv both{e_first.start, e_last.stop};
       HIP_TRY(launch_icwy_onepass(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_G, hcol, c->icwy_slots, c->icwy_tag,
@@ -2159,7 +2160,7 @@ struct Solver {
     }
     const int tw = k2w_tw >= 0 ? k2w_tw : chain_tw(nt);
     // (merged: the slack between the dots and partR is zeroed, since the all-reduce sums it too)
-    if (k2w_fold) {  // the dots reduced into d by the same launch (no finalize launch)
+    if (k2w_fold && !c->icwy_spin_off) {  // the dots reduced into d by the same launch (no finalize launch)
       if (++c->icwy_tag == 0) c->icwy_tag = 1;
       HIP_TRY(launch_icwy_dot(n, ws->w, Qv(0), ws->pitch, nv, nullptr, gc, s, &e_first, nt, tw, c->icwy_slots,
                               c->icwy_tag, d, merged ? kIcwyROff : 0, c->chain_err_dev));
@@ -2747,11 +2748,17 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ST_TRY(wait_event(c->ev_gram));
     prof_drain(c);
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
-    if (*reinterpret_cast<volatile unsigned*>(c->chain_err) != 0) {  // never on a healthy device
+    if (const unsigned ce = *reinterpret_cast<volatile unsigned*>(c->chain_err)) {  // never on a healthy device
       *c->chain_err = 0;
-      c->mgs_chain = 0;
-      return fail(SPIS_ERR_STATE, "persistent MGS chain: a workgroup never reached an exchange (the chain is "
-                                  "now disabled on this context; rerun the solve)");
+      // bit 0: a persistent MGS chain (K2p / K2b / K2q); bit 1: a one-reduce hand-off (the K2w
+      // dot pass's folded reduction, or K2s).  Each disables the kernels that spin on its own
+      // protocol, so the rerun takes launch boundaries instead (K2 launches; K2w's finalize)
+      if (ce & 1u) c->mgs_chain = 0;
+      if (ce & 2u) c->icwy_spin_off = true;
+      return fail(SPIS_ERR_STATE, (ce & 1u) ? "persistent MGS chain: a workgroup never reached an exchange (the chain "
+                                              "is now disabled on this context; rerun the solve)"
+                                            : "one-reduce MGS (K2w fold / K2s): a workgroup never reached a hand-off "
+                                              "(both are now disabled on this context; rerun the solve)");
     }
     if (stamps) {
       stamps[4 * k] = t_start;

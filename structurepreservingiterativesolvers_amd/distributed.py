@@ -286,9 +286,12 @@ class Comm:
         L = self.ctx.L
         self.transport = transport or os.environ.get("SPIS_TRANSPORT", "rccl")
         if self.transport == "host":
-            self._coll = _host_collective(dist)  # kept alive: the library holds the pointer
+            self._coll = _host_collective(dist)
             _lib.check(L.spis_comm_init_host(self.ctx.handle, self.world, self.rank, self._coll, None),
                        "spis_comm_init_host")
+            # the library keeps the raw function pointer on the (process-wide, cached) context:
+            # the thunk must live as long as the context, not as long as this Comm
+            self.ctx._host_coll = self._coll
         elif self.transport == "rccl":
             uid = (C.c_uint8 * 128)()
             if self.rank == 0:
@@ -535,7 +538,9 @@ def bench_main(args, metric):
                             + (f"; value = global iterations x {wl['norm']:.4g} (global DoF / the single-GPU "
                                "config's) / s" if wl["norm"] != 1.0 else "; value = global iterations / s"),
                 "config": config,
-                "orthogonalisation": getattr(args, "orthog", "mgs"),
+                # several GPUs: MGS's projections in one-reduce (inverse compact WY) form, K2w
+                "orthogonalisation": ("cgs2" if getattr(args, "orthog", "mgs") == "cgs2" else
+                                      "mgs-icwy" if getattr(args, "dist_mgs", 1) == 1 else "mgs"),
                 "global_dof": n_glob,
                 "k": args.k,
                 "parallelism": f"row partition x{P}, " + ("RCCL allreduce + halo send/recv" if comm.transport == "rccl" else

@@ -413,7 +413,23 @@ def _cp():
         _CHECKPOINTS.append(time.perf_counter())
 
 
+_MAX_STALE_RERUNS = 3
+
+
 def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
+    """One solve call.  A cached upload found stale by its content check (an operator edited in
+    place since it was uploaded) discards the run and solves again on the new contents, at most
+    ``_MAX_STALE_RERUNS`` times: an operator that changes during every solve (e.g. from a
+    callback) raises instead of looping."""
+    for _ in range(_MAX_STALE_RERUNS + 1):
+        r = _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing)
+        if r is not None:
+            return r
+    raise RuntimeError("an input operator changed in place during each of %d solves; "
+                       "the result cannot be trusted" % (_MAX_STALE_RERUNS + 1))
+
+
+def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     _cp()
     # a device matrix carries its context (distributed rank / communicator); else the default one
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
@@ -467,7 +483,9 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     if not all([chk.ok() for chk in checks]):  # an input matrix changed in place since its upload
         if status == _lib.OK and ws.value:
             ctx.L.spis_workspace_release(ws)
-        return _run(method, A, b, x0, k, tol, contol, conlist, pre, timing)
+        for key in [key for key in _SLSQP_MESSAGES if key[0] == id(ctx)]:  # the discarded run's
+            del _SLSQP_MESSAGES[key]
+        return None
     for item in keep:  # a Python exception inside a callback is re-raised as itself
         if isinstance(item, list) and item:
             raise item[0]

@@ -1063,10 +1063,17 @@ def test_full_size_swe_c5_cycle0_vs_oracle(spis):
     # inputs must take the device's branch (as in the C4 test), at SLSQP's minimum on "con"
     branch, sol, func, cl, _, terms = _slsqp_on_device_inputs(run_x, k, len(cons))
     assert branch == tdev[-1][1], (branch, tdev[-1])
+    arm = "same-as-oracle" if (trace[-1] == tdev[-1] and not bad) else "oracle-diverged"
+    ygap = float("nan")
     if branch == "con":
         yd = run_x.y[k - 1]
+        ygap = np.linalg.norm(yd - sol.x) / np.linalg.norm(sol.x)
+        assert ygap <= 1e-6, ygap  # the device's y is SLSQP's minimum on the same inputs (as C4)
         assert func(yd) <= func(sol.x) * (1 + 1e-9)
         _assert_invariants(cons, x)
+    print(f"C5 cycle 0 final step: device {tdev[-1]}, SLSQP on the device's inputs {branch!r}, "
+          f"oracle {trace[-1]} (SLSQP failure on its own inputs: {bool(bad)}), arm {arm}, "
+          f"|y_d - y_SLSQP|/|y_SLSQP| = {ygap:.3e}")
     if trace[-1] == tdev[-1] and not bad:  # the same final branch and iterate as the oracle
         # the constrained LS is SLSQP's on the oracle's side, stopped at ftol = ctol^2 = 1e-24 on
         # the objective: its y lies off the exact constrained minimiser by about the gap SLSQP

@@ -95,6 +95,31 @@ def test_content_digest_sees_every_entry():
             assert device.content_digest(B) != f
 
 
+@pytest.mark.parametrize("n", [5, 6, 7, 1001, 1002, 1003])
+def test_content_digest_sees_swapped_tail_entries(n):
+    """Swaps among the last (bytes mod 32) bytes: the tail is hashed by position, so swapping the
+    last two values, or indices[-1] with indices[-3] (8 bytes apart), changes the digest."""
+    rng = np.random.default_rng(n)
+    A = sps.csr_matrix(sps.random(n, n, density=0.3, random_state=rng) + sps.eye(n))
+    f = device.content_digest(A)
+    B = A.copy()
+    B.data[[-1, -2]] = B.data[[-2, -1]]
+    assert not np.array_equal(B.data, A.data) and device.content_digest(B) != f
+    C = A.copy()
+    C.indices[[-1, -3]] = C.indices[[-3, -1]]
+    if not np.array_equal(C.indices, A.indices):
+        assert device.content_digest(C) != f
+    for k in range(1, 32):  # one tail byte at every tail position, and a same-XOR pair 8 apart
+        raw = np.frombuffer(A.data.tobytes(), np.uint8).copy()
+        if k + 8 > raw.size:
+            break
+        raw[-k] ^= 0x5A
+        raw[-k - 8] ^= 0x5A
+        D = A.copy()
+        D.data = np.frombuffer(raw.tobytes(), np.float64).copy()
+        assert device.content_digest(D) != f
+
+
 def test_host_hash_independent_of_threads():
     import ctypes as C
 
