@@ -4,7 +4,7 @@
 set -e
 O=${1:-gpurun_out/r05mr}
 mkdir -p "$O"
-timeout -k 10 900 python -u -m pytest tests/test_gpu_multirank.py -x -v -s --timeout 400 --timeout-method thread -p no:cacheprovider > $O/multirank.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_multirank.py -v -s --timeout 400 --timeout-method thread -p no:cacheprovider > $O/multirank.log 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/c3.json 2> $O/c3.err
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "c5_cycle0" -x -v -s --timeout 500 --timeout-method thread -p no:cacheprovider > $O/c5c0.log 2>&1
 echo r05mr-done
