@@ -147,7 +147,7 @@ def load_traffic(args, c16, pipe):
     return t.get("bytes_per_launch", {}), f"{os.path.relpath(path, ROOT)} (git {t.get('git_rev')})"
 
 
-def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
+def cpu_baseline(dic, conlist, k, tol, budget_s, method="cgmres"):  # dic: the workload (A, b)
     """The oracle (CPU restatement of the reference solvers.cgmres, NumPy/SciPy +
     SLSQP exactly as the reference) on the same workload, bounded sample."""
     import oracle
@@ -164,8 +164,12 @@ def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
     solves = 0
     t0 = time.perf_counter()
     while True:
-        _, d = oracle.cgmres(dic["A"], dic["b"], x0, k, tol=tol, conlist=conlist)
-        iters += d["steps"]
+        if method == "cgmres_p":
+            _, d = oracle.cgmres_p(dic["A"], dic["b"], x0, k, conlist=conlist)
+            iters += len(d["res"])
+        else:
+            _, d = oracle.cgmres(dic["A"], dic["b"], x0, k, tol=tol, conlist=conlist)
+            iters += d["steps"]
         solves += 1
         if time.perf_counter() - t0 > budget_s or solves >= 3:
             break
@@ -176,7 +180,8 @@ def cpu_baseline(dic, conlist, k, tol, budget_s):  # dic: the workload (A, b)
         "cores": int(cores),
         "blas_threads": int(blas_threads),
         "kind": "port",
-        "sample": f"{solves} full CGMRES({k}) solve(s) of the same N={len(x0)} system ({iters} iterations, "
+        "sample": f"{solves} full {'CGMRES_P' if method == 'cgmres_p' else 'CGMRES'}({k}) solve(s) of the same "
+                  f"N={len(x0)} system ({iters} iterations, "
                   f"{dt:.1f} s); SciPy csr_matvec single-threaded, OpenBLAS {blas_threads} threads on "
                   f"{cores} affinity cores",
     }
@@ -230,6 +235,9 @@ def main():
     ap.add_argument("--cycles", type=int, default=10, help="restart cycles for c5")
     ap.add_argument("--k", type=int, default=30)
     ap.add_argument("--tol", type=float, default=1e-19)
+    ap.add_argument("--method", default="cgmres", choices=["cgmres", "cgmres_p"],
+                    help="cgmres (the BASELINE line) or cgmres_p (solvers.py:328-445: constraint i enforced from "
+                         "step i, every step constrained)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true", help="skip the standalone cold-cache SpMV timing")
@@ -289,7 +297,13 @@ def main():
     conlist = wl["conlist"]
     conlist_dev = device_constraints(conlist, ctx=ctx)
 
-    if wl["cycles"] > 1:
+    if args.method == "cgmres_p":
+        if wl["cycles"] > 1:
+            raise ValueError("cgmres_p is not restarted")
+
+        def solve():
+            return solvers.cgmres_p(Ad, bd, x0d, args.k, conlist=conlist_dev)
+    elif wl["cycles"] > 1:
         def solve():
             return solvers.cgmres_restarted(Ad, bd, x0d, args.k, wl["cycles"], tol=args.tol, conlist=conlist_dev)
     else:
@@ -318,7 +332,7 @@ def main():
         st = d["x"].stamps if "x" in d and hasattr(d["x"], "stamps") else None
         if st is not None:
             outside += (time.perf_counter() - ts) - (st[4 * args.k + 1] - st[4 * args.k])
-        iters += d["steps"]
+        iters += d["steps"] if "steps" in d else len(d["res"])
     ctx.synchronize()
     t1 = time.perf_counter()
     ms, cnt = _lib.profile_read(L, ctx.handle)
@@ -424,8 +438,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": wl["desc"] + f", N={n:,} DoF, nnz={A.nnz:,}, CGMRES(k={args.k}, tol={args.tol:g})"
+            "workload": wl["desc"] + f", N={n:,} DoF, nnz={A.nnz:,}, "
+                        + (f"CGMRES_P(k={args.k}, every step constrained)" if args.method == "cgmres_p" else
+                           f"CGMRES(k={args.k}, tol={args.tol:g})")
                         + (f" restarted x{wl['cycles']}" if wl["cycles"] > 1 else ""),
+            "method": args.method,
             "config": args.config,
             "orthogonalisation": orthog_label(n, args.k, args.chain, args.orthog),
             "global_dof": n,
@@ -448,7 +465,7 @@ def main():
         },
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(wl, conlist, args.k, args.tol, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(wl, conlist, args.k, args.tol, args.cpu_budget, args.method)
     print(json.dumps(out))
 
 

@@ -176,6 +176,14 @@ hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pi
                                const unsigned long long* seq = nullptr);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
                                hipStream_t s, int zero_to = 0);
+// the incremental constraint Gram's dots: part[i * grid + blk] = partial of L.v[i] . u (i < nvec);
+// reduce with launch_cgs_finalize(part, grid, nvec, ...)
+constexpr int kMdMax = 40;
+struct VecList {
+  const double* v[kMdMax];
+};
+hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
+                           hipStream_t s);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,

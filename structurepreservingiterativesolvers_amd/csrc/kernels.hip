@@ -1849,6 +1849,10 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
                                                             double* __restrict__ part, int px, YArg yx,
                                                             const double* __restrict__ x0, double* __restrict__ xo,
                                                             int64_t n_gx, CoefArg ca, int tw) {
+  // contraction off: every product rounded, then added, in all three one-reduce kernels (K2w's
+  // two passes and K2s), so their arithmetic is fixed by the source, not by the compiler's
+  // choice of fused multiply-adds in each kernel
+#pragma clang fp contract(off)
   __shared__ double s_c[kCgsMax];
   __shared__ double s_sum[4][4][64];  // [wave][element slot][lane]
   __shared__ double s_x[FX ? 4 : 1][4][64];
@@ -2018,6 +2022,68 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-dot for the incremental constraint Gram (spis.cpp con_inc_enqueue): part[i * grid + blk]
+// = the workgroup's partial of L.v[i] . u, i < nvec (<= kMdMax).  Vector i goes to wave i % 4 (as
+// cgs_dot): each wave reads u's chunk once for its vectors; 256-element chunks per workgroup
+// iteration (16-B loads when every pointer is 16-B aligned), a scalar tail otherwise; the products
+// are rounded, then added (contraction off); fixed-order wave sums.  Bytes: (nvec + 4) 8 N.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const double* __restrict__ u, VecList L,
+                                                          int nvec, bool vec, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  constexpr int kPerW = kMdMax / 4;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double acc[kPerW];
+#pragma unroll
+  for (int m = 0; m < kPerW; ++m) acc[m] = 0.0;
+  const int64_t n_vec = vec ? (n / kCgsChunk) * kCgsChunk : 0;
+  for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kCgsChunk; e0 < n_vec;
+       e0 += static_cast<int64_t>(gridDim.x) * kCgsChunk) {
+    const int64_t e = e0 + 2 * lane;
+    const double2 ua = *reinterpret_cast<const double2*>(u + e);
+    const double2 ub = *reinterpret_cast<const double2*>(u + e + 128);
+#pragma unroll
+    for (int m = 0; m < kPerW; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nvec) {
+        const double2 va = *reinterpret_cast<const double2*>(L.v[i] + e);
+        const double2 vb = *reinterpret_cast<const double2*>(L.v[i] + e + 128);
+        acc[m] += va.x * ua.x;
+        acc[m] += va.y * ua.y;
+        acc[m] += vb.x * ub.x;
+        acc[m] += vb.y * ub.y;
+      }
+    }
+  }
+  for (int64_t e = n_vec + static_cast<int64_t>(blockIdx.x) * 64 + lane; e < n; e += static_cast<int64_t>(gridDim.x) * 64) {
+    const double ue = u[e];
+#pragma unroll
+    for (int m = 0; m < kPerW; ++m) {
+      const int i = wid + 4 * m;
+      if (i < nvec) acc[m] += L.v[i][e] * ue;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < kPerW; ++m) {
+    const int i = wid + 4 * m;
+    if (i < nvec) {
+      const double t = wave_sum(acc[m]);
+      if (lane == 0) part[static_cast<int64_t>(i) * gridDim.x + blockIdx.x] = t;
+    }
+  }
+}
+
+hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
+                           hipStream_t s) {
+  if (nvec < 1 || nvec > kMdMax || grid < 1 || grid > kRedGrid) return hipErrorInvalidValue;
+  bool vec = aligned16d(u);
+  for (int i = 0; i < nvec; ++i) vec = vec && aligned16d(L.v[i]);
+  hipLaunchKernelGGL(multidot_kernel, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, vec, part);
+  return hipGetLastError();
+}
+
 // workgroup i reduces vector i's partials; add (nullable) + c -> h_out (host H column, nullable)
 // zero_to > gridDim.x: workgroup 0 also zeroes c[gridDim.x, zero_to) (the slack a merged
 // all-reduce carries beside the dots: summed every step, it must not grow)
@@ -2134,6 +2200,10 @@ __global__ __launch_bounds__(kBlock) void icwy_dot_kernel(int64_t n, const doubl
                                                           double* __restrict__ part, int tw,
                                                           unsigned long long* __restrict__ slots, unsigned tag,
                                                           double* __restrict__ d, int zero_to, unsigned* err) {
+  // contraction off: every product rounded, then added, in all three one-reduce kernels (K2w's
+  // two passes and K2s), so their arithmetic is fixed by the source, not by the compiler's
+  // choice of fused multiply-adds in each kernel
+#pragma clang fp contract(off)
   // rows [0, nv): q_l . w ; rows [nv, 2 nv - 1): q_l . q_{nv-1}, l < nv - 1
   __shared__ double s_wave[4];
   const int lane = threadIdx.x & 63;
@@ -2354,6 +2424,10 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
                                                               unsigned tag, unsigned* err, CoefArg ca, int px,
                                                               YArg yx, const double* __restrict__ x0,
                                                               double* __restrict__ xo, double* h_out) {
+  // contraction off: every product rounded, then added, in all three one-reduce kernels (K2w's
+  // two passes and K2s), so their arithmetic is fixed by the source, not by the compiler's
+  // choice of fused multiply-adds in each kernel
+#pragma clang fp contract(off)
   __shared__ double s_c[kCgsMax];
   __shared__ double s_sum[4][4][64];
   __shared__ double s_x[FX ? 4 : 1][4][64];

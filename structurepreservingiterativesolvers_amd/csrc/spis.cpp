@@ -117,6 +117,11 @@ struct spis_context {
   size_t cg_part_len = 0;
   double* cg_G = nullptr;              // its reduced output (64*64 + 4*64)
   double* cg_vpart = nullptr;          // K7t: the transpose's linear-term partials
+  double* inc_u = nullptr;             // incremental Gram: M z_a (n)
+  int64_t inc_u_len = 0;
+  double* inc_part = nullptr;          // its multidot partials (kMdMax x kRedGrid)
+  double* inc_res = nullptr;           // its reduced values (device), copied to con_pinned
+  size_t inc_res_len = 0;
   ncclComm_t comm = nullptr;
   // several ranks through a host callback instead of RCCL (spis_comm_init_host): the same
   // distributed code path with the collectives staged through host memory, so that several
@@ -225,6 +230,10 @@ struct ConCache {
   int cols = 0;
   double* Mx0 = nullptr;
   bool mx0_done = false;
+  // incremental Gram (con_step_*): the reduced entries of this solve's columns so far, index k = x0:
+  // gc(a, b) = z_a . M z_b, gv(a) = v . z_a; gcols = columns held (-1: none, x0's own terms neither)
+  int gcols = -1;
+  std::vector<double> gc, gv;
 };
 
 struct spis_workspace {
@@ -651,6 +660,9 @@ extern "C" int spis_context_destroy(spis_context* c) {
     if (c->cg_part) (void)hipFree(c->cg_part);
     if (c->cg_G) (void)hipFree(c->cg_G);
     if (c->cg_vpart) (void)hipFree(c->cg_vpart);
+    if (c->inc_u) (void)hipFree(c->inc_u);
+    if (c->inc_part) (void)hipFree(c->inc_part);
+    if (c->inc_res) (void)hipFree(c->inc_res);
     if (c->gram_ptrs) (void)hipFree(c->gram_ptrs);
     if (c->pinned) (void)hipHostFree(c->pinned);
     if (c->gram_pinned) (void)hipHostFree(c->gram_pinned);
@@ -1659,16 +1671,14 @@ static void con_terms_assemble(int m, const spis_constraint_desc* cons, int p, c
 }
 
 // fused path, synchronous: every launch of the step, then one wait
+struct ConStep;
+static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
+                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs);
+static void con_step_assemble(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons,
+                              const ConStep& cs, QuadCon* out);
 static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
                                   int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
-                                  QuadCon* out) {
-  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
-  ST_TRY(con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned));
-  HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
-  ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
-  con_terms_assemble(m, cons, p, c->con_pinned, out);
-  return SPIS_OK;
-}
+                                  QuadCon* out);
 
 // the fused reduction (con_gram_enqueue) serves this step
 static bool fused_con_ok(const spis_context* c, int p, int m, const spis_constraint_desc* cons) {
@@ -1744,12 +1754,237 @@ static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, cons
   return SPIS_OK;
 }
 
+// ---- incremental constraint Gram -------------------------------
+// A constrained step with p columns needs, per class-form constraint, G = U^T M U and v . U over
+// U = [z_0 .. z_{p-1}, x0] (solvers.py:33-36).  Within one solve Z and x0 never change, so the
+// entries of columns reduced at an earlier constrained step stay valid (ConCache gc / gv), and a
+// later step reduces only its new columns a: u = M z_a (one SpMV), then [z_0 .. z_a, x0] . u (one
+// multidot pass over a + 2 vectors) and v . z_a.  That is CGMRES's constrained suffix after the
+// first constrained step (solvers.py:230: every later step is constrained) and every step of
+// CGMRES_P (solvers.py:396-401), where the reference recomputes M @ Z and Z.T @ MZ whole.
+// Symmetric M only (gc(b, a) = gc(a, b) = z_b . M z_a; the K7t test, exact): a non-symmetric M's
+// quadratic term is not symmetric in the reference's algebra either, so it keeps the full path.
+// The first constrained step takes the full reduction (transpose + K7t) and seeds the caches,
+// unless its p is small enough that columns 0 .. p-1 from scratch cost less (kIncScratch).
+constexpr int kIncScratch = 8;
+
+struct ConStep {
+  bool inc = false;  // increments enqueued (else the full reduction)
+  int p = 0, m = 0;
+  std::vector<int> from;  // per constraint: first new column (inc)
+};
+
+static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
+  if (!fused_con_ok(c, p, m, cons) || p + 2 > kMdMax || static_cast<int>(ws->con.size()) < m) return false;
+  if (std::getenv("SPIS_GRAM_INC") != nullptr && std::atoi(std::getenv("SPIS_GRAM_INC")) == 0) return false;
+  for (int ci = 0; ci < m; ++ci) {
+    spis_matrix* M = cons[ci].M;
+    if (M == nullptr || M->all_zero) continue;
+    if (c->con_gram != 2) return false;  // the symmetric test is K7t's
+    SymTabView tv;
+    bool sym = false;
+    if (ensure_symtab(c, M, &tv, &sym) != SPIS_OK || !sym) return false;
+  }
+  return true;
+}
+
+// values one increment step writes (the order con_inc_take reads them)
+static size_t con_inc_len(int m, const spis_constraint_desc* cons, int p, const std::vector<int>& from,
+                          const spis_workspace* ws) {
+  size_t t = 0;
+  for (int ci = 0; ci < m; ++ci) {
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    for (int a = from[ci]; a < p; ++a) t += (hasM ? a + 2 : 0) + (cons[ci].v_dev ? 1 : 0);
+    if (ws->con[ci].gcols < 0) t += (hasM ? 1 : 0) + (cons[ci].v_dev ? 1 : 0);
+  }
+  return t;
+}
+
+static int con_inc_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
+                           int p, const double* Z, int64_t pitch, const double* x0, const ConStep& cs) {
+  hipStream_t st = c->stream;
+  const size_t total = con_inc_len(m, cons, p, cs.from, ws);
+  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, std::max<size_t>(total, 1)));
+  if (c->inc_u_len < n) {
+    if (c->inc_u) HIP_TRY(hipFree(c->inc_u));
+    HIP_TRY(hipMalloc(&c->inc_u, sizeof(double) * std::max<int64_t>(n, 1)));
+    c->inc_u_len = n;
+  }
+  if (!c->inc_part) HIP_TRY(hipMalloc(&c->inc_part, sizeof(double) * kMdMax * kRedGrid));
+  if (c->inc_res_len < total) {
+    if (c->inc_res) HIP_TRY(hipFree(c->inc_res));
+    HIP_TRY(hipMalloc(&c->inc_res, sizeof(double) * total));
+    c->inc_res_len = total;
+  }
+  const int g = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 255) / 256)));
+  size_t off = 0;
+  auto dots = [&](const double* u, const VecList& L, int nvec) -> int {
+    HIP_TRY(launch_multidot(n, u, L, nvec, c->inc_part, g, st));
+    HIP_TRY(launch_cgs_finalize(c->inc_part, g, nvec, c->inc_res + off, nullptr, nullptr, st));
+    off += static_cast<size_t>(nvec);
+    return SPIS_OK;
+  };
+  auto zv = [&](int a) { return Z + static_cast<int64_t>(a) * pitch; };
+  for (int ci = 0; ci < m; ++ci) {
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    for (int a = cs.from[ci]; a < p; ++a) {
+      if (hasM) {  // [z_0 .. z_a, x0] . M z_a
+        ST_TRY(spmv_local(c, ws, cons[ci].M, zv(a), c->inc_u));
+        VecList L{};
+        for (int b = 0; b <= a; ++b) L.v[b] = zv(b);
+        L.v[a + 1] = x0;
+        ST_TRY(dots(c->inc_u, L, a + 2));
+      }
+      if (cons[ci].v_dev) {  // v . z_a
+        VecList L{};
+        L.v[0] = cons[ci].v_dev;
+        ST_TRY(dots(zv(a), L, 1));
+      }
+    }
+    if (ws->con[ci].gcols < 0) {  // x0's own terms: x0 . M x0, v . x0
+      if (hasM) {
+        ST_TRY(spmv_local(c, ws, cons[ci].M, x0, c->inc_u));
+        VecList L{};
+        L.v[0] = x0;
+        ST_TRY(dots(c->inc_u, L, 1));
+      }
+      if (cons[ci].v_dev) {
+        VecList L{};
+        L.v[0] = cons[ci].v_dev;
+        ST_TRY(dots(x0, L, 1));
+      }
+    }
+  }
+  if (off != total) return fail(SPIS_ERR_STATE, "incremental Gram: %zu values, expected %zu", off, total);
+  if (total > 0) {
+    ST_TRY(allreduce_on(c, c->inc_res, static_cast<int64_t>(total), st));  // several GPUs: rows summed
+    HIP_TRY(hipMemcpyAsync(c->con_pinned, c->inc_res, sizeof(double) * total, hipMemcpyDeviceToHost, st));
+  }
+  return SPIS_OK;
+}
+
+// the increments into the caches (after the wait), in con_inc_enqueue's order
+static void con_inc_take(spis_workspace* ws, int m, const spis_constraint_desc* cons, const ConStep& cs,
+                         const double* src) {
+  const int k = ws->k;
+  auto G = [&](ConCache& cc, int a, int b) -> double& { return cc.gc[static_cast<size_t>(a) * (k + 1) + b]; };
+  size_t off = 0;
+  for (int ci = 0; ci < m; ++ci) {
+    ConCache& cc = ws->con[ci];
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    for (int a = cs.from[ci]; a < cs.p; ++a) {
+      if (hasM) {
+        for (int b = 0; b <= a; ++b) G(cc, a, b) = G(cc, b, a) = src[off + b];
+        G(cc, a, k) = G(cc, k, a) = src[off + a + 1];
+        off += static_cast<size_t>(a) + 2;
+      }
+      if (cons[ci].v_dev) cc.gv[a] = src[off++];
+    }
+    if (cc.gcols < 0) {
+      if (hasM) G(cc, k, k) = src[off++];
+      if (cons[ci].v_dev) cc.gv[k] = src[off++];
+    }
+    cc.gcols = cs.p;
+  }
+}
+
+// the full reduction's results (con_gram_enqueue's layout) into the caches
+static void con_full_take(spis_workspace* ws, int m, const spis_constraint_desc* cons, int p, const double* src) {
+  const int k = ws->k, np1 = p + 1;
+  const double* gvall = src + static_cast<size_t>(m) * np1 * np1;
+  int iv = 0;
+  for (int ci = 0; ci < m; ++ci) {
+    ConCache& cc = ws->con[ci];
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    const double* Gs = src + static_cast<size_t>(ci) * np1 * np1;
+    auto G = [&](int a, int b) -> double& { return cc.gc[static_cast<size_t>(a) * (k + 1) + b]; };
+    if (hasM)
+      for (int a = 0; a <= p; ++a)
+        for (int b = 0; b <= p; ++b) G(a == p ? k : a, b == p ? k : b) = Gs[static_cast<size_t>(a) * np1 + b];
+    if (cons[ci].v_dev) {
+      const double* gv = gvall + static_cast<size_t>(iv++) * np1;
+      for (int a = 0; a < p; ++a) cc.gv[a] = gv[a];
+      cc.gv[k] = gv[p];
+    }
+    cc.gcols = p;
+  }
+}
+
+// term0 / term1 / term2 (solvers.py:34-36) from the caches
+static void con_terms_from_cache(const spis_workspace* ws, int m, const spis_constraint_desc* cons, int p,
+                                 QuadCon* out) {
+  const int k = ws->k;
+  for (int ci = 0; ci < m; ++ci) {
+    const ConCache& cc = ws->con[ci];
+    auto G = [&](int a, int b) { return cc.gc[static_cast<size_t>(a) * (k + 1) + b]; };
+    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
+    const bool hasV = cons[ci].v_dev != nullptr;
+    QuadCon& q = out[ci];
+    q.term1.assign(p, 0.0);
+    q.term2.assign(static_cast<size_t>(p) * p, 0.0);
+    q.term0 = 0.5 * (hasM ? G(k, k) : 0.0) + cons[ci].c + (hasV ? cc.gv[k] : 0.0);
+    for (int a = 0; a < p; ++a) q.term1[a] = (hasV ? cc.gv[a] : 0.0) + (hasM ? G(k, a) : 0.0);
+    if (hasM)
+      for (int a = 0; a < p; ++a)
+        for (int b = 0; b < p; ++b) q.term2[static_cast<size_t>(a) * p + b] = 0.5 * G(a, b);
+  }
+}
+
+// one constrained step's reduction, enqueued on the main stream with its results copied to
+// c->con_pinned: the increments when every active constraint can take them, else the full
+// reduction (which seeds the caches when they are eligible)
+static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
+                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs) {
+  cs->p = p;
+  cs->m = m;
+  cs->inc = false;
+  cs->from.assign(m, 0);
+  if (con_inc_eligible(c, ws, m, cons, p)) {
+    bool fresh = false;  // a constraint without any cached column
+    for (int ci = 0; ci < m; ++ci) {
+      cs->from[ci] = std::max(0, std::min(ws->con[ci].gcols, p));
+      fresh = fresh || ws->con[ci].gcols < 0;
+    }
+    cs->inc = !fresh || p <= kIncScratch;
+  }
+  if (cs->inc) return con_inc_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, *cs);
+  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
+  return con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned);
+}
+
+// after the wait: the step's terms (and the caches brought up to date)
+static void con_step_assemble(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons,
+                              const ConStep& cs, QuadCon* out) {
+  if (cs.inc) {
+    con_inc_take(ws, cs.m, cons, cs, c->con_pinned);
+    con_terms_from_cache(ws, cs.m, cons, cs.p, out);
+    return;
+  }
+  con_terms_assemble(cs.m, cons, cs.p, c->con_pinned, out);
+  if (con_inc_eligible(c, ws, cs.m, cons, cs.p)) con_full_take(ws, cs.m, cons, cs.p, c->con_pinned);
+}
+
+// fused path, synchronous: the step's launches (increments or the full reduction), then one wait
+static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
+                                  int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
+                                  QuadCon* out) {
+  ConStep cs;
+  ST_TRY(con_step_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, &cs));
+  HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
+  ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
+  con_step_assemble(c, ws, cons, cs, out);
+  return SPIS_OK;
+}
+
 static int ensure_con_cache(spis_workspace* ws, size_t ncon, const spis_constraint_desc* cons) {
   if (ws->con.size() < ncon) ws->con.resize(ncon);
   for (size_t i = 0; i < ncon; ++i) {
     ConCache& cc = ws->con[i];
     cc.cols = 0;
     cc.mx0_done = false;
+    cc.gcols = -1;
+    cc.gc.assign(static_cast<size_t>(ws->k + 1) * (ws->k + 1), 0.0);
+    cc.gv.assign(static_cast<size_t>(ws->k + 1), 0.0);
     const bool mzero = cons[i].M == nullptr || cons[i].M->all_zero;
     if (!mzero && !cc.MZ) {
       HIP_TRY(hipMalloc(&cc.MZ, sizeof(double) * ws->pitch_n * ws->k));
@@ -2497,6 +2732,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     int deferred = -1;
     bool deferred_queued = false;
     int gram_queued = -1;  // iteration whose constraint reduction is already on the stream
+    ConStep gram_step;     // ... and what it enqueued (increments or the full reduction)
     int spec_kkt = -1;     // iteration whose KKT solve already ran (ycon, spec_kr)
     KKTResult spec_kr;
     // L mode: a forced constrained step's reduction (class-form constraints, fused path) is
@@ -2506,9 +2742,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
              fused_con_ok(c, jc + 1, o->n_constraints, o->constraints);
     };
     auto queue_gram = [&](int jc) -> int {
-      ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(o->n_constraints, jc + 1)));
-      ST_TRY(con_gram_enqueue(c, ws, o->n_constraints, o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, s,
-                              c->con_pinned));
+      ST_TRY(con_step_enqueue(c, ws, o->n_constraints, o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0,
+                              &gram_step));
       HIP_TRY(hipEventRecord(c->ev_gram, s));
       gram_queued = jc;
       return SPIS_OK;
@@ -2553,7 +2788,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         const double* hp = c->pinned + S.hoff(j);
         if (hp[j + 1] != 0.0) {
           ST_TRY(wait_event(c->ev_gram));
-          con_terms_assemble(o->n_constraints, o->constraints, j + 1, c->con_pinned, cons.data());
+          con_step_assemble(c, ws, o->constraints, gram_step, cons.data());
           if (!col_added) {
             for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
             qr.add_column(j, hcol.data());
@@ -2631,7 +2866,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           // terms assembled and the KKT solved before res_{j-1} was waited for (above)
         } else if (m_active > 0 && gram_queued == j && m_active == o->n_constraints) {
           ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
-          con_terms_assemble(m_active, o->constraints, p, c->con_pinned, cons.data());
+          con_step_assemble(c, ws, o->constraints, gram_step, cons.data());
         } else if (m_active > 0) {
           ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
                                       cons.data()));
