@@ -481,7 +481,7 @@ static int wait_event(hipEvent_t e) {
 
 // y = M x where x is a local vector (owned part valid); ghosts gathered through scratch if needed
 static int spmv_local(spis_context* c, spis_workspace* ws, const spis_matrix* M, const double* x,
-                      double* y) {
+                      double* y, hipStream_t st = nullptr) {  // st: one GPU only (several: c->stream)
   const int g = spmv_grid(M->view(), fixed_grid(c));
   if (c->dist_on() && M->n_ghost > 0) {
     if (!ws->ext || ws->ext_len < M->n_rows + M->n_ghost) {
@@ -494,7 +494,7 @@ static int spmv_local(spis_context* c, spis_workspace* ws, const spis_matrix* M,
     HIP_TRY(launch_spmv(M->view(), kEpiPlain, ws->ext, y, nullptr, nullptr, g, c->stream));
     return SPIS_OK;
   }
-  HIP_TRY(launch_spmv(M->view(), kEpiPlain, x, y, nullptr, nullptr, g, c->stream));
+  HIP_TRY(launch_spmv(M->view(), kEpiPlain, x, y, nullptr, nullptr, g, st != nullptr ? st : c->stream));
   return SPIS_OK;
 }
 
@@ -1673,7 +1673,7 @@ static void con_terms_assemble(int m, const spis_constraint_desc* cons, int p, c
 // fused path, synchronous: every launch of the step, then one wait
 struct ConStep;
 static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
-                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs);
+                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs, bool side);
 static void con_step_assemble(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons,
                               const ConStep& cs, QuadCon* out);
 static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons,
@@ -1772,6 +1772,7 @@ struct ConStep {
   bool inc = false;  // increments enqueued (else the full reduction)
   int p = 0, m = 0;
   std::vector<int> from;  // per constraint: first new column (inc)
+  hipStream_t st = nullptr;  // the stream the results are copied on (record the wait's event there)
 };
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
@@ -1802,7 +1803,7 @@ static size_t con_inc_len(int m, const spis_constraint_desc* cons, int p, const 
 
 static int con_inc_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
                            int p, const double* Z, int64_t pitch, const double* x0, const ConStep& cs) {
-  hipStream_t st = c->stream;
+  hipStream_t st = cs.st;
   const size_t total = con_inc_len(m, cons, p, cs.from, ws);
   ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, std::max<size_t>(total, 1)));
   if (c->inc_u_len < n) {
@@ -1829,7 +1830,7 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, int m, const spi
     const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
     for (int a = cs.from[ci]; a < p; ++a) {
       if (hasM) {  // [z_0 .. z_a, x0] . M z_a
-        ST_TRY(spmv_local(c, ws, cons[ci].M, zv(a), c->inc_u));
+        ST_TRY(spmv_local(c, ws, cons[ci].M, zv(a), c->inc_u, st));
         VecList L{};
         for (int b = 0; b <= a; ++b) L.v[b] = zv(b);
         L.v[a + 1] = x0;
@@ -1843,7 +1844,7 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, int m, const spi
     }
     if (ws->con[ci].gcols < 0) {  // x0's own terms: x0 . M x0, v . x0
       if (hasM) {
-        ST_TRY(spmv_local(c, ws, cons[ci].M, x0, c->inc_u));
+        ST_TRY(spmv_local(c, ws, cons[ci].M, x0, c->inc_u, st));
         VecList L{};
         L.v[0] = x0;
         ST_TRY(dots(c->inc_u, L, 1));
@@ -1934,10 +1935,11 @@ static void con_terms_from_cache(const spis_workspace* ws, int m, const spis_con
 // c->con_pinned: the increments when every active constraint can take them, else the full
 // reduction (which seeds the caches when they are eligible)
 static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
-                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs) {
+                            int p, const double* Z, int64_t pitch, const double* x0, ConStep* cs, bool side) {
   cs->p = p;
   cs->m = m;
   cs->inc = false;
+  cs->st = c->stream;
   cs->from.assign(m, 0);
   if (con_inc_eligible(c, ws, m, cons, p)) {
     bool fresh = false;  // a constraint without any cached column
@@ -1947,7 +1949,12 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     }
     cs->inc = !fresh || p <= kIncScratch;
   }
-  if (cs->inc) return con_inc_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, *cs);
+  if (cs->inc) {
+    // side: the increments on stream2, beside the latency-bound MGS chain the host has just queued
+    // (they read only z_0 .. z_{p-1}, finished by earlier chains, x0 and the constraint operators)
+    if (side && !c->dist_on()) cs->st = c->stream2;
+    return con_inc_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, *cs);
+  }
   ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
   return con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned);
 }
@@ -1969,7 +1976,7 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                   int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                   QuadCon* out) {
   ConStep cs;
-  ST_TRY(con_step_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, &cs));
+  ST_TRY(con_step_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, &cs, false));
   HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
   ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
   con_step_assemble(c, ws, cons, cs, out);
@@ -2737,14 +2744,16 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     KKTResult spec_kr;
     // L mode: a forced constrained step's reduction (class-form constraints, fused path) is
     // queued ahead of the residual of the iterate before it (queue_gram)
+    // the constraints step jc enforces: all of them (CGMRES), clist[:jc] (CGMRES_P, solvers.py:412)
+    auto m_of = [&](int jc) { return o->method == SPIS_CGMRES_P ? std::min(jc, o->n_constraints) : o->n_constraints; };
     auto gram_early_ok = [&](int jc) {
-      return o->method == SPIS_CGMRES && !use_cb && o->n_constraints > 0 &&
-             fused_con_ok(c, jc + 1, o->n_constraints, o->constraints);
+      return (o->method == SPIS_CGMRES || o->method == SPIS_CGMRES_P) && !use_cb && m_of(jc) > 0 &&
+             fused_con_ok(c, jc + 1, m_of(jc), o->constraints);
     };
-    auto queue_gram = [&](int jc) -> int {
-      ST_TRY(con_step_enqueue(c, ws, o->n_constraints, o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0,
-                              &gram_step));
-      HIP_TRY(hipEventRecord(c->ev_gram, s));
+    auto queue_gram = [&](int jc, bool side = false) -> int {
+      ST_TRY(con_step_enqueue(c, ws, m_of(jc), o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, &gram_step,
+                              side));
+      HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
       gram_queued = jc;
       return SPIS_OK;
     };
@@ -2779,7 +2788,11 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       // L mode, a step that is constrained whatever res_{j-1} says (the forced last step, or
       // safety set, :230): its reduction goes on the stream now, behind c_{j+1} / U_{j-1}'s
       // residual, not after the host has waited for that residual (C3: a 20 us gap before it)
-      if (L && gram_queued != j && (j == k - 1 || safety != kSafetyNone) && gram_early_ok(j)) ST_TRY(queue_gram(j));
+      // (CGMRES_P: every step from j = 1 is constrained, solvers.py:396-401; its increments go beside
+      // the chain just queued)
+      if (L && gram_queued != j && (o->method == SPIS_CGMRES_P || j == k - 1 || safety != kSafetyNone) &&
+          gram_early_ok(j))
+        ST_TRY(queue_gram(j, true));
       // ... and when U_{j-1}'s residual cannot stop the run (safety is not True) and the step
       // is not timed, LS_j's KKT solve runs now, while the GPU still works on that residual
       // (it was queued behind this reduction, see the end of the iteration); the result is
@@ -2788,7 +2801,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         const double* hp = c->pinned + S.hoff(j);
         if (hp[j + 1] != 0.0) {
           ST_TRY(wait_event(c->ev_gram));
-          con_step_assemble(c, ws, o->constraints, gram_step, cons.data());
+          con_step_assemble(c, ws, o->constraints, gram_step, cons.data());  // (gram_step.m constraints)
           if (!col_added) {
             for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
             qr.add_column(j, hcol.data());
@@ -2796,7 +2809,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           }
           std::fill(y0.begin(), y0.end(), 0.0);
           for (int a = 0; a < j; ++a) y0[a] = yk[a];
-          spec_kr = kkt_newton(j + 1, qr.R(), qr.ld(), qr.g(), o->n_constraints, cons.data(), y0.data(), ycon.data());
+          spec_kr = kkt_newton(j + 1, qr.R(), qr.ld(), qr.g(), gram_step.m, cons.data(), y0.data(), ycon.data());
           spec_kkt = j;
         }
       }
@@ -2862,9 +2875,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       } else {
         // class-form constraints reduced on the device (:242-247), KKT on the host (:251-255)
         if (stamps) stamps[2 * k + j] = now_s();
-        if (m_active > 0 && spec_kkt == j && m_active == o->n_constraints) {
+        if (m_active > 0 && spec_kkt == j && m_active == gram_step.m) {
           // terms assembled and the KKT solved before res_{j-1} was waited for (above)
-        } else if (m_active > 0 && gram_queued == j && m_active == o->n_constraints) {
+        } else if (m_active > 0 && gram_queued == j && m_active == gram_step.m) {
           ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
           con_step_assemble(c, ws, o->constraints, gram_step, cons.data());
         } else if (m_active > 0) {
@@ -2876,7 +2889,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (m_active == 0) {
           qr.solve(p, ycon.data());
         } else {
-          const KKTResult kr = (spec_kkt == j && m_active == o->n_constraints)
+          const KKTResult kr = (spec_kkt == j && m_active == gram_step.m)
                                    ? spec_kr
                                    : kkt_newton(p, qr.R(), qr.ld(), qr.g(), m_active, cons.data(), y0.data(), ycon.data());
           msg = kr.message;

@@ -713,6 +713,113 @@ int main(int argc, char** argv) {
     printf("cap 4096 vs 2048, dual rows: %lld differ\n", (long long)bad);
     return 0;
   }
+  if (argc > 2 && std::string(argv[2]) == "win") {
+    // K1w (windowed gathers, kernels.hip spmv_win_kernel) against K1dp, both on slab-ordered
+    // tables (K1w's split by windows of <= kWinChunks 64-column chunks), warm and cold; dual rows
+    // bitwise against K1dp
+    double *dx2, *dw, *db, *pa, *pb;
+    CK(hipMalloc(&dx2, 8 * pitch));
+    CK(hipMalloc(&dw, 8 * pitch));
+    CK(hipMalloc(&db, 8 * pitch));
+    CK(hipMalloc(&pa, 8 * 16384));
+    CK(hipMalloc(&pb, 8 * 16384));
+    std::vector<double> h2(pitch);
+    for (int64_t i = 0; i < pitch; ++i) h2[i] = i < n ? 1e-3 * ((i * 104729) % 997) - 0.4 : 0.0;
+    CK(hipMemcpy(dx2, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, h2.data(), 8 * pitch, hipMemcpyHostToDevice));
+    const double SD = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n;
+    const double SW = 10.0 * nnz + 4.0 * (n + 1) + 32.0 * n;  // K1w: 16-bit window positions
+    std::vector<int32_t> blk, pairs, bw, pw;
+    blocks(n, rp.data(), kPipeCap, 256, kPipeCap, blk);
+    std::vector<uint8_t> lab;
+    std::vector<double> key;
+    std::vector<int64_t> order, ow;
+    if (!slab_labels(n, rp.data(), ci.data(), lab, &key) || !build_slab_order(rp.data(), lab, blk, pairs, &order, &key)) {
+      printf("no slab order\n");
+      return 1;
+    }
+    bw = blk;
+    const auto tb = std::chrono::steady_clock::now();
+    if (!win_split_blocks(rp.data(), ci.data(), bw) || !build_slab_order(rp.data(), lab, bw, pw, &ow, &key)) {
+      printf("no window table\n");
+      return 1;
+    }
+    std::vector<int32_t> chunks;
+    std::vector<uint16_t> lidx;
+    win_build(rp.data(), ci.data(), bw, ow, chunks, lidx);
+    const double tbuild = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
+    const int nb = static_cast<int>(blk.size()) - 1, nbw = static_cast<int>(bw.size()) - 1;
+    int2 *ms, *msw;
+    int32_t* dch;
+    uint16_t* dli;
+    CK(hipMalloc(&ms, 4 * pairs.size()));
+    CK(hipMemcpy(ms, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&msw, 4 * pw.size()));
+    CK(hipMemcpy(msw, pw.data(), 4 * pw.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dch, 4 * chunks.size()));
+    CK(hipMemcpy(dch, chunks.data(), 4 * chunks.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dli, 2 * lidx.size()));
+    CK(hipMemcpy(dli, lidx.data(), 2 * lidx.size(), hipMemcpyHostToDevice));
+    const int64_t big = int64_t(1) << 26;
+    double* bx;
+    CK(hipMalloc(&bx, 8 * big));
+    CK(hipMemset(bx, 0, 8 * big));
+    const int gr = resident_grid(spmv_pipe_var_kernel<kPipeCap, 4>);
+    const int gw = resident_grid(spmv_win_kernel<kPipeCap, 4>);
+    printf("blocks %d (K1w %d after the window split, table built in %.2f s), resident grid %d / K1w %d\n", nb, nbw,
+           tbuild, gr, gw);
+    auto run = [&](const char* name, double bytes, auto&& launch) {
+      for (int cold = 0; cold < 2; ++cold) {
+        double tot = 0;
+        const int reps = 30;
+        for (int r = 0; r < reps + 3; ++r) {
+          if (cold) hipLaunchKernelGGL(read2_kernel, dim3(4096), dim3(kBlock), 0, s, big / 2,
+                                       reinterpret_cast<const double2*>(bx), pb + 8192);
+          launch();
+          CK(hipEventSynchronize(e1));
+          float ms_;
+          CK(hipEventElapsedTime(&ms_, e0, e1));
+          if (r >= 3) tot += ms_;
+        }
+        const double us = 1e3 * tot / reps;
+        printf("%s %-40s %8.2f us  %7.0f GB/s  (%.3f of 8 TB/s; K1dp bytes %.3f)\n", cold ? "COLD" : "WARM", name, us,
+               bytes / (us * 1e-6) / 1e9, bytes / (us * 1e-6) / 8e12, SD / (us * 1e-6) / 8e12);
+      }
+    };
+    auto k1dp = [&] {
+      hipExtLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4>), dim3(gr), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva, ms,
+                            nb, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr,
+                            (const int4*)nullptr);
+    };
+    auto k1w = [&](int g) {
+      hipExtLaunchKernelGGL((spmv_win_kernel<kPipeCap, 4>), dim3(g), dim3(kBlock), 0, s, e0, e1, 0, drp, dci, dva, dli, dch,
+                            msw, nbw, 2, dx, db, pa, dx2, dQ, dw, pb);
+    };
+    run("K1dp slab (the solver's)", SD, k1dp);
+    run("K1w slab, windows", SW, [&] { k1w(gw); });
+    for (int g : {256, 768}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "K1w slab, windows, grid %d", g);
+      run(nm, SW, [&] { k1w(g); });
+    }
+    std::vector<double> w1(n), w2(n), p1(16384), p2(16384);
+    k1dp();
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+    CK(hipMemset(dw, 0, 8 * n));
+    k1w(gw);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(w2.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+    std::vector<double> hb(n), hw(n);
+    double res_ref = 0, res_w = 0;
+    CK(hipMemcpy(p1.data(), pa, 8 * gw, hipMemcpyDeviceToHost));
+    for (int i = 0; i < gw; ++i) res_w += p1[i];
+    printf("K1w vs K1dp dual rows: %lld differ; K1w ||r||^2 partial sum %.17g\n", (long long)bad, res_w);
+    (void)res_ref;
+    return bad ? 1 : 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "slab") {
     // the solver's dual (kPipeCap table) in natural vs slab block order, resident grid vs more
     // workgroups, nontemporal matrix loads; warm (back to back: the matrix Infinity-Cache
@@ -795,6 +902,16 @@ int main(int argc, char** argv) {
   })
     SLABRUN("natural", false, 1, mn, 1, gr);
     SLABRUN("slab", false, 1, ms, 2, gr);
+#define FAKERUN(LABEL, FG)                                                                                      \
+  snprintf(nm, sizeof nm, "%s grid=%d", LABEL, gr);                                                            \
+  run(nm, [&] {                                                                                                \
+    hipExtLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, false, 1, false, false, false, FG>), dim3(gr), dim3(kBlock), 0, s, \
+                          e0, e1, 0, drp, dci, dva, ms, nb, 2, dx, db, (double*)nullptr, pa, dx2, dQ, dw, pb,          \
+                          (const uint16_t*)nullptr, (const int4*)nullptr);                                      \
+  })
+    FAKERUN("slab, gathers -> coalesced rows (probe)", 1);
+    FAKERUN("slab, gathers -> one address (probe)", 2);
+#undef FAKERUN
     for (int g : {512, 1024, 1280}) { SLABRUN("slab", false, 1, ms, 2, g); }
     SLABRUN("slab NT", true, 1, ms, 2, gr);
     SLABRUN("slab WPE2", false, 2, ms, 2, gr);

@@ -145,7 +145,10 @@ __device__ __forceinline__ void pipe_load_v(PipeStage<CAP>& st, const int2* __re
 // C16: columns from the 16-bit copy (c16, per-block bases; col16.h)
 // BUF: the matrix stream and the gathers through buffer descriptors (32-bit lane offsets), which
 // frees the registers for WPE = 4 waves per SIMD (4 workgroups per CU instead of 3)
-template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false, bool TM = false>
+// FAKEG (timing probe only, wrong results): 1 = the x gathers replaced by coalesced loads of the
+// block's own row range, 2 = by one broadcast address: what the kernel costs without gather latency
+template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false, bool TM = false,
+          int FAKEG = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE > 3 ? WPE : (C16 ? 3 : 8)))) void spmv_pipe_var_kernel(
     const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
@@ -213,7 +216,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
     double g1[kPer], g2[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
+      int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
+      if constexpr (FAKEG == 1) c = min(cur.r0 + ((threadIdx.x + u * kBlock) & 255), cur.r1 - 1);
+      if constexpr (FAKEG == 2) c = cur.r0;
       if constexpr (BUF) {
         g1[u] = buf_ld1(rx1, c * 8);
         if (DUAL) g2[u] = buf_ld1(rx2, c * 8);
