@@ -168,6 +168,8 @@ hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pit
 constexpr int64_t kIcwySlotWords = 2 * (2 * kCgsMax - 1) * static_cast<int64_t>(kRedGrid) + 2 * (2 * kCgsMax - 1) +
                                    2 * static_cast<int64_t>(kRedGrid) + 2;
 int icwy_onepass_max_grid();
+// the largest n K2s takes: one resident 256-element chunk per workgroup, or two (the second streamed)
+int64_t icwy_onepass_max_n();
 hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pitch, int nv, double* G, double* h_col,
                                unsigned long long* slots, unsigned tag, unsigned* err, hipStream_t s,
                                const LaunchEv* ev, int px = 0, const double* yx = nullptr,
@@ -184,6 +186,11 @@ struct VecList {
 };
 hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
                            hipStream_t s);
+// K6i: u = M x (not stored) and, in the same pass, the partials of L.v[i] . u (i < nl) followed by
+// those of P.v[i] . Q.v[i] (i < np <= kGramPairMax); M needs K1's row-block table (blk_row)
+constexpr int kGramPairMax = 8;
+hipError_t launch_spmv_gram(const CsrView& M, const double* x, const VecList& L, int nl, const VecList& P,
+                            const VecList& Q, int np, double* part, int grid, hipStream_t s);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,

@@ -2258,6 +2258,116 @@ hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nve
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// K6i: one constrained step's increments in one pass (spis.cpp con_inc_enqueue): u = M x by K1's
+// row blocks (u[r] bit-identical to K1's), never stored: each row's u[r] goes straight into the
+// partials of L.v[i] . u (i < nl), and the same row's P.v[i][r] * Q.v[i][r] into the partials of
+// the pair dots (i < np: v . z_a of the linear constraints).  Rows are the SpMV's (every row once),
+// so a pair dot covers [0, n) like any other.  part[i * gridDim.x + blk], i < nl + np, for
+// cgs_finalize.  Products rounded, then added (contraction off).  Bytes: M's nnz (12 B) + x
+// gathers + (nl + 2 np) 8 n: no u write and re-read, and one launch instead of a SpMV, a
+// multidot and a dot with a finalize each.
+// ---------------------------------------------------------------------------------------------
+template <int NL>
+__global__ __launch_bounds__(kBlock) void spmv_gram_kernel(
+    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
+    const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ x, VecList L, int nl, VecList P,
+    VecList Q, int np, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double s_prod[kNnzCap];
+  __shared__ double s_red[(NL + kGramPairMax) * 4];
+  __shared__ double s_wave[4];
+  double acc[NL], accp[kGramPairMax];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) acc[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < kGramPairMax; ++i) accp[i] = 0.0;
+  auto row_done = [&](int r, double sum) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+      if (i < nl) acc[i] += L.v[i][r] * sum;
+#pragma unroll
+    for (int i = 0; i < kGramPairMax; ++i)
+      if (i < np) accp[i] += P.v[i][r] * Q.v[i][r];
+  };
+  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
+    const int r0 = blk_row[blk];
+    const int r1 = blk_row[blk + 1];
+    const int nz0 = rp[r0];
+    const int nnz = rp[r1] - nz0;
+    if (nnz > kNnzCap) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
+      double a = 0.0;
+      for (int i = nz0 + threadIdx.x; i < nz0 + nnz; i += kBlock) a += va[i] * x[ci[i]];
+      const double sum = block_sum(a, s_wave);
+      if (threadIdx.x == 0) row_done(r0, sum);
+      continue;
+    }
+    constexpr int kPer = kNnzCap / kBlock;
+    int cols[kPer];
+    double vals[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      cols[u] = i < nnz ? ci[nz0 + i] : 0;
+      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
+    }
+    double xs[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) xs[u] = x[cols[u]];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = threadIdx.x + u * kBlock;
+      if (i < nnz) s_prod[i] = vals[u] * xs[u];
+    }
+    __syncthreads();
+    const int r = r0 + threadIdx.x;
+    if (r < r1) {
+      const int s = rp[r] - nz0;
+      const int e = rp[r + 1] - nz0;
+      double sum = 0.0;
+      for (int t = s; t < e; ++t) sum += s_prod[t];
+      row_done(r, sum);
+    }
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+    if (i < nl) {
+      const double t = wave_sum(acc[i]);
+      if (lane == 0) s_red[i * 4 + wid] = t;
+    }
+#pragma unroll
+  for (int i = 0; i < kGramPairMax; ++i)
+    if (i < np) {
+      const double t = wave_sum(accp[i]);
+      if (lane == 0) s_red[(nl + i) * 4 + wid] = t;
+    }
+  __syncthreads();
+  if (static_cast<int>(threadIdx.x) < nl + np) {
+    const double* w = s_red + threadIdx.x * 4;
+    part[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = ((w[0] + w[1]) + w[2]) + w[3];
+  }
+}
+
+hipError_t launch_spmv_gram(const CsrView& M, const double* x, const VecList& L, int nl, const VecList& P,
+                            const VecList& Q, int np, double* part, int grid, hipStream_t s) {
+  if (M.blk_row == nullptr || nl < 0 || nl > kMdMax || np < 0 || np > kGramPairMax || nl + np < 1 || grid < 1 ||
+      grid > kRedGrid)
+    return hipErrorInvalidValue;
+  dim3 g(grid), b(kBlock);
+#define SPIS_SG(NLV)                                                                                        \
+  hipLaunchKernelGGL(spmv_gram_kernel<NLV>, g, b, 0, s, M.indptr, M.indices, M.vals, M.blk_row, M.n_blk, x, \
+                     L, nl, P, Q, np, part)
+  if (nl <= 8) SPIS_SG(8);
+  else if (nl <= 16) SPIS_SG(16);
+  else if (nl <= 24) SPIS_SG(24);
+  else if (nl <= 32) SPIS_SG(32);
+  else SPIS_SG(kMdMax);
+#undef SPIS_SG
+  return hipGetLastError();
+}
+
 // workgroup i reduces vector i's partials; add (nullable) + c -> h_out (host H column, nullable)
 // zero_to > gridDim.x: workgroup 0 also zeroes c[gridDim.x, zero_to) (the slack a merged
 // all-reduce carries beside the dots: summed every step, it must not grow)
@@ -2593,7 +2703,7 @@ __device__ __forceinline__ double tag_sum(const unsigned long long* sl, int grid
   return block_sum(v, s_wave);
 }
 
-template <bool FX>
+template <bool FX, bool TWO>
 __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, double* __restrict__ w,
                                                               const double* __restrict__ Q, double* __restrict__ qn,
                                                               int64_t pitch, int nv, unsigned long long* slots,
@@ -2617,6 +2727,10 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
   const int nval = 2 * nv - 1;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const int64_t e = static_cast<int64_t>(blockIdx.x) * kCgsChunk + 2 * lane;  // e, e+1, e+128, e+129
+  // TWO: the workgroup also owns chunk blockIdx.x + grid (when it exists), streamed from memory in
+  // both passes instead of held in registers (n up to twice the resident chunks)
+  const int64_t e2 = (static_cast<int64_t>(blockIdx.x) + grid) * kCgsChunk + 2 * lane;
+  const bool two = TWO && (static_cast<int64_t>(blockIdx.x) + grid) * kCgsChunk < n;
   auto ld2 = [&](const double* p, int64_t i) -> double2 {
     if (i + 1 < n) return *reinterpret_cast<const double2*>(p + i);
     return make_double2(i < n ? p[i] : 0.0, 0.0);
@@ -2639,7 +2753,14 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
   {
     const double* ql = Q + static_cast<int64_t>(nv - 1) * pitch;
     const double2 la = ld2(ql, e), lb = ld2(ql, e + 128);
-    // 1. the dots, icwy_dot's arithmetic
+    double2 wa2 = make_double2(0.0, 0.0), wb2 = wa2, la2 = wa2, lb2 = wa2;
+    if (two) {
+      wa2 = ld2(w, e2);
+      wb2 = ld2(w, e2 + 128);
+      la2 = ld2(ql, e2);
+      lb2 = ld2(ql, e2 + 128);
+    }
+    // 1. the dots, icwy_dot's arithmetic (TWO: the second chunk's products after the first's)
 #pragma unroll
     for (int m = 0; m < kCgsPerWave; ++m) {
       const int i = wid + 4 * m;
@@ -2655,11 +2776,22 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
     for (int m = 0; m < kCgsPerWave; ++m) {
       const int i = wid + 4 * m;
       if (i < nv) {
+        double2 qa2 = make_double2(0.0, 0.0), qb2 = qa2;
+        if (two) {
+          qa2 = ld2(Qw + m * step, e2);
+          qb2 = ld2(Qw + m * step, e2 + 128);
+        }
         double acc = 0.0, acg = 0.0;
         acc += qa[m].x * wa.x;
         acc += qa[m].y * wa.y;
         acc += qb[m].x * wb.x;
         acc += qb[m].y * wb.y;
+        if (two) {
+          acc += qa2.x * wa2.x;
+          acc += qa2.y * wa2.y;
+          acc += qb2.x * wb2.x;
+          acc += qb2.y * wb2.y;
+        }
         acc = wave_sum(acc);
         if (lane == 0) tag_put(slots + 2 * (static_cast<int64_t>(i) * grid + blockIdx.x), tag, acc);
         if (i < nv - 1) {
@@ -2667,6 +2799,12 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
           acg += qa[m].y * la.y;
           acg += qb[m].x * lb.x;
           acg += qb[m].y * lb.y;
+          if (two) {
+            acg += qa2.x * la2.x;
+            acg += qa2.y * la2.y;
+            acg += qb2.x * lb2.x;
+            acg += qb2.y * lb2.y;
+          }
           acg = wave_sum(acg);
           if (lane == 0) tag_put(slots + 2 * (static_cast<int64_t>(nv + i) * grid + blockIdx.x), tag, acg);
         }
@@ -2689,62 +2827,83 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
     const double t = sum_partials(ca.rpart, ca.r_in, s_wave);
     if (threadIdx.x == 0) publish(ca.r_out, t, ca.flag, ca.seq);
   }
-  // 4. cgs_update's arithmetic on the register slices
-  double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-  double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
+  // 4. cgs_update's arithmetic on one chunk's slices (the register ones, or TWO's second chunk
+  // loaded again): w' = w - sum (stored), the fused GEMV, wave 0's ||w'||^2 terms into a0
+  double a0 = 0.0;
+  auto update = [&](int64_t ec, const double2 (&ua)[kCgsPerWave], const double2 (&ub)[kCgsPerWave], double2 va,
+                    double2 vb, double2 xa, double2 xb, double (&t)[4]) __attribute__((always_inline)) {
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
 #pragma unroll
-  for (int m = 0; m < kCgsPerWave; ++m) {
-    if (wid + 4 * m < nv) {
-      const double cm = s_c[wid + 4 * m];
-      p0 += cm * qa[m].x;
-      p1 += cm * qa[m].y;
-      p2 += cm * qb[m].x;
-      p3 += cm * qb[m].y;
-      if (FX && wid + 4 * m < px) {
-        const double ym = yx.v[wid + 4 * m];
-        g0 = fma(ym, qa[m].x, g0);
-        g1 = fma(ym, qa[m].y, g1);
-        g2 = fma(ym, qb[m].x, g2);
-        g3 = fma(ym, qb[m].y, g3);
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      if (wid + 4 * m < nv) {
+        const double cm = s_c[wid + 4 * m];
+        p0 += cm * ua[m].x;
+        p1 += cm * ua[m].y;
+        p2 += cm * ub[m].x;
+        p3 += cm * ub[m].y;
+        if (FX && wid + 4 * m < px) {
+          const double ym = yx.v[wid + 4 * m];
+          g0 = fma(ym, ua[m].x, g0);
+          g1 = fma(ym, ua[m].y, g1);
+          g2 = fma(ym, ub[m].x, g2);
+          g3 = fma(ym, ub[m].y, g3);
+        }
       }
     }
-  }
-  s_sum[wid][0][lane] = p0;
-  s_sum[wid][1][lane] = p1;
-  s_sum[wid][2][lane] = p2;
-  s_sum[wid][3][lane] = p3;
-  if (FX) {
-    s_x[wid][0][lane] = g0;
-    s_x[wid][1][lane] = g1;
-    s_x[wid][2][lane] = g2;
-    s_x[wid][3][lane] = g3;
-  }
-  __syncthreads();
-  double t[4];
+    s_sum[wid][0][lane] = p0;
+    s_sum[wid][1][lane] = p1;
+    s_sum[wid][2][lane] = p2;
+    s_sum[wid][3][lane] = p3;
+    if (FX) {
+      s_x[wid][0][lane] = g0;
+      s_x[wid][1][lane] = g1;
+      s_x[wid][2][lane] = g2;
+      s_x[wid][3][lane] = g3;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = (((s_sum[0][k][lane] + s_sum[1][k][lane]) + s_sum[2][k][lane]) + s_sum[3][k][lane]);
-  t[0] = wa.x - t[0];
-  t[1] = wa.y - t[1];
-  t[2] = wb.x - t[2];
-  t[3] = wb.y - t[3];
-  // the tail of a chunk past n holds zeros (ld2), so its t are 0 and add nothing below
-  if (wid == 0) {
-    st2(w, e, t[0], t[1]);
-    st2(w, e + 128, t[2], t[3]);
-  }
-  if (FX && wid == 1) {
-    double xs[4];
+    for (int k = 0; k < 4; ++k) t[k] = (((s_sum[0][k][lane] + s_sum[1][k][lane]) + s_sum[2][k][lane]) + s_sum[3][k][lane]);
+    t[0] = va.x - t[0];
+    t[1] = va.y - t[1];
+    t[2] = vb.x - t[2];
+    t[3] = vb.y - t[3];
+    // the tail of a chunk past n holds zeros (ld2), so its t are 0 and add nothing below
+    if (wid == 0) {
+      st2(w, ec, t[0], t[1]);
+      st2(w, ec + 128, t[2], t[3]);
+    }
+    if (FX && wid == 1) {
+      double xs[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
-    st2(xo, e, xs[0] + ba.x, xs[1] + ba.y);
-    st2(xo, e + 128, xs[2] + bb.x, xs[3] + bb.y);
-  }
-  double a0 = 0.0;
-  if (wid == 0) {
-    a0 += t[0] * t[0];
-    a0 += t[1] * t[1];
-    a0 += t[2] * t[2];
-    a0 += t[3] * t[3];
+      for (int k = 0; k < 4; ++k) xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
+      st2(xo, ec, xs[0] + xa.x, xs[1] + xa.y);
+      st2(xo, ec + 128, xs[2] + xb.x, xs[3] + xb.y);
+    }
+    if (wid == 0) {
+      a0 += t[0] * t[0];
+      a0 += t[1] * t[1];
+      a0 += t[2] * t[2];
+      a0 += t[3] * t[3];
+    }
+  };
+  double t[4], t2[4] = {0.0, 0.0, 0.0, 0.0};
+  update(e, qa, qb, wa, wb, ba, bb, t);
+  if (two) {
+    __syncthreads();  // s_sum / s_x read by every wave before they are written again
+#pragma unroll
+    for (int m = 0; m < kCgsPerWave; ++m) {
+      if (wid + 4 * m < nv) {
+        qa[m] = ld2(Qw + m * step, e2);
+        qb[m] = ld2(Qw + m * step, e2 + 128);
+      }
+    }
+    double2 xa2 = make_double2(0.0, 0.0), xb2 = xa2;
+    if (FX && wid == 1) {
+      xa2 = ld2(x0, e2);
+      xb2 = ld2(x0, e2 + 128);
+    }
+    update(e2, qa, qb, ld2(w, e2), ld2(w, e2 + 128), xa2, xb2, t2);
   }
   const double part = block_sum(a0, s_wave);
   if (threadIdx.x == 0) tag_put(slots + kOnePassN + 2 * blockIdx.x, tag, part);
@@ -2764,23 +2923,40 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
   if (wid == 0) {
     st2(qn, e, h == 0.0 ? 0.0 : t[0] / h, h == 0.0 ? 0.0 : t[1] / h);
     st2(qn, e + 128, h == 0.0 ? 0.0 : t[2] / h, h == 0.0 ? 0.0 : t[3] / h);
+    if (two) {
+      st2(qn, e2, h == 0.0 ? 0.0 : t2[0] / h, h == 0.0 ? 0.0 : t2[1] / h);
+      st2(qn, e2 + 128, h == 0.0 ? 0.0 : t2[2] / h, h == 0.0 ? 0.0 : t2[3] / h);
+    }
   }
 }
 
-int icwy_onepass_max_grid() {
-  static int cap = -1;
-  if (cap < 0) {
+// resident workgroups of the K2s variant (TWO: the two-chunk one), 0 if the query fails
+static int icwy_onepass_grid_cap(bool two) {
+  static int cap[2] = {-1, -1};
+  int& c = cap[two ? 1 : 0];
+  if (c < 0) {
     int dev = 0, cus = 0, per = 0, per_fx = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, icwy_onepass_kernel<false>, kBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fx, icwy_onepass_kernel<true>, kBlock, 0) != hipSuccess)
-      return 0;
+    hipError_t e0 = hipGetDevice(&dev);
+    if (e0 == hipSuccess) e0 = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e0 == hipSuccess)
+      e0 = two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, icwy_onepass_kernel<false, true>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, icwy_onepass_kernel<false, false>, kBlock, 0);
+    if (e0 == hipSuccess)
+      e0 = two ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fx, icwy_onepass_kernel<true, true>, kBlock, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_fx, icwy_onepass_kernel<true, false>, kBlock, 0);
+    if (e0 != hipSuccess) return 0;
     // every workgroup must be resident at once.  A kernel running beside it on another stream (the
     // side-stream GEMV) only delays the last workgroups' placement: it waits on nothing in here
-    cap = std::min<int>(kRedGrid, cus * std::min(per, per_fx));
+    c = std::min<int>(kRedGrid, cus * std::min(per, per_fx));
   }
-  return cap;
+  return c;
+}
+
+int icwy_onepass_max_grid() { return icwy_onepass_grid_cap(false); }
+
+int64_t icwy_onepass_max_n() {
+  return std::max<int64_t>(static_cast<int64_t>(kCgsChunk) * icwy_onepass_grid_cap(false),
+                           2 * static_cast<int64_t>(kCgsChunk) * icwy_onepass_grid_cap(true));
 }
 
 hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pitch, int nv, double* G, double* h_col,
@@ -2788,8 +2964,11 @@ hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pi
                                const LaunchEv* ev, int px, const double* yx, const double* x0, double* xo,
                                const double* rpart, int r_in, double* r_out, unsigned long long* flag,
                                const unsigned long long* seq) {
-  const int64_t grid = (n + kCgsChunk - 1) / kCgsChunk;
-  if (nv < 1 || nv > kCgsMax || n < 1 || grid > icwy_onepass_max_grid() || tag == 0 || slots == nullptr ||
+  const int64_t chunks = (n + kCgsChunk - 1) / kCgsChunk;
+  // one chunk per workgroup while they all fit, else two (the second streamed)
+  const bool two = chunks > icwy_onepass_grid_cap(false);
+  const int64_t grid = two ? (chunks + 1) / 2 : chunks;
+  if (nv < 1 || nv > kCgsMax || n < 1 || grid > icwy_onepass_grid_cap(two) || tag == 0 || slots == nullptr ||
       err == nullptr || G == nullptr || h_col == nullptr || !aligned16d(w) || !aligned16d(Q) || pitch % 2 != 0 ||
       (rpart != nullptr && (r_in < 1 || r_out == nullptr)))
     return hipErrorInvalidValue;
@@ -2801,12 +2980,17 @@ hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pi
   }
   const CoefArg ca{nullptr, G, h_col, rpart, r_in, r_out, flag, seq};
   double* qn = const_cast<double*>(Q) + static_cast<int64_t>(nv) * pitch;
-  if (px > 0)
-    launch_k(icwy_onepass_kernel<true>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, qn, pitch, nv, slots, tag, err,
-             ca, px, ya, x0, xo, h_col + nv);
-  else
-    launch_k(icwy_onepass_kernel<false>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, qn, pitch, nv, slots, tag, err,
-             ca, 0, ya, x0, xo, h_col + nv);
+#define SPIS_K2S(F, T)                                                                                          \
+  launch_k(icwy_onepass_kernel<F, T>, dim3(grid), dim3(kBlock), 0, s, ev, n, w, Q, qn, pitch, nv, slots, tag, \
+           err, ca, px, ya, x0, xo, h_col + nv)
+  if (px > 0) {
+    if (two) SPIS_K2S(true, true);
+    else SPIS_K2S(true, false);
+  } else {
+    if (two) SPIS_K2S(false, true);
+    else SPIS_K2S(false, false);
+  }
+#undef SPIS_K2S
   return hipGetLastError();
 }
 

@@ -54,15 +54,29 @@ void GivensQR::solve(int p, double* y) const {
   }
 }
 
+// Host-time note (round 5): the O(p^2) and O(p^3) sums below run with the loop over independent
+// sums innermost (u[b] here, J[a] and F[a] in residual, ...): every sum keeps its own operand
+// order, so results are bitwise those of the row-by-row loops, without one dependent add chain
+// per entry (C3's KKT solve, p = 30, m = 2: the GPU waits on it).
 double con_value(const QuadCon& c, int p, const double* y) {
   double lin = 0.0;
   for (int a = 0; a < p; ++a) lin += c.term1[a] * y[a];
-  double quad = 0.0;
-  for (int b = 0; b < p; ++b) {
-    double u = 0.0;
-    for (int a = 0; a < p; ++a) u += y[a] * c.term2[static_cast<size_t>(a) * p + b];
-    quad += u * y[b];
+  double ub[128];
+  std::vector<double> uv;
+  double* u = ub;
+  if (p > 128) {
+    uv.assign(p, 0.0);
+    u = uv.data();
   }
+  for (int b = 0; b < p; ++b) u[b] = 0.0;
+  const double* T = c.term2.data();
+  for (int a = 0; a < p; ++a) {  // u[b] = sum_a y[a] T[a][b], a ascending
+    const double ya = y[a];
+    const double* row = T + static_cast<size_t>(a) * p;
+    for (int b = 0; b < p; ++b) u[b] += ya * row[b];
+  }
+  double quad = 0.0;
+  for (int b = 0; b < p; ++b) quad += u[b] * y[b];
   return (c.term0 + lin) + quad;
 }
 
@@ -124,22 +138,31 @@ struct KKTState {
     return orig ? con_value(orig[i], p, y) * inv_s[i] : con_value(cons[i], p, y);
   }
 
+  // out[a] = init[a] + sum_b Sym[a][b] v[b], b ascending, for an exactly symmetric Sym (B, S_i:
+  // entrywise sums of commuting products): summed down column a, the loop over a innermost
+  void symv(const double* Sym, const double* init, const double* v, double* out) const {
+    for (int a = 0; a < p; ++a) out[a] = init[a];
+    for (int b = 0; b < p; ++b) {
+      const double vb = v[b];
+      const double* col = Sym + static_cast<size_t>(b) * p;
+      for (int a = 0; a < p; ++a) out[a] += col[a] * vb;
+    }
+  }
+
   void residual(const QuadCon* cons, const double* y, const double* lam, double* F,
                 std::vector<double>& J) const {
     // J (m x p row-major); F = [grad f + J' lam ; c + tau]
-    for (int i = 0; i < m; ++i) {
-      const std::vector<double>& Si = S[i];
-      for (int a = 0; a < p; ++a) {
-        double t = cons[i].term1[a];
-        for (int b = 0; b < p; ++b) t += Si[static_cast<size_t>(a) * p + b] * y[b];
-        J[static_cast<size_t>(i) * p + a] = t;
-      }
+    for (int i = 0; i < m; ++i) symv(S[i].data(), cons[i].term1.data(), y, J.data() + static_cast<size_t>(i) * p);
+    for (int a = 0; a < p; ++a) F[a] = -b0[a];
+    for (int b = 0; b < p; ++b) {
+      const double yb = y[b];
+      const double* col = B.data() + static_cast<size_t>(b) * p;
+      for (int a = 0; a < p; ++a) F[a] += col[a] * yb;
     }
-    for (int a = 0; a < p; ++a) {
-      double t = -b0[a];
-      for (int b = 0; b < p; ++b) t += B[static_cast<size_t>(a) * p + b] * y[b];
-      for (int i = 0; i < m; ++i) t += J[static_cast<size_t>(i) * p + a] * lam[i];
-      F[a] = t;
+    for (int i = 0; i < m; ++i) {
+      const double li = lam[i];
+      const double* Ji = J.data() + static_cast<size_t>(i) * p;
+      for (int a = 0; a < p; ++a) F[a] += Ji[a] * li;
     }
     for (int i = 0; i < m; ++i) F[p + i] = cval(cons, i, y) + tau[i];
   }
@@ -170,11 +193,17 @@ void grad_scale(const KKTState& st, const double* y, const double* lam, const do
   const int p = st.p, m = st.m;
   *gn = 0.0;
   *gs = 0.0;
+  std::vector<double> t(p);
+  for (int a = 0; a < p; ++a) t[a] = std::fabs(st.b0[a]);
+  for (int b = 0; b < p; ++b) {  // B exactly symmetric: row a summed down column a
+    const double yb = y[b];
+    const double* col = st.B.data() + static_cast<size_t>(b) * p;
+    for (int a = 0; a < p; ++a) t[a] += std::fabs(col[a] * yb);
+  }
+  for (int i = 0; i < m; ++i)
+    for (int a = 0; a < p; ++a) t[a] += std::fabs(J[static_cast<size_t>(i) * p + a] * lam[i]);
   for (int a = 0; a < p; ++a) {
-    double t = std::fabs(st.b0[a]);
-    for (int b = 0; b < p; ++b) t += std::fabs(st.B[static_cast<size_t>(a) * p + b] * y[b]);
-    for (int i = 0; i < m; ++i) t += std::fabs(J[static_cast<size_t>(i) * p + a] * lam[i]);
-    *gs = std::max(*gs, t);
+    *gs = std::max(*gs, t[a]);
     *gn = std::max(*gn, std::fabs(F[a]));
   }
 }
@@ -188,7 +217,7 @@ void grad_scale(const KKTState& st, const double* y, const double* lam, const do
 bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, double delta, double shift_rel) {
   if (m >= p) return true;
   for (int a = 0; a < p; ++a) W[static_cast<size_t>(a) * p + a] += delta;
-  std::vector<double> v(p), u(p);
+  std::vector<double> v(p), u(p), tw(p);
   for (int i = 0; i < m; ++i) {
     double* col = Jt.data() + static_cast<size_t>(i) * p;
     double nrm = 0.0;
@@ -211,11 +240,15 @@ bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, dou
       for (int a = i; a < p; ++a) x[a] -= t * v[a];
     }
     // W <- H W H with H = I - s2 v v' (W symmetric up to rounding: both sides explicitly)
-    for (int a = 0; a < p; ++a) {  // W <- W H: row a -= s2 (W_a . v) v'
+    // W <- W H: row a -= s2 (W_a . v) v' (the row sums formed side by side, b ascending)
+    std::fill(tw.begin(), tw.end(), 0.0);
+    for (int b = i; b < p; ++b) {
+      const double vb = v[b];
+      for (int a = 0; a < p; ++a) tw[a] += W[static_cast<size_t>(a) * p + b] * vb;
+    }
+    for (int a = 0; a < p; ++a) {
       double* row = W.data() + static_cast<size_t>(a) * p;
-      double t = 0.0;
-      for (int b = i; b < p; ++b) t += row[b] * v[b];
-      t *= s2;
+      const double t = tw[a] * s2;
       for (int b = i; b < p; ++b) row[b] -= t * v[b];
     }
     std::fill(u.begin(), u.end(), 0.0);  // W <- H W: W -= s2 v (v' W)
@@ -240,17 +273,21 @@ bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, dou
       if (c == d) dmax = std::max(dmax, std::fabs(t));
     }
   const double shift = shift_rel * dmax;
+  std::vector<double> tr(nz);
   for (int c = 0; c < nz; ++c) {  // in-place Cholesky
-    double d = Rm[static_cast<size_t>(c) * nz + c] + shift;
-    for (int k = 0; k < c; ++k) d -= Rm[static_cast<size_t>(c) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
+    const double* rc = Rm.data() + static_cast<size_t>(c) * nz;
+    double d = rc[c] + shift;
+    for (int k = 0; k < c; ++k) d -= rc[k] * rc[k];
     if (!(d > 0.0)) return false;
     d = std::sqrt(d);
     Rm[static_cast<size_t>(c) * nz + c] = d;
-    for (int r = c + 1; r < nz; ++r) {
-      double t = Rm[static_cast<size_t>(r) * nz + c];
-      for (int k = 0; k < c; ++k) t -= Rm[static_cast<size_t>(r) * nz + k] * Rm[static_cast<size_t>(c) * nz + k];
-      Rm[static_cast<size_t>(r) * nz + c] = t / d;
+    // column c below the diagonal: one sum per row r, k ascending, formed side by side
+    for (int r = c + 1; r < nz; ++r) tr[r] = Rm[static_cast<size_t>(r) * nz + c];
+    for (int k = 0; k < c; ++k) {
+      const double ck = rc[k];
+      for (int r = c + 1; r < nz; ++r) tr[r] -= Rm[static_cast<size_t>(r) * nz + k] * ck;
     }
+    for (int r = c + 1; r < nz; ++r) Rm[static_cast<size_t>(r) * nz + c] = tr[r] / d;
   }
   return true;
 }
@@ -294,13 +331,16 @@ Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& l
   if (!(bscale > 0.0)) bscale = 1.0;
   // f - rho^2 = ||g - R v||^2 from the residual itself (1/2 v'Bv - b0'v cancels to roundoff of
   // |b0| |v| near a solution whose f is ~1e-21, so merit comparisons would be noise)
-  auto fval = [&](const double* v) {
-    double t = 0.0;
-    for (int a = 0; a < p; ++a) {
-      double r = st.g[a];
-      for (int b = a; b < p; ++b) r -= st.R[static_cast<size_t>(b) * st.ld + a] * v[b];
-      t += r * r;
+  std::vector<double> fr(p);
+  auto fval = [&](const double* v) {  // r[a] = g[a] - sum_{b >= a} R[a][b] v[b], b ascending
+    for (int a = 0; a < p; ++a) fr[a] = st.g[a];
+    for (int b = 0; b < p; ++b) {
+      const double vb = v[b];
+      const double* col = st.R + static_cast<size_t>(b) * st.ld;
+      for (int a = 0; a <= b; ++a) fr[a] -= col[a] * vb;
     }
+    double t = 0.0;
+    for (int a = 0; a < p; ++a) t += fr[a] * fr[a];
     return t;
   };
   auto viol = [&](const double* v) {
@@ -326,11 +366,8 @@ Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& l
       for (int i = 0; i < m; ++i) cons_ok = cons_ok && std::fabs(F[p + i]) <= st.tau[i];
       if (cons_ok && gn <= 64.0 * DBL_EPSILON * gs) { run.stop = Stop::kFloor; break; }
     }
-    for (int a = 0; a < p; ++a) {
-      double t = -st.b0[a];
-      for (int b = 0; b < p; ++b) t += st.B[static_cast<size_t>(a) * p + b] * y[b];
-      gf[a] = t;
-    }
+    for (int a = 0; a < p; ++a) gf[a] = -st.b0[a];
+    st.symv(st.B.data(), gf.data(), y, gf.data());
     lagrangian_hessian(st, lam.data(), J, W, Jt);
     double delta = 0.0;
     bool pd = reduced_pd(W, Jt, p, m, 0.0, 0.0);
@@ -491,15 +528,23 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   st.R = R;
   st.g = g;
   st.ld = ld;
+  // B[a][b] = 2 sum_{k <= min(a, b)} R[k][a] R[k][b], k ascending: rank-one updates by row k of
+  // R (the same sums, formed side by side; R column-major: R[k][a] = R[a * ld + k])
   st.B.assign(static_cast<size_t>(p) * p, 0.0);
   st.b0.assign(p, 0.0);
-  for (int a = 0; a < p; ++a) {
-    for (int b = 0; b < p; ++b) {
-      double t = 0.0;
-      const int top = std::min(a, b);
-      for (int k = 0; k <= top; ++k) t += R[static_cast<size_t>(a) * ld + k] * R[static_cast<size_t>(b) * ld + k];
-      st.B[static_cast<size_t>(a) * p + b] = 2.0 * t;
+  {
+    std::vector<double> rk(p);
+    for (int k = 0; k < p; ++k) {
+      for (int b = k; b < p; ++b) rk[b] = R[static_cast<size_t>(b) * ld + k];
+      for (int a = k; a < p; ++a) {
+        const double ra = rk[a];
+        double* row = st.B.data() + static_cast<size_t>(a) * p;
+        for (int b = k; b < p; ++b) row[b] += ra * rk[b];
+      }
     }
+    for (double& t : st.B) t *= 2.0;
+  }
+  for (int a = 0; a < p; ++a) {
     double t = 0.0;
     for (int k = 0; k <= a; ++k) t += R[static_cast<size_t>(a) * ld + k] * g[k];
     st.b0[a] = 2.0 * t;
@@ -542,12 +587,7 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   //    iteration limit (C4: 13.6 ms host time, then the same fallback as the reference's).
   if (m > 0) {
     std::vector<double> Jc(static_cast<size_t>(m) * p);
-    for (int i = 0; i < m; ++i)
-      for (int a = 0; a < p; ++a) {
-        double t = cons[i].term1[a];
-        for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y[b];
-        Jc[static_cast<size_t>(i) * p + a] = t;
-      }
+    for (int i = 0; i < m; ++i) st.symv(st.S[i].data(), cons[i].term1.data(), y, Jc.data() + static_cast<size_t>(i) * p);
     for (int i = 0; i < m; ++i) {  // Householder QR of the rows (J' columns), pivot by pivot
       double* ri = Jc.data() + static_cast<size_t>(i) * p;
       double nrm = 0.0;
@@ -582,13 +622,11 @@ KKTResult kkt_newton(int p, const double* R, int ld, const double* g, int m, con
   std::vector<QuadCon> sc(cons, cons + m);
   st.orig = cons;
   st.inv_s.assign(m, 1.0);
+  std::vector<double> gi(p);
   for (int i = 0; i < m; ++i) {
+    st.symv(st.S[i].data(), cons[i].term1.data(), y0, gi.data());
     double nrm = 0.0;
-    for (int a = 0; a < p; ++a) {
-      double t = cons[i].term1[a];
-      for (int b = 0; b < p; ++b) t += st.S[i][static_cast<size_t>(a) * p + b] * y0[b];
-      nrm += t * t;
-    }
+    for (int a = 0; a < p; ++a) nrm += gi[a] * gi[a];
     nrm = std::sqrt(nrm);
     if (!(nrm > 0.0) || !std::isfinite(nrm)) continue;
     const double f = 1.0 / nrm;

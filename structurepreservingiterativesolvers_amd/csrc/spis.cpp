@@ -119,7 +119,8 @@ struct spis_context {
   double* cg_vpart = nullptr;          // K7t: the transpose's linear-term partials
   double* inc_u = nullptr;             // incremental Gram: M z_a (n)
   int64_t inc_u_len = 0;
-  double* inc_part = nullptr;          // its multidot partials (kMdMax x kRedGrid)
+  double* inc_part = nullptr;          // its partials (values x grid: K6i, multidot)
+  size_t inc_part_len = 0;
   double* inc_res = nullptr;           // its reduced values (device), copied to con_pinned
   size_t inc_res_len = 0;
   ncclComm_t comm = nullptr;
@@ -1768,11 +1769,27 @@ static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, cons
 // unless its p is small enough that columns 0 .. p-1 from scratch cost less (kIncScratch).
 constexpr int kIncScratch = 8;
 
+// one value an increment step computes: G(a, b) = z_a . M z_b of constraint ci (m), else its
+// v . z_a (gv[a]); a, b = k stand for x0
+struct IncSlot {
+  int ci, a, b;
+  bool m;
+};
+// one pass over a constraint matrix: u = M z_a (a = k: M x0), dotted with [z_0 .. z_a, x0] (x0)
+struct IncPass {
+  int ci, a, slot0, nl;
+};
+
 struct ConStep {
   bool inc = false;  // increments enqueued (else the full reduction)
   int p = 0, m = 0;
   std::vector<int> from;  // per constraint: first new column (inc)
   hipStream_t st = nullptr;  // the stream the results are copied on (record the wait's event there)
+  // inc: the values in partial / result order: the first pass's, the pair dots v . z_a, v . x0
+  // (carried by that pass, K6i, when they fit), the other passes'
+  std::vector<IncSlot> slots;
+  std::vector<IncPass> passes;
+  int pair0 = 0, npair = 0;
 };
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
@@ -1789,104 +1806,127 @@ static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const s
   return true;
 }
 
-// values one increment step writes (the order con_inc_take reads them)
-static size_t con_inc_len(int m, const spis_constraint_desc* cons, int p, const std::vector<int>& from,
-                          const spis_workspace* ws) {
-  size_t t = 0;
+// the values and passes of one increment step (ConStep::slots / passes, in partial order)
+static void con_inc_plan(int m, const spis_constraint_desc* cons, int p, const spis_workspace* ws, ConStep& cs) {
+  const int k = ws->k;
+  cs.slots.clear();
+  cs.passes.clear();
+  std::vector<IncSlot> pairs;  // grouped by constraint (one multidot per constraint when not carried)
   for (int ci = 0; ci < m; ++ci) {
     const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
-    for (int a = from[ci]; a < p; ++a) t += (hasM ? a + 2 : 0) + (cons[ci].v_dev ? 1 : 0);
-    if (ws->con[ci].gcols < 0) t += (hasM ? 1 : 0) + (cons[ci].v_dev ? 1 : 0);
+    const bool hasV = cons[ci].v_dev != nullptr;
+    for (int a = cs.from[ci]; a < p; ++a) {
+      if (hasM) cs.passes.push_back({ci, a, 0, a + 2});
+      if (hasV) pairs.push_back({ci, a, 0, false});
+    }
+    if (ws->con[ci].gcols < 0) {  // x0's own terms: x0 . M x0, v . x0
+      if (hasM) cs.passes.push_back({ci, k, 0, 1});
+      if (hasV) pairs.push_back({ci, k, 0, false});
+    }
   }
-  return t;
+  auto add_pass = [&](IncPass& ps) {
+    ps.slot0 = static_cast<int>(cs.slots.size());
+    if (ps.a == k) {
+      cs.slots.push_back({ps.ci, k, k, true});
+      return;
+    }
+    for (int b = 0; b <= ps.a; ++b) cs.slots.push_back({ps.ci, ps.a, b, true});
+    cs.slots.push_back({ps.ci, ps.a, k, true});
+  };
+  if (!cs.passes.empty()) add_pass(cs.passes[0]);
+  cs.pair0 = static_cast<int>(cs.slots.size());
+  cs.npair = static_cast<int>(pairs.size());
+  cs.slots.insert(cs.slots.end(), pairs.begin(), pairs.end());
+  for (size_t i = 1; i < cs.passes.size(); ++i) add_pass(cs.passes[i]);
 }
 
-static int con_inc_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
-                           int p, const double* Z, int64_t pitch, const double* x0, const ConStep& cs) {
+static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons, int64_t n,
+                           const double* Z, int64_t pitch, const double* x0, const ConStep& cs) {
   hipStream_t st = cs.st;
-  const size_t total = con_inc_len(m, cons, p, cs.from, ws);
-  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, std::max<size_t>(total, 1)));
-  if (c->inc_u_len < n) {
-    if (c->inc_u) HIP_TRY(hipFree(c->inc_u));
-    HIP_TRY(hipMalloc(&c->inc_u, sizeof(double) * std::max<int64_t>(n, 1)));
-    c->inc_u_len = n;
+  const int k = ws->k;
+  const size_t total = cs.slots.size();
+  if (total == 0) return SPIS_OK;
+  ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, total));
+  const int g = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 255) / 256)));
+  if (c->inc_part_len < total * g) {
+    if (c->inc_part) HIP_TRY(hipFree(c->inc_part));
+    HIP_TRY(hipMalloc(&c->inc_part, sizeof(double) * total * g));
+    c->inc_part_len = total * g;
   }
-  if (!c->inc_part) HIP_TRY(hipMalloc(&c->inc_part, sizeof(double) * kMdMax * kRedGrid));
   if (c->inc_res_len < total) {
     if (c->inc_res) HIP_TRY(hipFree(c->inc_res));
     HIP_TRY(hipMalloc(&c->inc_res, sizeof(double) * total));
     c->inc_res_len = total;
   }
-  const int g = fixed_grid(c) ? kRedGrid : static_cast<int>(std::min<int64_t>(kRedGrid, std::max<int64_t>(1, (n + 255) / 256)));
-  size_t off = 0;
-  auto dots = [&](const double* u, const VecList& L, int nvec) -> int {
-    HIP_TRY(launch_multidot(n, u, L, nvec, c->inc_part, g, st));
-    HIP_TRY(launch_cgs_finalize(c->inc_part, g, nvec, c->inc_res + off, nullptr, nullptr, st));
-    off += static_cast<size_t>(nvec);
-    return SPIS_OK;
-  };
-  auto zv = [&](int a) { return Z + static_cast<int64_t>(a) * pitch; };
-  for (int ci = 0; ci < m; ++ci) {
-    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
-    for (int a = cs.from[ci]; a < p; ++a) {
-      if (hasM) {  // [z_0 .. z_a, x0] . M z_a
-        ST_TRY(spmv_local(c, ws, cons[ci].M, zv(a), c->inc_u, st));
-        VecList L{};
-        for (int b = 0; b <= a; ++b) L.v[b] = zv(b);
-        L.v[a + 1] = x0;
-        ST_TRY(dots(c->inc_u, L, a + 2));
-      }
-      if (cons[ci].v_dev) {  // v . z_a
-        VecList L{};
-        L.v[0] = cons[ci].v_dev;
-        ST_TRY(dots(zv(a), L, 1));
-      }
+  auto zv = [&](int a) { return a == k ? x0 : Z + static_cast<int64_t>(a) * pitch; };
+  auto part_at = [&](int slot) { return c->inc_part + static_cast<size_t>(slot) * g; };
+  bool carried = false;
+  for (size_t i = 0; i < cs.passes.size(); ++i) {
+    const IncPass& ps = cs.passes[i];
+    spis_matrix* M = cons[ps.ci].M;
+    VecList L{};
+    if (ps.a == k) {
+      L.v[0] = x0;
+    } else {
+      for (int b = 0; b <= ps.a; ++b) L.v[b] = zv(b);
+      L.v[ps.a + 1] = x0;
     }
-    if (ws->con[ci].gcols < 0) {  // x0's own terms: x0 . M x0, v . x0
-      if (hasM) {
-        ST_TRY(spmv_local(c, ws, cons[ci].M, x0, c->inc_u, st));
-        VecList L{};
-        L.v[0] = x0;
-        ST_TRY(dots(c->inc_u, L, 1));
+    const CsrView mv = M->view();
+    if (mv.blk_row != nullptr && (!c->dist_on() || M->n_ghost == 0)) {  // K6i: one pass
+      VecList P{}, Q{};
+      int np = 0;
+      if (i == 0 && cs.npair <= kGramPairMax) {
+        for (int q = 0; q < cs.npair; ++q) {
+          const IncSlot& sl = cs.slots[cs.pair0 + q];
+          P.v[q] = cons[sl.ci].v_dev;
+          Q.v[q] = zv(sl.a);
+        }
+        np = cs.npair;
+        carried = true;
       }
-      if (cons[ci].v_dev) {
-        VecList L{};
-        L.v[0] = cons[ci].v_dev;
-        ST_TRY(dots(x0, L, 1));
+      HIP_TRY(launch_spmv_gram(mv, zv(ps.a), L, ps.nl, P, Q, np, part_at(ps.slot0), g, st));
+    } else {  // several GPUs with ghost columns: the exchange-aware SpMV, then the multidot
+      if (c->inc_u_len < n) {
+        if (c->inc_u) HIP_TRY(hipFree(c->inc_u));
+        HIP_TRY(hipMalloc(&c->inc_u, sizeof(double) * std::max<int64_t>(n, 1)));
+        c->inc_u_len = n;
       }
+      ST_TRY(spmv_local(c, ws, M, zv(ps.a), c->inc_u, st));
+      HIP_TRY(launch_multidot(n, c->inc_u, L, ps.nl, part_at(ps.slot0), g, st));
     }
   }
-  if (off != total) return fail(SPIS_ERR_STATE, "incremental Gram: %zu values, expected %zu", off, total);
-  if (total > 0) {
-    ST_TRY(allreduce_on(c, c->inc_res, static_cast<int64_t>(total), st));  // several GPUs: rows summed
-    HIP_TRY(hipMemcpyAsync(c->con_pinned, c->inc_res, sizeof(double) * total, hipMemcpyDeviceToHost, st));
-  }
+  if (!carried)  // the pair dots: one multidot per constraint, v . [its columns]
+    for (int q = 0; q < cs.npair;) {
+      const int ci = cs.slots[cs.pair0 + q].ci;
+      VecList L{};
+      int cnt = 0;
+      while (q + cnt < cs.npair && cs.slots[cs.pair0 + q + cnt].ci == ci && cnt < kMdMax) {
+        L.v[cnt] = zv(cs.slots[cs.pair0 + q + cnt].a);
+        ++cnt;
+      }
+      HIP_TRY(launch_multidot(n, cons[ci].v_dev, L, cnt, part_at(cs.pair0 + q), g, st));
+      q += cnt;
+    }
+  HIP_TRY(launch_cgs_finalize(c->inc_part, g, static_cast<int>(total), c->inc_res, nullptr, nullptr, st));
+  ST_TRY(allreduce_on(c, c->inc_res, static_cast<int64_t>(total), st));  // several GPUs: rows summed
+  HIP_TRY(hipMemcpyAsync(c->con_pinned, c->inc_res, sizeof(double) * total, hipMemcpyDeviceToHost, st));
   return SPIS_OK;
 }
 
-// the increments into the caches (after the wait), in con_inc_enqueue's order
-static void con_inc_take(spis_workspace* ws, int m, const spis_constraint_desc* cons, const ConStep& cs,
-                         const double* src) {
+// the increments into the caches (after the wait)
+static void con_inc_take(spis_workspace* ws, int m, const ConStep& cs, const double* src) {
   const int k = ws->k;
-  auto G = [&](ConCache& cc, int a, int b) -> double& { return cc.gc[static_cast<size_t>(a) * (k + 1) + b]; };
-  size_t off = 0;
-  for (int ci = 0; ci < m; ++ci) {
-    ConCache& cc = ws->con[ci];
-    const bool hasM = cons[ci].M != nullptr && !cons[ci].M->all_zero;
-    for (int a = cs.from[ci]; a < cs.p; ++a) {
-      if (hasM) {
-        for (int b = 0; b <= a; ++b) G(cc, a, b) = G(cc, b, a) = src[off + b];
-        G(cc, a, k) = G(cc, k, a) = src[off + a + 1];
-        off += static_cast<size_t>(a) + 2;
-      }
-      if (cons[ci].v_dev) cc.gv[a] = src[off++];
+  for (size_t s = 0; s < cs.slots.size(); ++s) {
+    const IncSlot& sl = cs.slots[s];
+    ConCache& cc = ws->con[sl.ci];
+    if (sl.m) {
+      cc.gc[static_cast<size_t>(sl.a) * (k + 1) + sl.b] = src[s];
+      cc.gc[static_cast<size_t>(sl.b) * (k + 1) + sl.a] = src[s];
+    } else {
+      cc.gv[sl.a] = src[s];
     }
-    if (cc.gcols < 0) {
-      if (hasM) G(cc, k, k) = src[off++];
-      if (cons[ci].v_dev) cc.gv[k] = src[off++];
-    }
-    cc.gcols = cs.p;
   }
+  for (int ci = 0; ci < m; ++ci) ws->con[ci].gcols = cs.p;
 }
 
 // the full reduction's results (con_gram_enqueue's layout) into the caches
@@ -1953,7 +1993,8 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     // side: the increments on stream2, beside the latency-bound MGS chain the host has just queued
     // (they read only z_0 .. z_{p-1}, finished by earlier chains, x0 and the constraint operators)
     if (side && !c->dist_on()) cs->st = c->stream2;
-    return con_inc_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, *cs);
+    con_inc_plan(m, cons, p, ws, *cs);
+    return con_inc_enqueue(c, ws, cons, n, Z, pitch, x0, *cs);
   }
   ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
   return con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned);
@@ -1963,7 +2004,7 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
 static void con_step_assemble(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons,
                               const ConStep& cs, QuadCon* out) {
   if (cs.inc) {
-    con_inc_take(ws, cs.m, cons, cs, c->con_pinned);
+    con_inc_take(ws, cs.m, cs, c->con_pinned);
     con_terms_from_cache(ws, cs.m, cons, cs.p, out);
     return;
   }
@@ -2242,10 +2283,11 @@ struct Solver {
   // register-resident basis slices) wins wherever it fits (lkdv, N = 100,002: MGS 29.1 -> 18.0 us,
   // 22,272 -> 26,485-28,246 it/s; 200,004: +3-7%; 250,002: +6.6%; gpurun_out/r04k2s), while
   // K2w's two launches lose to K2q from N = 250,000 on (gpurun_out/r04k2ws2): so K2w is taken at
-  // small N only where K2s fits (n <= 256 icwy_onepass_max_grid(), <= 262,144).  Every step must
+  // small N only where K2s fits (icwy_onepass_max_n(): one resident chunk of 256 per workgroup up
+  // to 262,144, two chunks, the second streamed, up to 524,288; C4's 300,006).  Every step must
   // take it (k <= kCgsMax): a later K2q step would read Gram entries (chain_gsub) it never wrote
   bool k2w_small() const {
-    const int64_t cap = k2w_small_n >= 0 ? k2w_small_n : 256 * static_cast<int64_t>(icwy_onepass_max_grid());
+    const int64_t cap = k2w_small_n >= 0 ? k2w_small_n : icwy_onepass_max_n();
     return c->mgs_chain == 3 && !c->cgs2 && k <= kCgsMax && n <= cap;
   }
   static constexpr uint64_t kHSentinel = 0x7FF4DEAD5EC0FFEEull;  // a signalling NaN no kernel writes
@@ -2392,7 +2434,7 @@ struct Solver {
     const int px = (yx && ws->Zb == ws->Q) ? jx + 1 : 0;
     if (yx && px == 0) return fail(SPIS_ERR_STATE, "fused update GEMV needs Z = Q");
     // K2s: one GPU, small N: the whole step in one launch, the basis slices held in registers
-    if (!c->dist_on() && k2w_onepass && !c->icwy_spin_off && (n + 255) / 256 <= icwy_onepass_max_grid() && n_gx() == n) {
+    if (!c->dist_on() && k2w_onepass && !c->icwy_spin_off && n <= icwy_onepass_max_n() && n_gx() == n) {
       if (++c->icwy_tag == 0) c->icwy_tag = 1;
       const LaunchEv both{e_first.start, e_last.stop};
       HIP_TRY(launch_icwy_onepass(n, ws->w, Qv(0), ws->pitch, nv, c->icwy_G, hcol, c->icwy_slots, c->icwy_tag,
@@ -2939,6 +2981,14 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
       ws->n_iter_y = j + 1;
       if (L) {
+        // step j+1 constrained whatever res_j says (CGMRES_P; CGMRES once safety is set, :230):
+        // its reduction reads z_0 .. z_{j+1}, complete when c_{j+1} (queued above) ends, so it
+        // goes on the main stream right behind that chain, ahead of U_j's GEMV and a_{j+2}: it
+        // runs while the host solves LS_j and is done when the host reaches LS_{j+1} (beside the
+        // chain on stream2 it was starved by the persistent SpMV and chain kernels)
+        if (j + 2 < k && gram_queued != j + 1 && (o->method == SPIS_CGMRES_P || safety != kSafetyNone) &&
+            gram_early_ok(j + 1))
+          ST_TRY(queue_gram(j + 1));
         // x_j: from c_{j+1} (fused), else a GEMV beside c_{j+1} on the side stream, or after it
         // on the main stream when c_{j+1} computed x_j from the speculative unconstrained y_j
         if (!fused || constrained) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));

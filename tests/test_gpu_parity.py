@@ -1432,7 +1432,7 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
         assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
 
 
-@pytest.mark.parametrize("n", [65_536, 100_002, 196_608, 1001])
+@pytest.mark.parametrize("n", [65_536, 100_002, 196_608, 1001, 300_006, 393_216])
 def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     """K2s (small N, one GPU: K2w's dots, coefficients, update with the fused GEMV, norm and
     normalise in one launch over register-resident basis slices) against K2w's launches
@@ -1442,7 +1442,9 @@ def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     ulp apart: hipcc had contracted different multiply-adds into FMAs in the one-pass and the
     two-pass kernels; all three now compile with contraction off.)  GMRES in L mode, so the fused GEMV
     and the residual hand-off ride in the launch (the golden suite covers the constrained
-    solves); repeated solves reuse the tag slots."""
+    solves); repeated solves reuse the tag slots.  Above 1,024 chunks (262,144) each workgroup takes
+    two chunks, the second streamed (300,006 and 393,216 here): its dot and norm partials carry both
+    chunks, so the grouping differs from the two-pass kernels' at every n: roundoff."""
     from structurepreservingiterativesolvers_amd import solvers
 
     rng = np.random.default_rng(n)
@@ -1459,7 +1461,7 @@ def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     assert ra[-1] < 1e-3 * ra[0]
     assert all(np.array_equal(p, q) for p, q in zip(runs[1], runs[2]))  # run to run
     xb, rb, Qb = runs[1]
-    if n % 256 == 0:  # the same grouping of every partial and sum: bitwise
+    if n % 256 == 0 and n <= 262_144:  # the same grouping of every partial and sum: bitwise
         assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
     else:
         assert np.linalg.norm(xa - xb) <= 1e-12 * np.linalg.norm(xa)
