@@ -60,15 +60,16 @@ def mgs_chain_bytes(n, k, chain):
       one-reduce two-pass MGS (chain 4, and chain 3 beyond K2q): 8 N (j + 2) for the dots (w,
           q_0 .. q_j) + 8 N (j + 3) for the update (q_0 .. q_j and w read, w written) + 16 N for
           the update GEMV it carries from j >= 1 + 16 N for the normalise;
-      its one-launch form K2s (chain 3 or 4, N <= 262,144, k <= 32: spis.cpp k2w_small): 8 N
-          (j + 2) (w, q_0 .. q_j read once) + 16 N (w' and q_{j+1} written) + 16 N for the GEMV;
+      its one-launch form K2s (chain 3 or 4, N <= 524,288, k <= 32: spis.cpp k2w_small): 8 N
+          (j + 2) (w, q_0 .. q_j read once) + 16 N (w' and q_{j+1} written) + 16 N for the GEMV,
+          + 8 N_s (j + 2) for the streamed second chunks (N_s ~ N / 2 beyond 262,144) read again;
       per-step launches (chain 0): 32 N (j + 1) + 16 N (y, q_i, q_{i+1} read, y written; the
           normalise reads y, writes q)."""
     tot = 0.0
     k2q = (n + 1) // 2 <= 255 * 512 * 4
     for j in range(k):
         if k2s_used(n, k, chain):
-            b = 8 * n * (j + 2) + 16 * n + (16 * n if j >= 1 else 0)
+            b = 8 * n * (j + 2) + 16 * n + (16 * n if j >= 1 else 0) + 8 * k2s_reread(n) * (j + 2)
         elif chain == 4 or (chain == 3 and not k2q):
             b = 8 * n * (j + 2) + 8 * n * (j + 3) + (16 * n if j >= 1 else 0) + 16 * n
         elif chain == 3:
@@ -85,8 +86,16 @@ def mgs_chain_bytes(n, k, chain):
 
 def k2s_used(n, k, chain):
     """One GPU: does the library take K2s, the one-launch one-reduce MGS (spis.cpp k2w_small and
-    arnoldi_post_icwy: chain 3 or 4, k <= 32, N within its 1024 resident 256-row workgroups)?"""
-    return chain in (3, 4) and k <= 32 and n <= 256 * 1024
+    arnoldi_post_icwy: chain 3 or 4, k <= 32, N within its 1024 resident 256-row workgroups, one
+    register chunk each, and as many streamed second chunks: kernels.hip icwy_onepass_max_n)?"""
+    return chain in (3, 4) and k <= 32 and n <= 2 * 256 * 1024
+
+
+def k2s_reread(n):
+    """Elements K2s reads twice (its streamed second chunks, dots then update): beyond 1024 chunks of
+    256 rows each workgroup takes two chunks (kernels.hip launch_icwy_onepass), the second streamed."""
+    chunks = (n + 255) // 256
+    return 0 if chunks <= 1024 else max(0, n - 256 * ((chunks + 1) // 2))
 
 
 def orthog_label(n, k, chain, orthog):

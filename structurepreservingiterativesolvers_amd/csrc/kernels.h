@@ -184,13 +184,9 @@ constexpr int kMdMax = 40;
 struct VecList {
   const double* v[kMdMax];
 };
+// (the last n2 of the nvec vectors are dotted with u2 instead)
 hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
-                           hipStream_t s);
-// K6i: u = M x (not stored) and, in the same pass, the partials of L.v[i] . u (i < nl) followed by
-// those of P.v[i] . Q.v[i] (i < np <= kGramPairMax); M needs K1's row-block table (blk_row)
-constexpr int kGramPairMax = 8;
-hipError_t launch_spmv_gram(const CsrView& M, const double* x, const VecList& L, int nl, const VecList& P,
-                            const VecList& Q, int np, double* part, int grid, hipStream_t s);
+                           hipStream_t s, const double* u2 = nullptr, int n2 = 0);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,

@@ -2198,17 +2198,21 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
 
 // ---------------------------------------------------------------------------------------------
 // Multi-dot for the incremental constraint Gram (spis.cpp con_inc_enqueue): part[i * grid + blk]
-// = the workgroup's partial of L.v[i] . u, i < nvec (<= kMdMax).  Vector i goes to wave i % 4 (as
-// cgs_dot): each wave reads u's chunk once for its vectors; 256-element chunks per workgroup
-// iteration (16-B loads when every pointer is 16-B aligned), a scalar tail otherwise; the products
-// are rounded, then added (contraction off); fixed-order wave sums.  Bytes: (nvec + 4) 8 N.
+// = the workgroup's partial of L.v[i] . u, i < nvec (<= kMdMax), where the last n2 vectors take u2
+// instead of u (a constraint's v . z_a riding with its M z_a pass).  Vector i goes to wave i % 4
+// (as cgs_dot): each wave reads u's (and u2's) chunk once for its vectors; 256-element chunks per
+// workgroup iteration (16-B loads when every pointer is 16-B aligned), a scalar tail otherwise;
+// the products are rounded, then added (contraction off); fixed-order wave sums.
+// Bytes: (nvec + 4 (+ 4)) 8 N.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const double* __restrict__ u, VecList L,
-                                                          int nvec, bool vec, double* __restrict__ part) {
+                                                          int nvec, const double* __restrict__ u2, int n2, bool vec,
+                                                          double* __restrict__ part) {
 #pragma clang fp contract(off)
   constexpr int kPerW = kMdMax / 4;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int first2 = nvec - n2;  // vectors first2 .. nvec - 1 are dotted with u2
   double acc[kPerW];
 #pragma unroll
   for (int m = 0; m < kPerW; ++m) acc[m] = 0.0;
@@ -2218,25 +2222,32 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const doubl
     const int64_t e = e0 + 2 * lane;
     const double2 ua = *reinterpret_cast<const double2*>(u + e);
     const double2 ub = *reinterpret_cast<const double2*>(u + e + 128);
+    double2 wa = make_double2(0.0, 0.0), wb = wa;
+    if (n2 > 0) {
+      wa = *reinterpret_cast<const double2*>(u2 + e);
+      wb = *reinterpret_cast<const double2*>(u2 + e + 128);
+    }
 #pragma unroll
     for (int m = 0; m < kPerW; ++m) {
       const int i = wid + 4 * m;
       if (i < nvec) {
         const double2 va = *reinterpret_cast<const double2*>(L.v[i] + e);
         const double2 vb = *reinterpret_cast<const double2*>(L.v[i] + e + 128);
-        acc[m] += va.x * ua.x;
-        acc[m] += va.y * ua.y;
-        acc[m] += vb.x * ub.x;
-        acc[m] += vb.y * ub.y;
+        const double2 xa = i < first2 ? ua : wa, xb = i < first2 ? ub : wb;
+        acc[m] += va.x * xa.x;
+        acc[m] += va.y * xa.y;
+        acc[m] += vb.x * xb.x;
+        acc[m] += vb.y * xb.y;
       }
     }
   }
   for (int64_t e = n_vec + static_cast<int64_t>(blockIdx.x) * 64 + lane; e < n; e += static_cast<int64_t>(gridDim.x) * 64) {
     const double ue = u[e];
+    const double we = n2 > 0 ? u2[e] : 0.0;
 #pragma unroll
     for (int m = 0; m < kPerW; ++m) {
       const int i = wid + 4 * m;
-      if (i < nvec) acc[m] += L.v[i][e] * ue;
+      if (i < nvec) acc[m] += L.v[i][e] * (i < first2 ? ue : we);
     }
   }
 #pragma unroll
@@ -2250,121 +2261,12 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const doubl
 }
 
 hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
-                           hipStream_t s) {
-  if (nvec < 1 || nvec > kMdMax || grid < 1 || grid > kRedGrid) return hipErrorInvalidValue;
-  bool vec = aligned16d(u);
-  for (int i = 0; i < nvec; ++i) vec = vec && aligned16d(L.v[i]);
-  hipLaunchKernelGGL(multidot_kernel, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, vec, part);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// K6i: one constrained step's increments in one pass (spis.cpp con_inc_enqueue): u = M x by K1's
-// row blocks (u[r] bit-identical to K1's), never stored: each row's u[r] goes straight into the
-// partials of L.v[i] . u (i < nl), and the same row's P.v[i][r] * Q.v[i][r] into the partials of
-// the pair dots (i < np: v . z_a of the linear constraints).  Rows are the SpMV's (every row once),
-// so a pair dot covers [0, n) like any other.  part[i * gridDim.x + blk], i < nl + np, for
-// cgs_finalize.  Products rounded, then added (contraction off).  Bytes: M's nnz (12 B) + x
-// gathers + (nl + 2 np) 8 n: no u write and re-read, and one launch instead of a SpMV, a
-// multidot and a dot with a finalize each.
-// ---------------------------------------------------------------------------------------------
-template <int NL>
-__global__ __launch_bounds__(kBlock) void spmv_gram_kernel(
-    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
-    const int32_t* __restrict__ blk_row, int n_blk, const double* __restrict__ x, VecList L, int nl, VecList P,
-    VecList Q, int np, double* __restrict__ part) {
-#pragma clang fp contract(off)
-  __shared__ double s_prod[kNnzCap];
-  __shared__ double s_red[(NL + kGramPairMax) * 4];
-  __shared__ double s_wave[4];
-  double acc[NL], accp[kGramPairMax];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) acc[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < kGramPairMax; ++i) accp[i] = 0.0;
-  auto row_done = [&](int r, double sum) {
-#pragma unroll
-    for (int i = 0; i < NL; ++i)
-      if (i < nl) acc[i] += L.v[i][r] * sum;
-#pragma unroll
-    for (int i = 0; i < kGramPairMax; ++i)
-      if (i < np) accp[i] += P.v[i][r] * Q.v[i][r];
-  };
-  for (int blk = blockIdx.x; blk < n_blk; blk += gridDim.x) {
-    const int r0 = blk_row[blk];
-    const int r1 = blk_row[blk + 1];
-    const int nz0 = rp[r0];
-    const int nnz = rp[r1] - nz0;
-    if (nnz > kNnzCap) {  // one long row (r1 == r0 + 1): K1's workgroup reduction
-      double a = 0.0;
-      for (int i = nz0 + threadIdx.x; i < nz0 + nnz; i += kBlock) a += va[i] * x[ci[i]];
-      const double sum = block_sum(a, s_wave);
-      if (threadIdx.x == 0) row_done(r0, sum);
-      continue;
-    }
-    constexpr int kPer = kNnzCap / kBlock;
-    int cols[kPer];
-    double vals[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int i = threadIdx.x + u * kBlock;
-      cols[u] = i < nnz ? ci[nz0 + i] : 0;
-      vals[u] = i < nnz ? va[nz0 + i] : 0.0;
-    }
-    double xs[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) xs[u] = x[cols[u]];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int i = threadIdx.x + u * kBlock;
-      if (i < nnz) s_prod[i] = vals[u] * xs[u];
-    }
-    __syncthreads();
-    const int r = r0 + threadIdx.x;
-    if (r < r1) {
-      const int s = rp[r] - nz0;
-      const int e = rp[r + 1] - nz0;
-      double sum = 0.0;
-      for (int t = s; t < e; ++t) sum += s_prod[t];
-      row_done(r, sum);
-    }
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < NL; ++i)
-    if (i < nl) {
-      const double t = wave_sum(acc[i]);
-      if (lane == 0) s_red[i * 4 + wid] = t;
-    }
-#pragma unroll
-  for (int i = 0; i < kGramPairMax; ++i)
-    if (i < np) {
-      const double t = wave_sum(accp[i]);
-      if (lane == 0) s_red[(nl + i) * 4 + wid] = t;
-    }
-  __syncthreads();
-  if (static_cast<int>(threadIdx.x) < nl + np) {
-    const double* w = s_red + threadIdx.x * 4;
-    part[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = ((w[0] + w[1]) + w[2]) + w[3];
-  }
-}
-
-hipError_t launch_spmv_gram(const CsrView& M, const double* x, const VecList& L, int nl, const VecList& P,
-                            const VecList& Q, int np, double* part, int grid, hipStream_t s) {
-  if (M.blk_row == nullptr || nl < 0 || nl > kMdMax || np < 0 || np > kGramPairMax || nl + np < 1 || grid < 1 ||
-      grid > kRedGrid)
+                           hipStream_t s, const double* u2, int n2) {
+  if (nvec < 1 || nvec > kMdMax || grid < 1 || grid > kRedGrid || n2 < 0 || n2 > nvec || (n2 > 0 && u2 == nullptr))
     return hipErrorInvalidValue;
-  dim3 g(grid), b(kBlock);
-#define SPIS_SG(NLV)                                                                                        \
-  hipLaunchKernelGGL(spmv_gram_kernel<NLV>, g, b, 0, s, M.indptr, M.indices, M.vals, M.blk_row, M.n_blk, x, \
-                     L, nl, P, Q, np, part)
-  if (nl <= 8) SPIS_SG(8);
-  else if (nl <= 16) SPIS_SG(16);
-  else if (nl <= 24) SPIS_SG(24);
-  else if (nl <= 32) SPIS_SG(32);
-  else SPIS_SG(kMdMax);
-#undef SPIS_SG
+  bool vec = aligned16d(u) && (n2 == 0 || aligned16d(u2));
+  for (int i = 0; i < nvec; ++i) vec = vec && aligned16d(L.v[i]);
+  hipLaunchKernelGGL(multidot_kernel, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, u2, n2, vec, part);
   return hipGetLastError();
 }
 
@@ -2965,7 +2867,10 @@ hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pi
                                const double* rpart, int r_in, double* r_out, unsigned long long* flag,
                                const unsigned long long* seq) {
   const int64_t chunks = (n + kCgsChunk - 1) / kCgsChunk;
-  // one chunk per workgroup while they all fit, else two (the second streamed)
+  // one chunk per workgroup while they all fit, else two per workgroup, the second streamed.
+  // Halving the grid beats filling it (C4, N = 300,006: 586 workgroups 28.0-28.4 us per launch vs
+  // 1,024 with only 148 chunks streamed 30.9-31.8 us, K2q 30.4-31.0; gpurun_out/r05k2s2, r05k2s3):
+  // the spin hand-offs' cost grows with the workgroups that publish and poll
   const bool two = chunks > icwy_onepass_grid_cap(false);
   const int64_t grid = two ? (chunks + 1) / 2 : chunks;
   if (nv < 1 || nv > kCgsMax || n < 1 || grid > icwy_onepass_grid_cap(two) || tag == 0 || slots == nullptr ||

@@ -119,7 +119,7 @@ struct spis_context {
   double* cg_vpart = nullptr;          // K7t: the transpose's linear-term partials
   double* inc_u = nullptr;             // incremental Gram: M z_a (n)
   int64_t inc_u_len = 0;
-  double* inc_part = nullptr;          // its partials (values x grid: K6i, multidot)
+  double* inc_part = nullptr;          // its multidot partials (values x grid)
   size_t inc_part_len = 0;
   double* inc_res = nullptr;           // its reduced values (device), copied to con_pinned
   size_t inc_res_len = 0;
@@ -495,7 +495,10 @@ static int spmv_local(spis_context* c, spis_workspace* ws, const spis_matrix* M,
     HIP_TRY(launch_spmv(M->view(), kEpiPlain, ws->ext, y, nullptr, nullptr, g, c->stream));
     return SPIS_OK;
   }
-  HIP_TRY(launch_spmv(M->view(), kEpiPlain, x, y, nullptr, nullptr, g, st != nullptr ? st : c->stream));
+  // one GPU: the pipelined kernel on the matrix's K1p table (rows bit-identical to K1's)
+  // (else K1 on the row-block table)
+  const CsrView pv = M->dual_view().blk_meta != nullptr ? M->dual_view() : M->view();
+  HIP_TRY(launch_spmv(pv, kEpiPlain, x, y, nullptr, nullptr, spmv_grid(pv, false), st != nullptr ? st : c->stream));
   return SPIS_OK;
 }
 
@@ -1785,8 +1788,8 @@ struct ConStep {
   int p = 0, m = 0;
   std::vector<int> from;  // per constraint: first new column (inc)
   hipStream_t st = nullptr;  // the stream the results are copied on (record the wait's event there)
-  // inc: the values in partial / result order: the first pass's, the pair dots v . z_a, v . x0
-  // (carried by that pass, K6i, when they fit), the other passes'
+  // inc: the values in partial / result order: the first pass's, the pair dots v . z_a, v . x0,
+  // the other passes'
   std::vector<IncSlot> slots;
   std::vector<IncPass> passes;
   int pair0 = 0, npair = 0;
@@ -1860,10 +1863,19 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_const
   }
   auto zv = [&](int a) { return a == k ? x0 : Z + static_cast<int64_t>(a) * pitch; };
   auto part_at = [&](int slot) { return c->inc_part + static_cast<size_t>(slot) * g; };
+  if (c->inc_u_len < n) {
+    if (c->inc_u) HIP_TRY(hipFree(c->inc_u));
+    HIP_TRY(hipMalloc(&c->inc_u, sizeof(double) * std::max<int64_t>(n, 1)));
+    c->inc_u_len = n;
+  }
+  // per pass: u = M z_a (K1p), then [z_0 .. z_a, x0] . u (multidot); the pair dots v . z_a ride in
+  // the first pass's multidot when they are one constraint's (the slots follow that pass's), else
+  // one multidot per constraint; one finalize for every value.  (A fused SpMV + dots kernel, the
+  // dots in the SpMV's row epilogue, ran 75-175 us per pass at C3 against 26 + 8-30 here: its
+  // epilogue loads of the dotted vectors are not prefetched: gpurun_out/r05inc3)
   bool carried = false;
   for (size_t i = 0; i < cs.passes.size(); ++i) {
     const IncPass& ps = cs.passes[i];
-    spis_matrix* M = cons[ps.ci].M;
     VecList L{};
     if (ps.a == k) {
       L.v[0] = x0;
@@ -1871,31 +1883,24 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_const
       for (int b = 0; b <= ps.a; ++b) L.v[b] = zv(b);
       L.v[ps.a + 1] = x0;
     }
-    const CsrView mv = M->view();
-    if (mv.blk_row != nullptr && (!c->dist_on() || M->n_ghost == 0)) {  // K6i: one pass
-      VecList P{}, Q{};
-      int np = 0;
-      if (i == 0 && cs.npair <= kGramPairMax) {
-        for (int q = 0; q < cs.npair; ++q) {
-          const IncSlot& sl = cs.slots[cs.pair0 + q];
-          P.v[q] = cons[sl.ci].v_dev;
-          Q.v[q] = zv(sl.a);
-        }
-        np = cs.npair;
+    int nl = ps.nl, n2 = 0;
+    const double* u2 = nullptr;
+    if (i == 0 && cs.npair > 0 && ps.nl + cs.npair <= kMdMax) {
+      const int ci2 = cs.slots[cs.pair0].ci;
+      bool one = true;
+      for (int q = 0; q < cs.npair; ++q) one = one && cs.slots[cs.pair0 + q].ci == ci2;
+      if (one) {
+        for (int q = 0; q < cs.npair; ++q) L.v[nl + q] = zv(cs.slots[cs.pair0 + q].a);
+        u2 = cons[ci2].v_dev;
+        n2 = cs.npair;
+        nl += n2;
         carried = true;
       }
-      HIP_TRY(launch_spmv_gram(mv, zv(ps.a), L, ps.nl, P, Q, np, part_at(ps.slot0), g, st));
-    } else {  // several GPUs with ghost columns: the exchange-aware SpMV, then the multidot
-      if (c->inc_u_len < n) {
-        if (c->inc_u) HIP_TRY(hipFree(c->inc_u));
-        HIP_TRY(hipMalloc(&c->inc_u, sizeof(double) * std::max<int64_t>(n, 1)));
-        c->inc_u_len = n;
-      }
-      ST_TRY(spmv_local(c, ws, M, zv(ps.a), c->inc_u, st));
-      HIP_TRY(launch_multidot(n, c->inc_u, L, ps.nl, part_at(ps.slot0), g, st));
     }
+    ST_TRY(spmv_local(c, ws, cons[ps.ci].M, zv(ps.a), c->inc_u, st));
+    HIP_TRY(launch_multidot(n, c->inc_u, L, nl, part_at(ps.slot0), g, st, u2, n2));
   }
-  if (!carried)  // the pair dots: one multidot per constraint, v . [its columns]
+  if (!carried)
     for (int q = 0; q < cs.npair;) {
       const int ci = cs.slots[cs.pair0 + q].ci;
       VecList L{};
