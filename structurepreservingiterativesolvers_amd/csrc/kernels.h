@@ -184,9 +184,11 @@ constexpr int kMdMax = 40;
 struct VecList {
   const double* v[kMdMax];
 };
-// (the last n2 of the nvec vectors are dotted with u2 instead)
+// (the last n2 of the nvec vectors are dotted with u2 instead; px > 0: also xo = x0 + sum_{i < px}
+// y[i] L.v[i], the update GEMV riding along)
 hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
-                           hipStream_t s, const double* u2 = nullptr, int n2 = 0);
+                           hipStream_t s, const double* u2 = nullptr, int n2 = 0, int px = 0,
+                           const double* y = nullptr, const double* x0 = nullptr, double* xo = nullptr);
 // x = Z[:, :p] y + x0 ; y on the host (p <= kYArg: passed as a kernel argument) or in HBM
 hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const double* y,
                        bool y_on_host, const double* x0, double* x, hipStream_t s,

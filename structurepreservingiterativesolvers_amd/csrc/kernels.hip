@@ -2203,13 +2203,19 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
 // (as cgs_dot): each wave reads u's (and u2's) chunk once for its vectors; 256-element chunks per
 // workgroup iteration (16-B loads when every pointer is 16-B aligned), a scalar tail otherwise;
 // the products are rounded, then added (contraction off); fixed-order wave sums.
-// Bytes: (nvec + 4 (+ 4)) 8 N.
+// GX: the update GEMV of the step before rides along, xo = x0 + sum_{i < px} y_i L.v[i] (L.v[0 ..
+// px-1] = z_0 .. z_{px-1}, read here anyway): each wave sums its vectors' terms in order, the
+// four waves' sums are added in wave order through LDS, then x0 (numpy's Z @ y + x0 order).
+// Bytes: (nvec + 4 (+ 4)) 8 N (+ 16 N with GX).
 // ---------------------------------------------------------------------------------------------
+template <bool GX>
 __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const double* __restrict__ u, VecList L,
                                                           int nvec, const double* __restrict__ u2, int n2, bool vec,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part, int px, YArg ya,
+                                                          const double* __restrict__ x0, double* __restrict__ xo) {
 #pragma clang fp contract(off)
   constexpr int kPerW = kMdMax / 4;
+  __shared__ double s_g[GX ? 4 : 1][4][64];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int first2 = nvec - n2;  // vectors first2 .. nvec - 1 are dotted with u2
@@ -2227,6 +2233,7 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const doubl
       wa = *reinterpret_cast<const double2*>(u2 + e);
       wb = *reinterpret_cast<const double2*>(u2 + e + 128);
     }
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
 #pragma unroll
     for (int m = 0; m < kPerW; ++m) {
       const int i = wid + 4 * m;
@@ -2238,16 +2245,55 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const doubl
         acc[m] += va.y * xa.y;
         acc[m] += vb.x * xb.x;
         acc[m] += vb.y * xb.y;
+        if (GX && i < px) {
+          const double yi = ya.v[i];
+          g0 += yi * va.x;
+          g1 += yi * va.y;
+          g2 += yi * vb.x;
+          g3 += yi * vb.y;
+        }
       }
     }
+    if (GX) {
+      s_g[wid][0][lane] = g0;
+      s_g[wid][1][lane] = g1;
+      s_g[wid][2][lane] = g2;
+      s_g[wid][3][lane] = g3;
+      __syncthreads();
+      if (wid == 0) {
+        double t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = ((s_g[0][q][lane] + s_g[1][q][lane]) + s_g[2][q][lane]) + s_g[3][q][lane];
+        const double2 xa = *reinterpret_cast<const double2*>(x0 + e);
+        const double2 xb = *reinterpret_cast<const double2*>(x0 + e + 128);
+        *reinterpret_cast<double2*>(xo + e) = make_double2(t[0] + xa.x, t[1] + xa.y);
+        *reinterpret_cast<double2*>(xo + e + 128) = make_double2(t[2] + xb.x, t[3] + xb.y);
+      }
+      __syncthreads();
+    }
   }
-  for (int64_t e = n_vec + static_cast<int64_t>(blockIdx.x) * 64 + lane; e < n; e += static_cast<int64_t>(gridDim.x) * 64) {
-    const double ue = u[e];
-    const double we = n2 > 0 ? u2[e] : 0.0;
+  // the scalar tail: 64 elements per workgroup iteration, the trip count uniform over the
+  // workgroup (GX's barriers), lanes past n idle
+  for (int64_t eb = n_vec + static_cast<int64_t>(blockIdx.x) * 64; eb < n; eb += static_cast<int64_t>(gridDim.x) * 64) {
+    const int64_t e = eb + lane;
+    const bool in = e < n;
+    const double ue = in ? u[e] : 0.0;
+    const double we = in && n2 > 0 ? u2[e] : 0.0;
+    double ge = 0.0;
 #pragma unroll
     for (int m = 0; m < kPerW; ++m) {
       const int i = wid + 4 * m;
-      if (i < nvec) acc[m] += L.v[i][e] * (i < first2 ? ue : we);
+      if (i < nvec && in) {
+        const double le = L.v[i][e];
+        acc[m] += le * (i < first2 ? ue : we);
+        if (GX && i < px) ge += ya.v[i] * le;
+      }
+    }
+    if (GX) {
+      s_g[wid][0][lane] = ge;
+      __syncthreads();
+      if (wid == 0 && in) xo[e] = ((s_g[0][0][lane] + s_g[1][0][lane]) + s_g[2][0][lane]) + s_g[3][0][lane] + x0[e];
+      __syncthreads();
     }
   }
 #pragma unroll
@@ -2261,12 +2307,21 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(int64_t n, const doubl
 }
 
 hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nvec, double* part, int grid,
-                           hipStream_t s, const double* u2, int n2) {
-  if (nvec < 1 || nvec > kMdMax || grid < 1 || grid > kRedGrid || n2 < 0 || n2 > nvec || (n2 > 0 && u2 == nullptr))
+                           hipStream_t s, const double* u2, int n2, int px, const double* y, const double* x0,
+                           double* xo) {
+  if (nvec < 1 || nvec > kMdMax || grid < 1 || grid > kRedGrid || n2 < 0 || n2 > nvec || (n2 > 0 && u2 == nullptr) ||
+      px < 0 || px > nvec - n2 || px > kYArg || (px > 0 && (y == nullptr || x0 == nullptr || xo == nullptr)))
     return hipErrorInvalidValue;
-  bool vec = aligned16d(u) && (n2 == 0 || aligned16d(u2));
+  bool vec = aligned16d(u) && (n2 == 0 || aligned16d(u2)) && (px == 0 || (aligned16d(x0) && aligned16d(xo)));
   for (int i = 0; i < nvec; ++i) vec = vec && aligned16d(L.v[i]);
-  hipLaunchKernelGGL(multidot_kernel, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, u2, n2, vec, part);
+  YArg ya;
+  for (int i = 0; i < px; ++i) ya.v[i] = y[i];
+  if (px > 0)
+    hipLaunchKernelGGL(multidot_kernel<true>, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, u2, n2, vec, part, px, ya,
+                       x0, xo);
+  else
+    hipLaunchKernelGGL(multidot_kernel<false>, dim3(grid), dim3(kBlock), 0, s, n, u, L, nvec, u2, n2, vec, part, 0, ya,
+                       x0, xo);
   return hipGetLastError();
 }
 

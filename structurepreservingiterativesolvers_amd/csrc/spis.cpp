@@ -1793,6 +1793,12 @@ struct ConStep {
   std::vector<IncSlot> slots;
   std::vector<IncPass> passes;
   int pair0 = 0, npair = 0;
+  // the caller's request: the previous step's update GEMV x = x0 + Z[:, :gx_p] y (gx_p <= kYArg) in a
+  // multidot that reads z_0 .. z_{gx_p - 1} anyway; gx_done tells whether one took it
+  int gx_p = 0;
+  const double* gx_y = nullptr;
+  double* gx_out = nullptr;
+  bool gx_done = false;
 };
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
@@ -1844,7 +1850,7 @@ static void con_inc_plan(int m, const spis_constraint_desc* cons, int p, const s
 }
 
 static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_constraint_desc* cons, int64_t n,
-                           const double* Z, int64_t pitch, const double* x0, const ConStep& cs) {
+                           const double* Z, int64_t pitch, const double* x0, ConStep& cs) {
   hipStream_t st = cs.st;
   const int k = ws->k;
   const size_t total = cs.slots.size();
@@ -1897,8 +1903,15 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_const
         carried = true;
       }
     }
+    // the GEMV rides in the first pass whose list holds z_0 .. z_{gx_p - 1} (one GPU: x over the
+    // local rows is all of x)
+    int px = 0;
+    if (!cs.gx_done && cs.gx_p > 0 && ps.a != k && ps.a + 1 >= cs.gx_p && !c->dist_on()) {
+      px = cs.gx_p;
+      cs.gx_done = true;
+    }
     ST_TRY(spmv_local(c, ws, cons[ps.ci].M, zv(ps.a), c->inc_u, st));
-    HIP_TRY(launch_multidot(n, c->inc_u, L, nl, part_at(ps.slot0), g, st, u2, n2));
+    HIP_TRY(launch_multidot(n, c->inc_u, L, nl, part_at(ps.slot0), g, st, u2, n2, px, cs.gx_y, x0, cs.gx_out));
   }
   if (!carried)
     for (int q = 0; q < cs.npair;) {
@@ -1984,6 +1997,7 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   cs->p = p;
   cs->m = m;
   cs->inc = false;
+  cs->gx_done = false;
   cs->st = c->stream;
   cs->from.assign(m, 0);
   if (con_inc_eligible(c, ws, m, cons, p)) {
@@ -2800,6 +2814,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     auto queue_gram = [&](int jc, bool side = false) -> int {
       ST_TRY(con_step_enqueue(c, ws, m_of(jc), o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, &gram_step,
                               side));
+      gram_step.gx_p = 0;  // a GEMV request holds for one enqueue
       HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
       gram_queued = jc;
       return SPIS_OK;
@@ -2991,12 +3006,21 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         // goes on the main stream right behind that chain, ahead of U_j's GEMV and a_{j+2}: it
         // runs while the host solves LS_j and is done when the host reaches LS_{j+1} (beside the
         // chain on stream2 it was starved by the persistent SpMV and chain kernels)
+        // U_j's GEMV rides in its multidot (the increments read z_0 .. z_{j+1}): no GEMV launch and
+        // no side-stream hand-off before [U_j res | a_{j+2}]
+        const bool need_gemv = !fused || constrained;
+        bool gemv_done = false;
         if (j + 2 < k && gram_queued != j + 1 && (o->method == SPIS_CGMRES_P || safety != kSafetyNone) &&
-            gram_early_ok(j + 1))
+            gram_early_ok(j + 1)) {
+          gram_step.gx_p = need_gemv && p <= kYArg ? p : 0;
+          gram_step.gx_y = y.data();
+          gram_step.gx_out = S.xbuf(j);
           ST_TRY(queue_gram(j + 1));
+          gemv_done = gram_step.gx_done;
+        }
         // x_j: from c_{j+1} (fused), else a GEMV beside c_{j+1} on the side stream, or after it
         // on the main stream when c_{j+1} computed x_j from the speculative unconstrained y_j
-        if (!fused || constrained) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));
+        if (need_gemv && !gemv_done) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
           ST_TRY(S.enqueue_dual(j, j + 2));
