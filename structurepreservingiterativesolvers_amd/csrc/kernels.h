@@ -177,7 +177,7 @@ hipError_t launch_icwy_onepass(int64_t n, double* w, const double* Q, int64_t pi
                                int r_in = 0, double* r_out = nullptr, unsigned long long* flag = nullptr,
                                const unsigned long long* seq = nullptr);
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
-                               hipStream_t s, int zero_to = 0);
+                               hipStream_t s, int zero_to = 0, bool pin = false);
 // the incremental constraint Gram's dots: part[i * grid + blk] = partial of L.v[i] . u (i < nvec);
 // reduce with launch_cgs_finalize(part, grid, nvec, ...)
 constexpr int kMdMax = 40;

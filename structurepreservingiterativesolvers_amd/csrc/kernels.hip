@@ -2328,14 +2328,18 @@ hipError_t launch_multidot(int64_t n, const double* u, const VecList& L, int nve
 // workgroup i reduces vector i's partials; add (nullable) + c -> h_out (host H column, nullable)
 // zero_to > gridDim.x: workgroup 0 also zeroes c[gridDim.x, zero_to) (the slack a merged
 // all-reduce carries beside the dots: summed every step, it must not grow)
+// pin: c is host memory a host thread polls (system-scope stores, each value its own flag)
 __global__ __launch_bounds__(kBlock) void cgs_finalize_kernel(const double* __restrict__ part, int n_in,
                                                               double* __restrict__ c, const double* __restrict__ add,
-                                                              double* __restrict__ h_out, int zero_to) {
+                                                              double* __restrict__ h_out, int zero_to, bool pin) {
   __shared__ double s_wave[4];
   const int i = blockIdx.x;
   const double t = sum_partials(part + static_cast<int64_t>(i) * n_in, n_in, s_wave);
   if (threadIdx.x == 0) {
-    c[i] = t;
+    if (pin)
+      pin_store(c + i, t);
+    else
+      c[i] = t;
     if (h_out != nullptr) h_out[i] = add[i] + t;
   }
   if (i == 0)
@@ -2412,8 +2416,8 @@ hipError_t launch_icwy_update(int64_t n, double* w, const double* Q, int64_t pit
 }
 
 hipError_t launch_cgs_finalize(const double* part, int n_in, int nv, double* c, const double* add, double* h_out,
-                               hipStream_t s, int zero_to) {
-  hipLaunchKernelGGL(cgs_finalize_kernel, dim3(nv), dim3(kBlock), 0, s, part, n_in, c, add, h_out, zero_to);
+                               hipStream_t s, int zero_to, bool pin) {
+  hipLaunchKernelGGL(cgs_finalize_kernel, dim3(nv), dim3(kBlock), 0, s, part, n_in, c, add, h_out, zero_to, pin);
   return hipGetLastError();
 }
 

@@ -1771,6 +1771,7 @@ static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, cons
 // The first constrained step takes the full reduction (transpose + K7t) and seeds the caches,
 // unless its p is small enough that columns 0 .. p-1 from scratch cost less (kIncScratch).
 constexpr int kIncScratch = 8;
+constexpr uint64_t kConSentinel = 0x7FF4DEAD5EC0FFEDull;  // a signalling NaN no kernel writes
 
 // one value an increment step computes: G(a, b) = z_a . M z_b of constraint ci (m), else its
 // v . z_a (gv[a]); a, b = k stand for x0
@@ -1799,6 +1800,7 @@ struct ConStep {
   const double* gx_y = nullptr;
   double* gx_out = nullptr;
   bool gx_done = false;
+  size_t polled = 0;  // > 0: the values arrive as polled pinned slots (no ev_gram to wait for)
 };
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
@@ -1925,6 +1927,17 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_const
       HIP_TRY(launch_multidot(n, cons[ci].v_dev, L, cnt, part_at(cs.pair0 + q), g, st));
       q += cnt;
     }
+  if (!c->dist_on()) {  // the finalize stores the values straight into pinned memory, system scope,
+                        // each its own flag (con_step_wait polls them): no copy packet, and no
+                        // system-scope event release (an L2 write-back, ~5 us before the next kernel)
+    for (size_t i = 0; i < total; ++i) reinterpret_cast<volatile uint64_t*>(c->con_pinned)[i] = kConSentinel;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, c->con_pinned, 0));
+    HIP_TRY(launch_cgs_finalize(c->inc_part, g, static_cast<int>(total), static_cast<double*>(dp), nullptr, nullptr, st,
+                                0, true));
+    cs.polled = total;
+    return SPIS_OK;
+  }
   HIP_TRY(launch_cgs_finalize(c->inc_part, g, static_cast<int>(total), c->inc_res, nullptr, nullptr, st));
   ST_TRY(allreduce_on(c, c->inc_res, static_cast<int64_t>(total), st));  // several GPUs: rows summed
   HIP_TRY(hipMemcpyAsync(c->con_pinned, c->inc_res, sizeof(double) * total, hipMemcpyDeviceToHost, st));
@@ -1989,6 +2002,25 @@ static void con_terms_from_cache(const spis_workspace* ws, int m, const spis_con
   }
 }
 
+// the host's wait for a step's reduction: its polled pinned slots, else ev_gram (recorded behind it)
+static int con_step_wait(spis_context* c, const ConStep& cs) {
+  if (cs.polled == 0) return wait_event(c->ev_gram);
+  const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(c->con_pinned);
+  const double t0 = now_s();
+  for (size_t i = 0; i < cs.polled; ++i)
+    for (unsigned spin = 0; __atomic_load_n(const_cast<const uint64_t*>(w + i), __ATOMIC_ACQUIRE) == kConSentinel;
+         ++spin) {
+      if ((spin & 4095) == 4095 && now_s() - t0 > 0.02) {  // a failed stream never writes them
+        const hipError_t e = hipStreamQuery(cs.st);
+        if (e != hipSuccess && e != hipErrorNotReady) return fail(SPIS_ERR_HIP, "stream: %s", hipGetErrorString(e));
+        if (e == hipSuccess && __atomic_load_n(const_cast<const uint64_t*>(w + i), __ATOMIC_ACQUIRE) == kConSentinel)
+          return fail(SPIS_ERR_STATE, "constraint increments: the stream drained without value %zu", i);
+      }
+      __builtin_ia32_pause();
+    }
+  return SPIS_OK;
+}
+
 // one constrained step's reduction, enqueued on the main stream with its results copied to
 // c->con_pinned: the increments when every active constraint can take them, else the full
 // reduction (which seeds the caches when they are eligible)
@@ -1998,6 +2030,7 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   cs->m = m;
   cs->inc = false;
   cs->gx_done = false;
+  cs->polled = 0;
   cs->st = c->stream;
   cs->from.assign(m, 0);
   if (con_inc_eligible(c, ws, m, cons, p)) {
@@ -2037,8 +2070,8 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                   QuadCon* out) {
   ConStep cs;
   ST_TRY(con_step_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, &cs, false));
-  HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking synchronize wakes
-  ST_TRY(wait_event(c->ev_gram));                    // up tens of us late
+  if (cs.polled == 0) HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking
+  ST_TRY(con_step_wait(c, cs));                                         // synchronize wakes up late
   con_step_assemble(c, ws, cons, cs, out);
   return SPIS_OK;
 }
@@ -2815,7 +2848,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       ST_TRY(con_step_enqueue(c, ws, m_of(jc), o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, &gram_step,
                               side));
       gram_step.gx_p = 0;  // a GEMV request holds for one enqueue
-      HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
+      if (gram_step.polled == 0) HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
       gram_queued = jc;
       return SPIS_OK;
     };
@@ -2862,7 +2895,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (L && gram_queued == j && safety != kSafetyTrue && !o->timing && spec_kkt != j) {
         const double* hp = c->pinned + S.hoff(j);
         if (hp[j + 1] != 0.0) {
-          ST_TRY(wait_event(c->ev_gram));
+          ST_TRY(con_step_wait(c, gram_step));
           con_step_assemble(c, ws, o->constraints, gram_step, cons.data());  // (gram_step.m constraints)
           if (!col_added) {
             for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
@@ -2940,7 +2973,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         if (m_active > 0 && spec_kkt == j && m_active == gram_step.m) {
           // terms assembled and the KKT solved before res_{j-1} was waited for (above)
         } else if (m_active > 0 && gram_queued == j && m_active == gram_step.m) {
-          ST_TRY(wait_event(c->ev_gram));  // queued before res_{j-1} was waited for (L mode)
+          ST_TRY(con_step_wait(c, gram_step));  // queued before res_{j-1} was waited for (L mode)
           con_step_assemble(c, ws, o->constraints, gram_step, cons.data());
         } else if (m_active > 0) {
           ST_TRY(constraint_terms_all(c, ws, m_active, o->constraints, n, p, ws->Zb, ws->pitch, ws->x0,
