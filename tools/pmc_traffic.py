@@ -14,8 +14,9 @@ options.  Its last launches are the bench's standalone timing of the solver's Sp
 calibration: the evicting read (stream_read_kernel, 1 GiB of 16-B loads per lane) gives
 FETCH_SIZE's unit, the 1 GiB zero-fill of its buffer (__amd_rocclr_fillBufferAligned)
 WRITE_SIZE's.  Reported per launch: the dual SpMV in the solver and standalone cold, the MGS of
-one Arnoldi step (every kernel of it, mean over the chain positions the solves ran), with the
-SHA-256 of csrc/kernels.hip and the options.
+one Arnoldi step (every kernel of it, mean over the chain positions the solves ran), the
+constrained step's basis transpose and K7t / K7m Gram launches, with the SHA-256 of
+csrc/kernels.hip and the options.
 """
 from __future__ import annotations
 
@@ -96,6 +97,13 @@ def reduce(cfg, fetch_csv, write_csv, out):
         },
         "kernel_names": sorted({names[d] for d in solver_dual} | {names[d] for d in mgs}),
     }
+    # the constrained step's full reduction (round 5): the basis transpose and the K7t / K7m Gram
+    for key, pat in (("transpose", "transpose_basis_kernel"), ("gram_sym", "constraint_gram_sym_kernel"),
+                     ("gram_mfma", "constraint_gram_mfma_kernel")):
+        ds = [d for d in byte if d <= end_solver and pat in names[d]]
+        if ds:
+            res["bytes_per_launch"][key] = statistics.mean(byte[d] for d in ds)
+            res["launches"][key] = len(ds)
     a = argparse.Namespace(config=cfg, spmv_pipe="auto", col16=1, slab_key=1, chain=3, nt_basis=2, orthog="mgs",
                            no_fuse=False, M=None)
     wl = bench.build_workload(argparse.Namespace(config=cfg, M=None, cycles=1))
