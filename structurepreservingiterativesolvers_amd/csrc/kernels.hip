@@ -16,7 +16,6 @@
 #include <type_traits>
 
 #include "kernels.h"
-#include "win_table.h"
 
 namespace spis {
 
@@ -555,179 +554,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
       part1[blockIdx.x] = tot1;
       if (DUAL) part2[blockIdx.x] = tot2;
     }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// K1w: the pipelined dual SpMV with windowed gathers (win_table.h).  K1dp gathers x1[c], x2[c]
-// from global memory after the block's columns arrive: a dependent round trip per block that a
-// probe measured at a third of the kernel (C3 dual 36.2 -> 24.6 us warm, C5 474 -> 300 us, with
-// the gathers replaced by coalesced loads; profiles/r05_spmv_gather_probe.txt).  Here each block's
-// x values arrive as whole 64-column chunks (its window, <= kWinChunks chunks, chunk ids from a
-// table), loaded one block ahead with the block's values and 16-bit window positions: nothing in
-// the prefetch depends on another load except the chunk ids, which are themselves loaded one
-// block earlier still.  The window goes to LDS as (x1, x2) pairs, the products gather from it,
-// and the row sums are K1's (left to right): rows bit-identical to SciPy.
-// LDS: window 32 KB + products 34 KB: two workgroups per CU.
-// ---------------------------------------------------------------------------------------------
-#ifndef SPIS_WIN_WPE
-#define SPIS_WIN_WPE 2  // waves per SIMD the kernel is compiled for (LDS allows 2 at 32 chunks)
-#endif
-constexpr int kWinPer = kWinChunks * 64 / kBlock;  // window pairs per thread
-template <int CAP>
-struct WinStage {
-  static constexpr int kPer = CAP / kBlock;
-  int r0, r1, nz0, nnz;
-  int lid[kPer];
-  double vals[kPer];
-  int rs, re;
-  double a1, a2;
-  double2 win[kWinPer];
-};
-
-template <int CAP, int MODE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SPIS_WIN_WPE, SPIS_WIN_WPE))) void spmv_win_kernel(
-    const int32_t* __restrict__ rp, const int32_t* __restrict__ ci, const double* __restrict__ va,
-    const uint16_t* __restrict__ lidx, const int32_t* __restrict__ chunks, const int2* __restrict__ meta, int n_blk,
-    int walk, const double* __restrict__ x1, const double* __restrict__ aux1, double* __restrict__ part1,
-    const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2) {
-  static_assert(MODE == 4, "the dual (residual of x1 against aux1 = b, Arnoldi w = A x2, q0 . w)");
-  constexpr int kPer = WinStage<CAP>::kPer;
-  __shared__ double2 s_p[CAP + CAP / 16];
-  __shared__ double2 s_w[kWinChunks * 64];
-  __shared__ double s_wave[4];
-  double pt1 = 0.0, pt2 = 0.0;
-  int b0, b1, bs;
-  block_walk(n_blk, walk, b0, b1, bs);
-  const int ms = walk == 2 ? 2 : 1;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // chunk ids of this thread's window pairs (slot wave + 4 u) for a block
-  auto load_ids = [&](int lb, int (&ids)[kWinPer]) {
-#pragma unroll
-    for (int u = 0; u < kWinPer; ++u) ids[u] = lb < b1 ? chunks[static_cast<int64_t>(lb) * kWinChunks + wave + 4 * u] : -1;
-  };
-  auto load = [&](WinStage<CAP>& st, int lb, const int (&ids)[kWinPer]) {
-    const int2 m0 = meta[lb * ms];
-    const int2 m1 = meta[lb * ms + 1];
-    st.r0 = m0.x;
-    st.r1 = m1.x;
-    st.nz0 = m0.y;
-    st.nnz = m1.y - m0.y;
-#pragma unroll
-    for (int u = 0; u < kWinPer; ++u) {
-      const int c = ids[u] * 64 + lane;
-      st.win[u] = ids[u] >= 0 ? make_double2(x1[c], x2[c]) : make_double2(0.0, 0.0);
-    }
-    if (st.nnz > CAP) return;  // a long row: read directly by the workgroup-wide path
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int i = threadIdx.x + u * kBlock;
-      st.lid[u] = i < st.nnz ? lidx[st.nz0 + i] : 0;
-      st.vals[u] = i < st.nnz ? va[st.nz0 + i] : 0.0;
-    }
-    const int r = st.r0 + threadIdx.x;
-    if (r < st.r1) {
-      st.rs = rp[r] - st.nz0;
-      st.re = rp[r + 1] - st.nz0;
-      st.a1 = aux1[r];
-      st.a2 = aux2[r];
-    } else {
-      st.rs = st.re = 0;
-    }
-  };
-  int ids[kWinPer];  // the chunk ids of the block after the next one
-  auto step = [&](WinStage<CAP>& cur, WinStage<CAP>& nxt, int blk) __attribute__((always_inline)) {
-    const int nb = blk + bs;
-    if (cur.nnz > CAP) {  // one long row (r1 == r0 + 1): K1's workgroup reduction on the columns
-      double acc1 = 0.0, acc2 = 0.0;
-      for (int i = cur.nz0 + threadIdx.x; i < cur.nz0 + cur.nnz; i += kBlock) {
-        const int c = ci[i];
-        acc1 += va[i] * x1[c];
-        acc2 += va[i] * x2[c];
-      }
-      const double s1 = block_sum(acc1, s_wave), s2 = block_sum(acc2, s_wave);
-      if (threadIdx.x == 0) {
-        const int r0 = cur.r0;
-        const double t = s1 - aux1[r0];
-        pt1 += t * t;
-        y2[r0] = s2;
-        pt2 += aux2[r0] * s2;
-      }
-      if (nb < b1) load(nxt, nb, ids);
-      load_ids(nb + bs, ids);
-      return;
-    }
-    // the next block's window, values and positions first: in flight through this block's LDS phases
-    if (nb < b1) load(nxt, nb, ids);
-    load_ids(nb + bs, ids);
-#pragma unroll
-    for (int u = 0; u < kWinPer; ++u) s_w[threadIdx.x + u * kBlock] = cur.win[u];
-    __syncthreads();
-    const int pbase = threadIdx.x + (threadIdx.x >> 4);
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int i = threadIdx.x + u * kBlock;
-      if (i < cur.nnz) {
-        const double2 g = s_w[cur.lid[u]];
-        s_p[pbase + u * (kBlock + kBlock / 16)] = make_double2(cur.vals[u] * g.x, cur.vals[u] * g.y);
-      }
-    }
-    __syncthreads();
-    const int r = cur.r0 + threadIdx.x;
-    if (r < cur.r1) {
-      double s1 = 0.0, s2 = 0.0;
-      int t = cur.rs;
-      for (; t + 8 <= cur.re; t += 8) {
-        double2 pp[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) pp[u] = s_p[t + u + ((t + u) >> 4)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          s1 += pp[u].x;
-          s2 += pp[u].y;
-        }
-      }
-      for (; t + 4 <= cur.re; t += 4) {
-        const double2 p0 = s_p[t + (t >> 4)], p1 = s_p[t + 1 + ((t + 1) >> 4)];
-        const double2 p2 = s_p[t + 2 + ((t + 2) >> 4)], p3 = s_p[t + 3 + ((t + 3) >> 4)];
-        s1 += p0.x;
-        s2 += p0.y;
-        s1 += p1.x;
-        s2 += p1.y;
-        s1 += p2.x;
-        s2 += p2.y;
-        s1 += p3.x;
-        s2 += p3.y;
-      }
-      for (; t < cur.re; ++t) {
-        const double2 pp = s_p[t + (t >> 4)];
-        s1 += pp.x;
-        s2 += pp.y;
-      }
-      const double tt = s1 - cur.a1;
-      pt1 += tt * tt;
-      y2[r] = s2;
-      pt2 += cur.a2 * s2;
-    }
-    __syncthreads();
-  };
-  WinStage<CAP> sa, sb;
-  if (b0 < b1) {
-    load_ids(b0, ids);
-    load(sa, b0, ids);
-    load_ids(b0 + bs, ids);
-  }
-  for (int blk = b0; blk < b1; blk += 2 * bs) {
-    step(sa, sb, blk);
-    if (blk + bs >= b1) break;
-    step(sb, sa, blk + bs);
-  }
-  const double tot1 = block_sum(pt1, s_wave);
-  const double tot2 = block_sum(pt2, s_wave);
-  if (threadIdx.x == 0) {
-    part1[blockIdx.x] = tot1;
-    part2[blockIdx.x] = tot2;
   }
 }
 

@@ -714,7 +714,7 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (argc > 2 && std::string(argv[2]) == "win") {
-    // K1w (windowed gathers, kernels.hip spmv_win_kernel) against K1dp, both on slab-ordered
+    // K1w (windowed gathers, spmv_variants.hip spmv_win_kernel) against K1dp, both on slab-ordered
     // tables (K1w's split by windows of <= kWinChunks 64-column chunks), warm and cold; dual rows
     // bitwise against K1dp
     double *dx2, *dw, *db, *pa, *pb;

@@ -1,4 +1,5 @@
-// win_table.h — host-side tables of the windowed SpMV (K1w, kernels.hip spmv_win_kernel).
+// win_table.h — host-side tables of the windowed SpMV experiment (K1w, tools/spmv_variants.hip spmv_win_kernel;
+// measured slower than K1dp, DESIGN.md §3 "LDS-staged x windows").
 //
 // Each row block of the solver's SpMV table gathers x at a few hundred to ~2,000 distinct
 // columns, in a handful of narrow ranges (swe: the block's own DoF group and the coupled groups'
