@@ -2536,6 +2536,14 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
     ba = ld2(x0, e);
     bb = ld2(x0, e + 128);
   }
+  // 0. the previous update's true residual (its partials are complete: stream order), published
+  // before anything else, so that the host, which enqueues the next dual SpMV once it has read it,
+  // gets the whole launch to do so (published after the dots, it left a 3-10 us gap before that
+  // SpMV at C2 and C4)
+  if (ca.rpart != nullptr && blockIdx.x == 0) {
+    const double t = sum_partials(ca.rpart, ca.r_in, s_wave);
+    if (threadIdx.x == 0) publish(ca.r_out, t, ca.flag, ca.seq);
+  }
   double2 qa[kCgsPerWave], qb[kCgsPerWave];
   {
     const double* ql = Q + static_cast<int64_t>(nv - 1) * pitch;
@@ -2610,10 +2618,6 @@ __global__ __launch_bounds__(kBlock, 4) void icwy_onepass_kernel(int64_t n, doub
   __syncthreads();
   // 3. the coefficients (d already in s_d: ca.d == nullptr)
   icwy_coefficients(ca, nv, s_c, s_gt, s_d);
-  if (ca.rpart != nullptr && blockIdx.x == 0) {
-    const double t = sum_partials(ca.rpart, ca.r_in, s_wave);
-    if (threadIdx.x == 0) publish(ca.r_out, t, ca.flag, ca.seq);
-  }
   // 4. cgs_update's arithmetic on one chunk's slices (the register ones, or TWO's second chunk
   // loaded again): w' = w - sum (stored), the fused GEMV, wave 0's ||w'||^2 terms into a0
   double a0 = 0.0;
