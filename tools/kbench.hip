@@ -912,6 +912,42 @@ int main(int argc, char** argv) {
     FAKERUN("slab, gathers -> coalesced rows (probe)", 1);
     FAKERUN("slab, gathers -> one address (probe)", 2);
 #undef FAKERUN
+    {  // interleaved (x_j, z) pairs: one 16-B gather per nonzero, rows checked bit-equal
+      std::vector<double> hx(n), hp(2 * pitch, 0.0);
+      CK(hipMemcpy(hx.data(), dx, 8 * n, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < n; ++i) {
+        hp[2 * i] = hx[i];
+        hp[2 * i + 1] = h2[i];
+      }
+      double* dp;
+      CK(hipMalloc(&dp, 16 * pitch));
+      CK(hipMemcpy(dp, hp.data(), 16 * pitch, hipMemcpyHostToDevice));
+      snprintf(nm, sizeof nm, "slab, (x, z) pair gathers grid=%d", gr);
+      run(nm, [&] {
+        hipExtLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, false, 1, false, false, false, 3>), dim3(gr), dim3(kBlock),
+                              0, s, e0, e1, 0, drp, dci, dva, ms, nb, 2, dp, db, (double*)nullptr, pa, dx2, dQ, dw, pb,
+                              (const uint16_t*)nullptr, (const int4*)nullptr);
+      });
+      std::vector<double> w1(n), w2(n), p1(gr), p2(gr), q1(gr), q2(gr);
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4>), dim3(gr), dim3(kBlock), 0, s, drp, dci, dva, ms, nb, 2, dx, db,
+                         (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr, (const int4*)nullptr);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(w1.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(p1.data(), pa, 8 * gr, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(q1.data(), pb, 8 * gr, hipMemcpyDeviceToHost));
+      hipLaunchKernelGGL((spmv_pipe_var_kernel<kPipeCap, 4, false, 1, false, false, false, 3>), dim3(gr), dim3(kBlock), 0, s,
+                         drp, dci, dva, ms, nb, 2, dp, db, (double*)nullptr, pa, dx2, dQ, dw, pb, (const uint16_t*)nullptr,
+                         (const int4*)nullptr);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(w2.data(), dw, 8 * n, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(p2.data(), pa, 8 * gr, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(q2.data(), pb, 8 * gr, hipMemcpyDeviceToHost));
+      int64_t bad = 0;
+      for (int64_t i = 0; i < n; ++i) bad += w1[i] != w2[i];
+      for (int i = 0; i < gr; ++i) bad += (p1[i] != p2[i]) + (q1[i] != q2[i]);
+      printf("pair gathers vs two gathers: %lld rows / partials differ\n", (long long)bad);
+      CK(hipFree(dp));
+    }
     for (int g : {512, 1024, 1280}) { SLABRUN("slab", false, 1, ms, 2, g); }
     SLABRUN("slab NT", true, 1, ms, 2, gr);
     SLABRUN("slab WPE2", false, 2, ms, 2, gr);

@@ -148,7 +148,8 @@ __device__ __forceinline__ void pipe_load_v(PipeStage<CAP>& st, const int2* __re
 // BUF: the matrix stream and the gathers through buffer descriptors (32-bit lane offsets), which
 // frees the registers for WPE = 4 waves per SIMD (4 workgroups per CU instead of 3)
 // FAKEG (timing probe only, wrong results): 1 = the x gathers replaced by coalesced loads of the
-// block's own row range, 2 = by one broadcast address: what the kernel costs without gather latency
+// block's own row range, 2 = by one broadcast address: what the kernel costs without gather latency;
+// 3 (correct, DUAL only): x1 holds interleaved (x1, x2) pairs, one 16-B gather per nonzero
 template <int CAP, int MODE, bool NT = false, int WPE = 1, bool C16 = false, bool BUF = false, bool TM = false,
           int FAKEG = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE > 3 ? WPE : (C16 ? 3 : 8)))) void spmv_pipe_var_kernel(
@@ -185,8 +186,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
         double acc1 = 0.0, acc2 = 0.0;
         for (int i = cur.nz0 + threadIdx.x; i < cur.nz0 + cur.nnz; i += kBlock) {
           const int c = C16 ? col16_decode(c16[i], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : ci[i];
-          acc1 += va[i] * x1[c];
-          if (DUAL) acc2 += va[i] * x2[c];
+          if constexpr (FAKEG == 3) {
+            acc1 += va[i] * x1[2 * c];
+            acc2 += va[i] * x1[2 * c + 1];
+          } else {
+            acc1 += va[i] * x1[c];
+            if (DUAL) acc2 += va[i] * x2[c];
+          }
         }
         s1 = block_sum(acc1, s_wave);
         if (DUAL) s2 = block_sum(acc2, s_wave);
@@ -221,7 +227,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, WPE
       int c = C16 ? col16_decode(cur.cols[u], cur.bs0, cur.bs1, cur.bs2, cur.bs3) : cur.cols[u];
       if constexpr (FAKEG == 1) c = min(cur.r0 + ((threadIdx.x + u * kBlock) & 255), cur.r1 - 1);
       if constexpr (FAKEG == 2) c = cur.r0;
-      if constexpr (BUF) {
+      if constexpr (FAKEG == 3) {
+        const double2 pr = reinterpret_cast<const double2*>(x1)[c];
+        g1[u] = pr.x;
+        g2[u] = pr.y;
+      } else if constexpr (BUF) {
         g1[u] = buf_ld1(rx1, c * 8);
         if (DUAL) g2[u] = buf_ld1(rx2, c * 8);
       } else {
