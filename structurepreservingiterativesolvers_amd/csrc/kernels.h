@@ -71,8 +71,11 @@ struct LaunchEv {
   hipEvent_t stop = nullptr;
 };
 
+// (zf, gen, kEpiR0 on the pipelined table only: *zf != gen means x is all zeros (launch_copy_flag)
+// and A finite: r = aux bit for bit without reading the matrix)
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
-                       double* partials, int grid, hipStream_t s, const LaunchEv* ev = nullptr);
+                       double* partials, int grid, hipStream_t s, const LaunchEv* ev = nullptr,
+                       const unsigned* zf = nullptr, unsigned gen = 0);
 // K1d: residual SpMV of x1 (||A x1 - b||^2 partials -> part1) and Arnoldi SpMV of x2 (w = A x2,
 // q0.w partials -> part2) reading the matrix once; both bit-identical to launch_spmv's.  A must
 // carry the kDualCap row-block table; grid <= kSpmvGrid (the partial arrays' length)
@@ -84,7 +87,8 @@ hipError_t launch_spmv_dual(const CsrView& A, const double* x1, const double* b,
 // mode 6 = two true residuals (x1, x2 against aux1 = aux2 = b: ||.||^2 partials, nothing stored)
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev = nullptr);
+                            int grid, hipStream_t s, const LaunchEv* ev = nullptr, const unsigned* zf = nullptr,
+                            unsigned gen = 0);
 // y -= h_i q_i, h_i = sum(part_in); part_out = q_next . y (or y . y if q_next == nullptr)
 hipError_t launch_mgs_step(int64_t n, double* y, const double* qi, const double* qnext,
                            const double* part_in, int n_in, double* part_out, double* h_out,
@@ -246,6 +250,8 @@ hipError_t launch_finalize2(const double* part1, const double* part2, int n_in, 
                             hipStream_t s, unsigned long long* flag);
 hipError_t launch_axpy(int64_t n, double h, const double* x, double* y, hipStream_t s);
 hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s);
+// y = x; *flag = gen if any x[e] != 0
+hipError_t launch_copy_flag(int64_t n, const double* x, double* y, unsigned* flag, unsigned gen, hipStream_t s);
 // streaming read of n doubles (16-B aligned, n even): evicts L2 and the Infinity Cache
 hipError_t launch_stream_read(int64_t n, const double* x, double* sink, hipStream_t s);
 // send[i] = x[idx[i]]

@@ -392,7 +392,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
     const int2* __restrict__ meta, int n_blk, int walk, const double* __restrict__ x1,
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
-    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base) {
+    double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base,
+    const unsigned* __restrict__ zf, unsigned gen) {
   constexpr bool DUAL = MODE == 4 || MODE == 6;
   constexpr int kPer = PipeStage<CAP>::kPer;
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
@@ -404,6 +405,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
   int b0, b1, bs;
   block_walk(n_blk, walk, b0, b1, bs);
   const int ms = walk == 2 ? 2 : 1;  // walk 2: (start, end) pair per block (an ordered table)
+  if (MODE == kEpiR0 && zf != nullptr && *zf != gen) {
+    // r0 = b - A x0 with x0 all zeros (copy_flag_kernel saw no nonzero) and A finite (the host
+    // checked at upload): every product is +-0, every row sum +0 (0.0 + (-0.0) = +0.0), so
+    // r = b - 0.0 = b bit for bit; the same walk and row -> thread mapping as below, so the
+    // ||r||^2 partials are the full path's too.  Skips the matrix and the gathers.
+    for (int blk = b0; blk < b1; blk += bs) {
+      const int2 m0 = meta[blk * ms];
+      const int2 m1 = meta[blk * ms + 1];
+      if (m1.y - m0.y > CAP) {  // one long row: thread 0, as the full path (block_sum of zeros = +0)
+        if (threadIdx.x == 0) {
+          const double t = aux1[m0.x] - 0.0;
+          y1[m0.x] = t;
+          pt1 += t * t;
+        }
+        continue;
+      }
+      const int r = m0.x + threadIdx.x;
+      if (r < m1.x) {
+        const double t = aux1[r] - 0.0;
+        y1[r] = t;
+        pt1 += t * t;
+      }
+    }
+    const double tot1 = block_sum(pt1, s_wave);
+    if (threadIdx.x == 0) part1[blockIdx.x] = tot1;
+    return;
+  }
   // one block: cur's products and row sums, nxt (block nb) loaded meanwhile.  The loop below
   // alternates two stages (no stage copy at the back edge: the copy's register moves spilled)
   auto step = [&](PipeStage<CAP>& cur, PipeStage<CAP>& nxt, int blk) __attribute__((always_inline)) {
@@ -559,15 +587,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
 
 hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const double* aux1, double* y1,
                             double* part1, const double* x2, const double* aux2, double* y2, double* part2,
-                            int grid, hipStream_t s, const LaunchEv* ev) {
+                            int grid, hipStream_t s, const LaunchEv* ev, const unsigned* zf, unsigned gen) {
   dim3 g(grid), b(kBlock);
+  if (mode == kEpiR0 && zf != nullptr) {  // r0 with the x0 = 0 test
+    if (A.col16 != nullptr)
+      launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,
+               A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, zf, gen);
+    else
+      launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,
+               A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, zf, gen);
+    return hipGetLastError();
+  }
 #define SPIS_PIPE(M)                                                                                            \
   if (A.col16 != nullptr)                                                                                       \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
-             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base);               \
+             A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base,                  \
+             static_cast<const unsigned*>(nullptr), 0u);                                                       \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
-             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr)
+             A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr,                                \
+             static_cast<const unsigned*>(nullptr), 0u)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
@@ -627,9 +666,10 @@ int blas_grid(int64_t n, bool fixed) {
 }
 
 hipError_t launch_spmv(const CsrView& A, int epi, const double* x, double* y, const double* aux,
-                       double* partials, int grid, hipStream_t s, const LaunchEv* ev) {
+                       double* partials, int grid, hipStream_t s, const LaunchEv* ev, const unsigned* zf,
+                       unsigned gen) {
   if (A.blk_meta != nullptr)
-    return launch_spmv_pipe(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev);
+    return launch_spmv_pipe(A, epi, x, aux, y, partials, nullptr, nullptr, nullptr, nullptr, grid, s, ev, zf, gen);
   dim3 g(grid), b(kBlock);
   switch (epi) {
     case kEpiPlain:
@@ -3008,6 +3048,29 @@ hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s) {
   if (g > 4 * kRedGrid) g = 4 * kRedGrid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(kBlock), 0, s, n, x, y);
+  return hipGetLastError();
+}
+
+// y = x, and *flag = gen if any x[e] != 0 (a plain store from every lane that sees one: they all
+// write the same value).  The solver's x0 copy: with flag != gen afterwards x0 is all zeros and the
+// r0 SpMV skips the matrix (spmv_pipe_kernel MODE 3, zf)
+__global__ __launch_bounds__(kBlock) void copy_flag_kernel(int64_t n, const double* __restrict__ x,
+                                                           double* __restrict__ y, unsigned* flag, unsigned gen) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  bool nz = false;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
+    const double v = x[e];
+    y[e] = v;
+    nz = nz || v != 0.0;
+  }
+  if (nz) *flag = gen;
+}
+
+hipError_t launch_copy_flag(int64_t n, const double* x, double* y, unsigned* flag, unsigned gen, hipStream_t s) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  if (g > 4 * kRedGrid) g = 4 * kRedGrid;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(copy_flag_kernel, dim3(g), dim3(kBlock), 0, s, n, x, y, flag, gen);
   return hipGetLastError();
 }
 

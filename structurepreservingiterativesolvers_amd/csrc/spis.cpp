@@ -172,6 +172,8 @@ struct spis_context {
   unsigned* chain_epoch = nullptr;           // tag base, advanced by each chain
   unsigned* chain_err = nullptr;             // pinned, device-mapped: a chain exchange timed out
   unsigned* chain_err_dev = nullptr;
+  unsigned* x0_flag = nullptr;  // device word: the solve's generation when its x0 has a nonzero entry
+  unsigned x0_gen = 0;
   bool icwy_spin_off = false;  // a one-reduce hand-off (K2w fold / K2s) timed out: finalize launches
   std::vector<hipEvent_t> ev_free;
   struct Pending { int kind; hipEvent_t a, b; };
@@ -203,6 +205,7 @@ struct spis_matrix {
   int4* base_nat_d = nullptr;     // its per-block bases, natural block order
   int4* base_slab_d = nullptr;    // the same in slab order
   bool all_zero = false;
+  bool all_finite = true;  // every stored value finite (A x0 with x0 = 0 is then exactly 0)
   GramSplit gram_rows{};  // K7m's XCD-group row ranges (natural row order)
   // K7t's slot table (symmetric matrices; sym_state -1 unknown, 0 not symmetric, 1 built)
   int sym_state = -1;
@@ -659,6 +662,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     (void)hipFree(c->gemv_flag);
     (void)hipFree(c->chain_epoch);
     if (c->chain_err) (void)hipHostFree(c->chain_err);
+    if (c->x0_flag) (void)hipFree(c->x0_flag);
     if (c->gram_part) (void)hipFree(c->gram_part);
     if (c->gram_G) (void)hipFree(c->gram_G);
     if (c->cg_part) (void)hipFree(c->cg_part);
@@ -937,11 +941,12 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
                   (long long)(n_rows + n_ghost));
     for (int64_t r = 0; r < n_rows; ++r)
       if (indptr[r + 1] < indptr[r]) return fail(SPIS_ERR_ARG, "indptr not monotone at row %lld", (long long)r);
-    bool all_zero = true;
+    bool all_zero = true, all_finite = true;
     for (int64_t i = 0; i < nnz; ++i) {
       if (indices[i] < 0 || indices[i] >= n_cols)
         return fail(SPIS_ERR_ARG, "column index %d out of range at %lld", indices[i], (long long)i);
       if (data[i] != 0.0) all_zero = false;
+      if (!std::isfinite(data[i])) all_finite = false;
     }
     HIP_TRY(hipSetDevice(c->device));
     std::unique_ptr<spis_matrix> M(new spis_matrix());
@@ -952,6 +957,7 @@ extern "C" int spis_csr_upload(spis_context* c, int64_t n_rows, int64_t n_cols, 
     M->n_cols = n_cols;
     M->nnz = nnz;
     M->all_zero = all_zero;
+    M->all_finite = all_finite;
     gram_split(n_rows, indptr, &M->gram_rows);
     std::vector<int32_t> blk;
     build_row_blocks(n_rows, indptr, blk, M->n_long);
@@ -2763,7 +2769,21 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // r0 = b - A x0 ; beta = ||r0|| ; q0 = r0 / beta      (solvers.py:167-177)
     // copies: x0 into the workspace (zero padding for K2q's pairs, one buffer for every x0 use);
     // x0 into a halo'd buffer only when the SpMV reads ghost entries
-    HIP_TRY(launch_copy(n, x0, ws->x0, s));
+    // x0 = 0 (the copy sees no nonzero) on a finite single-rank matrix: the r0 SpMV skips the
+    // matrix, r0 = b bit for bit (spmv_pipe_kernel MODE 3)
+    // (SPIS_X0_ZERO_TEST=0: always the full SpMV, the A/B of test_x0_zero_fast_path_bit_identical)
+    const bool x0_test = !c->dist_on() && A->n_ghost == 0 && A->all_finite && A->dual_view().blk_meta != nullptr &&
+                         (std::getenv("SPIS_X0_ZERO_TEST") == nullptr || std::atoi(std::getenv("SPIS_X0_ZERO_TEST")) != 0);
+    if (x0_test) {
+      if (!c->x0_flag) {
+        HIP_TRY(hipMalloc(&c->x0_flag, sizeof(unsigned)));
+        HIP_TRY(hipMemsetAsync(c->x0_flag, 0, sizeof(unsigned), s));
+      }
+      if (++c->x0_gen == 0) ++c->x0_gen;  // a stale word never equals a new generation
+      HIP_TRY(launch_copy_flag(n, x0, ws->x0, c->x0_flag, c->x0_gen, s));
+    } else {
+      HIP_TRY(launch_copy(n, x0, ws->x0, s));
+    }
     const double* xr0 = ws->x0;
     if (A->n_ghost > 0 || c->dist_on()) {
       HIP_TRY(launch_copy(n, x0, ws->xj, s));
@@ -2772,7 +2792,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       // x0's ghost rows for the update GEMV over n_gx() rows
       if (S.n_gx() > n) HIP_TRY(launch_copy(S.n_gx() - n, ws->xj + n, ws->x0 + n, s));
     }
-    HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s));
+    HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s, nullptr,
+                        x0_test ? c->x0_flag : nullptr, c->x0_gen));
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
     // beta: the normalize kernel's one system-scope store into pinned memory; the host spins

@@ -1432,6 +1432,34 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
         assert np.array_equal(xa, xb) and np.array_equal(ra, rb) and np.array_equal(Qa, Qb)
 
 
+@pytest.mark.parametrize("x0_kind", ["zeros", "negzeros", "nonzero"])
+def test_x0_zero_fast_path_bit_identical(spis, x0_kind, monkeypatch):
+    """r0 = b - A x0 with x0 all zeros skips the matrix (spis.cpp: the x0 copy flags a nonzero entry,
+    spmv_pipe_kernel MODE 3 reads the flag): on a finite matrix every product is +-0 and every row sum
+    +0, so r0 = b bit for bit and the ||r0||^2 partials are the full path's.  The whole constrained
+    solve (C3's shape at M = 30) bitwise equal with the test on and off (SPIS_X0_ZERO_TEST=0), for
+    +0 and -0 zeros and for a nonzero x0 (the flag set: the full SpMV either way); and x[0] = b."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    n = dic["A"].shape[0]
+    x0 = {"zeros": np.zeros(n), "negzeros": -np.zeros(n),
+          "nonzero": 1e-3 * np.random.default_rng(5).standard_normal(n)}[x0_kind]
+    cons = swe_ls.constraints(dic, np.zeros(n))
+    runs = []
+    for flag in ("1", "0", "1"):
+        monkeypatch.setenv("SPIS_X0_ZERO_TEST", flag)
+        x, d = solvers.cgmres(dic["A"], dic["b"], x0, 20, tol=1e-19, conlist=cons)
+        runs.append((np.asarray(x), np.asarray(d["res"]), np.asarray(d["x"][0]), list(d["x"].trace)))
+    for r in runs[1:]:
+        assert np.array_equal(r[0], runs[0][0]) and np.array_equal(r[1], runs[0][1])
+        assert np.array_equal(r[2], runs[0][2]) and r[3] == runs[0][3]
+    if x0_kind != "nonzero":
+        assert np.array_equal(runs[0][2], dic["b"])  # x[0] = r0 = b
+
+
 @pytest.mark.parametrize("n", [65_536, 100_002, 196_608, 1001, 300_006, 393_216])
 def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     """K2s (small N, one GPU: K2w's dots, coefficients, update with the fused GEMV, norm and
