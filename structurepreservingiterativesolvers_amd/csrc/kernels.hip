@@ -3218,8 +3218,9 @@ __global__ __launch_bounds__(kBlock) void gram_partial_kernel(int64_t n, int nu,
 // out[j] = sum over rows of part[row][j] (row-major rows x npairs), one workgroup per output:
 // strided per-thread sums then block_sum's fixed tree (deterministic); optional symmetrize:
 // out[a np1 + b] += (the same sum of part[.][b np1 + a]) for the np1 x np1 prefix (K7t's H + H^T)
+// (pin: out is host memory a host thread polls, system-scope stores, each value its own flag)
 __global__ __launch_bounds__(kBlock) void reduce_cols_kernel(int npairs, int rows, const double* __restrict__ part,
-                                                             double* __restrict__ out, int sym_np1) {
+                                                             double* __restrict__ out, int sym_np1, bool pin) {
   __shared__ double s_wave[4];
   const int j = blockIdx.x;
   double s = 0.0;
@@ -3232,7 +3233,12 @@ __global__ __launch_bounds__(kBlock) void reduce_cols_kernel(int npairs, int row
     for (int r = threadIdx.x; r < rows; r += kBlock) st += part[static_cast<int64_t>(r) * npairs + jt];
     tot = tot + block_sum(st, s_wave);
   }
-  if (threadIdx.x == 0) out[j] = tot;
+  if (threadIdx.x == 0) {
+    if (pin)
+      pin_store(out + j, tot);
+    else
+      out[j] = tot;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void gram_reduce_kernel(int npairs, int grid,
@@ -3551,7 +3557,7 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 
 hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                       double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
-                                      hipStream_t s) {
+                                      hipStream_t s, bool pin) {
   const int np1 = p + 1;
   if (np1 > 32 || nvv < 0 || nvv > 4 || nvv * np1 > kBlock) return hipErrorInvalidValue;
   const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -3564,7 +3570,7 @@ hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nvv == 0) return e;
   const int npairs = nvv * np1;
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, g, vpart, Gv, 0);
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, g, vpart, Gv, 0, pin);
   return hipGetLastError();
 }
 
@@ -3802,7 +3808,7 @@ hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, con
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int npairs = np1 * np1 + nvv * np1;
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, grid, partials, G, 0);
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, grid, partials, G, 0, false);
   return hipGetLastError();
 }
 
@@ -3996,7 +4002,7 @@ static int sym_grid() {
 }
 
 hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
-                                      hipStream_t s) {
+                                      hipStream_t s, bool pin) {
   if (np1 > 32) return hipErrorInvalidValue;
   if (T.ns != kSymSlots) return hipErrorInvalidValue;
   const int grid = sym_grid();
@@ -4004,7 +4010,7 @@ hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int np2 = np1 * np1;
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(np2), dim3(kBlock), 0, s, np2, grid, partials, G, np1);
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3(np2), dim3(kBlock), 0, s, np2, grid, partials, G, np1, pin);
   return hipGetLastError();
 }
 

@@ -1564,8 +1564,14 @@ static int ensure_host_buf(double** buf, size_t* len, size_t need) {
 // Enqueues the transpose and every constraint matrix's Gram of one step on stream st, each result
 // copied to dst (layout: con_result_len).  One-time buffers and matrix copies are made first
 // (they may synchronise the main stream, on first use only).
+// a constrained step's reduction results polled in pinned memory: each value its own flag, armed with
+// this sentinel (a signalling NaN no kernel writes) before the launches
+constexpr uint64_t kConSentinel = 0x7FF4DEAD5EC0FFEDull;
+using PollRanges = std::vector<std::pair<size_t, size_t>>;  // (offset, count) in c->con_pinned
+
 static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int64_t n,
-                            int p, const double* Z, int64_t pitch, const double* x0, hipStream_t st, double* dst) {
+                            int p, const double* Z, int64_t pitch, const double* x0, hipStream_t st, double* dst,
+                            PollRanges* poll = nullptr) {
   const int np1 = p + 1;
   const int ut_cols = np1 <= 32 ? 32 : 64;  // Ut is N x np1 row-major: size for this p bucket
   // several GPUs: a constraint matrix's ghost columns read the Ut rows of their owners, received
@@ -1614,6 +1620,28 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   const size_t voff = static_cast<size_t>(m) * np1 * np1;
   const int nv = static_cast<int>(vlist.size());
   bool v_done = nv == 0;
+  bool all_sym = tsym;
+  for (const Launch& L : plan) all_sym = all_sym && L.sym;
+  if (poll != nullptr && all_sym && !c->dist_on()) {
+    // one GPU, K7t only: the reductions store every value into dst (pinned) themselves, system
+    // scope, each its own flag (the host polls them, con_step_wait): no copy packets and no
+    // system-scope event release in front of the host's KKT solve
+    poll->clear();
+    if (nv > 0) poll->push_back({voff, static_cast<size_t>(nv) * np1});
+    for (const Launch& L : plan) poll->push_back({static_cast<size_t>(L.ci) * np1 * np1, static_cast<size_t>(np1) * np1});
+    for (const auto& rg : *poll)
+      for (size_t q = 0; q < rg.second; ++q) reinterpret_cast<volatile uint64_t*>(dst)[rg.first + q] = kConSentinel;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, dst, 0));
+    double* dstd = static_cast<double*>(dp);
+    if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
+    HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart, dstd + voff, st,
+                                       true));
+    for (const Launch& L : plan)
+      HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, dstd + static_cast<size_t>(L.ci) * np1 * np1,
+                                         st, true));
+    return SPIS_OK;
+  }
   if (tsym) {  // Ut + the linear terms in one pass over the basis
     if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
     HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart,
@@ -1777,7 +1805,6 @@ static int constraint_terms_all(spis_context* c, spis_workspace* ws, int m, cons
 // The first constrained step takes the full reduction (transpose + K7t) and seeds the caches,
 // unless its p is small enough that columns 0 .. p-1 from scratch cost less (kIncScratch).
 constexpr int kIncScratch = 8;
-constexpr uint64_t kConSentinel = 0x7FF4DEAD5EC0FFEDull;  // a signalling NaN no kernel writes
 
 // one value an increment step computes: G(a, b) = z_a . M z_b of constraint ci (m), else its
 // v . z_a (gv[a]); a, b = k stand for x0
@@ -1806,7 +1833,7 @@ struct ConStep {
   const double* gx_y = nullptr;
   double* gx_out = nullptr;
   bool gx_done = false;
-  size_t polled = 0;  // > 0: the values arrive as polled pinned slots (no ev_gram to wait for)
+  PollRanges poll;  // non-empty: the values arrive as polled pinned slots (no ev_gram to wait for)
 };
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
@@ -1941,7 +1968,7 @@ static int con_inc_enqueue(spis_context* c, spis_workspace* ws, const spis_const
     HIP_TRY(hipHostGetDevicePointer(&dp, c->con_pinned, 0));
     HIP_TRY(launch_cgs_finalize(c->inc_part, g, static_cast<int>(total), static_cast<double*>(dp), nullptr, nullptr, st,
                                 0, true));
-    cs.polled = total;
+    cs.poll.assign(1, {size_t(0), total});
     return SPIS_OK;
   }
   HIP_TRY(launch_cgs_finalize(c->inc_part, g, static_cast<int>(total), c->inc_res, nullptr, nullptr, st));
@@ -2010,10 +2037,11 @@ static void con_terms_from_cache(const spis_workspace* ws, int m, const spis_con
 
 // the host's wait for a step's reduction: its polled pinned slots, else ev_gram (recorded behind it)
 static int con_step_wait(spis_context* c, const ConStep& cs) {
-  if (cs.polled == 0) return wait_event(c->ev_gram);
+  if (cs.poll.empty()) return wait_event(c->ev_gram);
   const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(c->con_pinned);
   const double t0 = now_s();
-  for (size_t i = 0; i < cs.polled; ++i)
+  for (const auto& rg : cs.poll)
+    for (size_t i = rg.first; i < rg.first + rg.second; ++i)
     for (unsigned spin = 0; __atomic_load_n(const_cast<const uint64_t*>(w + i), __ATOMIC_ACQUIRE) == kConSentinel;
          ++spin) {
       if ((spin & 4095) == 4095 && now_s() - t0 > 0.02) {  // a failed stream never writes them
@@ -2036,7 +2064,7 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   cs->m = m;
   cs->inc = false;
   cs->gx_done = false;
-  cs->polled = 0;
+  cs->poll.clear();
   cs->st = c->stream;
   cs->from.assign(m, 0);
   if (con_inc_eligible(c, ws, m, cons, p)) {
@@ -2055,7 +2083,7 @@ static int con_step_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     return con_inc_enqueue(c, ws, cons, n, Z, pitch, x0, *cs);
   }
   ST_TRY(ensure_host_buf(&c->con_pinned, &c->con_pinned_len, con_result_len(m, p)));
-  return con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned);
+  return con_gram_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, c->stream, c->con_pinned, &cs->poll);
 }
 
 // after the wait: the step's terms (and the caches brought up to date)
@@ -2076,7 +2104,7 @@ static int constraint_terms_fused(spis_context* c, spis_workspace* ws, int m, co
                                   QuadCon* out) {
   ConStep cs;
   ST_TRY(con_step_enqueue(c, ws, m, cons, n, p, Z, pitch, x0, &cs, false));
-  if (cs.polled == 0) HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking
+  if (cs.poll.empty()) HIP_TRY(hipEventRecord(c->ev_gram, c->stream));  // spin on it: a blocking
   ST_TRY(con_step_wait(c, cs));                                         // synchronize wakes up late
   con_step_assemble(c, ws, cons, cs, out);
   return SPIS_OK;
@@ -2296,7 +2324,10 @@ struct Solver {
     *reinterpret_cast<volatile uint64_t*>(c->pinned + roff(j)) = kHSentinel;
   }
 
-  double* xbuf(int j) const { return (j & 1) ? ws->xj2 : ws->xj; }
+  double* xbuf(int j) const { return (j == k - 1 && x_last) ? x_last : (j & 1) ? ws->xj2 : ws->xj; }
+  // one GPU: x_{k-1} (only ever a GEMV's output, n rows) goes straight to the caller's x[-1] buffer,
+  // which its residual then reads: no copy at the solve's end
+  double* x_last = nullptr;
   int launch_dual(int j, int ja, const double* bvec, const LaunchEv* le) {
     HIP_TRY(launch_spmv_dual(A->dual_view(), xbuf(j), bvec, c->partR, Zv(ja), ws->w, Qv(0), c->partA, gs, c->stream,
                              le));
@@ -2758,6 +2789,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     Solver S{c, A, o, ws, b, n, k, spmv_grid(A->dual_view(), fixed_grid(c)), blas_grid(n, fixed_grid(c)), {}, {}};
     ST_TRY(ensure_pinned(c, S.pinned_need()));
     hipStream_t s = c->stream;
+    if (!c->dist_on() && out->x_final_dev && out->x_final_dev != b && out->x_final_dev != x0)
+      S.x_last = out->x_final_dev;  // (a caller buffer aliasing b or x0 keeps the copy at the end)
     double* stamps = out->stamps_host;  // [0,k) iter start, [k,2k) iter end, [2k,3k) con start, [3k,4k) con end
     const double t_start = now_s();
     for (int i = 0; i < k; ++i) {
@@ -2869,7 +2902,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       ST_TRY(con_step_enqueue(c, ws, m_of(jc), o->constraints, n, jc + 1, ws->Zb, ws->pitch, ws->x0, &gram_step,
                               side));
       gram_step.gx_p = 0;  // a GEMV request holds for one enqueue
-      if (gram_step.polled == 0) HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
+      if (gram_step.poll.empty()) HIP_TRY(hipEventRecord(c->ev_gram, gram_step.st));
       gram_queued = jc;
       return SPIS_OK;
     };
@@ -3110,7 +3143,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // Arnoldi step, which never touches xj / r0), then one synchronisation
     if (out->x_final_dev) {
       if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
-      else HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));
+      else if (!have_x || S.xbuf(last_x) != out->x_final_dev)
+        HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));
     }
     if (deferred >= 0) {  // U_{k-2}'s residual, on its own if the run ended before U_{k-1}
       if (!deferred_queued) ST_TRY(S.enqueue_residual(deferred));
