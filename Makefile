@@ -54,3 +54,10 @@ tools/chainbench: tools/chainbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<
 tools/kbench: tools/kbench.hip $(SRC)/kernels.hip $(SRC)/kernels.h $(SRC)/slab_order.h $(SRC)/col16.h
 	$(HIPCC) $(HIPFLAGS) $(CXXFLAGS) -o $@ $<
+
+# tools/host_phases.py: spis_solve with its host phase marks compiled in (not the product library)
+tools/libspis_phases.so: $(SRC)/spis.cpp $(OBJS)
+	$(HIPCC) $(CXXFLAGS) -DSPIS_HOST_PHASES -x hip --offload-arch=$(ARCH) -c $< -o build/spis_phases.o
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(filter-out build/spis.o,$(OBJS)) build/spis_phases.o -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
+
+phases: tools/libspis_phases.so

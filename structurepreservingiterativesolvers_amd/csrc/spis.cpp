@@ -2748,9 +2748,31 @@ struct Solver {
 
 }  // namespace
 
+// tools/host_phases.py: a build with -DSPIS_HOST_PHASES (make phases) prints the mean host time
+// of spis_solve's phases every 40 calls (the product build compiles the marks away)
+#ifdef SPIS_HOST_PHASES
+static double g_phase_t[12], g_phase_acc[12];
+static int g_phase_calls = 0;
+#define PHASE(i) (g_phase_t[i] = now_s())
+extern "C" double spis_debug_phase_t0() { return g_phase_t[0]; }  // the last call's entry time
+static void phase_report(int np) {  // the first 10 calls (allocations, warm-up) are not counted
+  if (++g_phase_calls <= 10) return;
+  for (int i = 1; i < np; ++i) g_phase_acc[i] += g_phase_t[i] - g_phase_t[i - 1];
+  if (g_phase_calls % 40 == 10) {
+    std::fprintf(stderr, "spis_solve phases (us):");
+    for (int i = 1; i < np; ++i) std::fprintf(stderr, " %d:%.1f", i, 1e6 * g_phase_acc[i] / (g_phase_calls - 10));
+    std::fprintf(stderr, "\n");
+  }
+}
+#else
+#define PHASE(i) ((void)0)
+static void phase_report(int) {}
+#endif
+
 extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, const double* x0,
                           const spis_solve_opts* o, spis_solve_out* out, spis_workspace** ws_out) {
   ABI_GUARD({
+    PHASE(0);
     if (!c || !A || !b || !x0 || !o || !out || !ws_out) return fail(SPIS_ERR_ARG, "null argument");
     const int k = o->k;
     if (k < 1 || k > kMaxK) return fail(SPIS_ERR_ARG, "k=%d out of range [1,%d]", k, kMaxK);
@@ -2770,9 +2792,11 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (o->constraints[i].M && o->constraints[i].M->n_rows != n)
         return fail(SPIS_ERR_ARG, "constraint %d matrix size mismatch", i);
     HIP_TRY(hipSetDevice(c->device));
+    PHASE(1);
     const bool sep_z = o->pre_matrix != nullptr || o->pre_fn != nullptr || o->pre_ilu != nullptr;
     spis_workspace* ws = nullptr;
     ST_TRY(get_workspace(c, n, n + A->n_ghost, k, sep_z, &ws));
+    PHASE(2);
     std::unique_ptr<spis_workspace, int (*)(spis_workspace*)> guard(ws, spis_workspace_release);
     ws->steps = 0;
     ws->n_iter_y = 0;
@@ -2783,6 +2807,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ws->last_con_p = 0;
     const bool use_cb = o->conls_fn != nullptr;
     if (!use_cb && o->n_constraints > 0) ST_TRY(ensure_con_cache(ws, o->n_constraints, o->constraints));
+    PHASE(3);
 
     // every solver SpMV runs on the kDualCap row blocks, so the fused and the single launches
     // group their partial sums identically (bit-identical results either way)
@@ -2793,6 +2818,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       S.x_last = out->x_final_dev;  // (a caller buffer aliasing b or x0 keeps the copy at the end)
     double* stamps = out->stamps_host;  // [0,k) iter start, [k,2k) iter end, [2k,3k) con start, [3k,4k) con end
     const double t_start = now_s();
+    PHASE(4);
     for (int i = 0; i < k; ++i) {
       out->branch_host[i] = SPIS_BRANCH_UNCON;
       out->events_host[i] = 0;
@@ -2855,6 +2881,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       ST_TRY(wait_event(c->ev_gram));
     }
     const double beta = *beta_slot;
+    PHASE(5);
     int n_res = 0;
     out->res_host[n_res++] = beta;
     int steps = 0;
@@ -3139,15 +3166,25 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       last_x = j;
       pending = j;
     }
+    PHASE(6);
+    // the run reached its last iteration, whose residual is the last work queued (below)
+    bool tail_launch = pending != k - 1;
     // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
     // Arnoldi step, which never touches xj / r0), then one synchronisation
     if (out->x_final_dev) {
-      if (ws->broke_at_start) HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
-      else if (!have_x || S.xbuf(last_x) != out->x_final_dev)
+      if (ws->broke_at_start) {
+        HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
+        tail_launch = true;
+      } else if (!have_x || S.xbuf(last_x) != out->x_final_dev) {
         HIP_TRY(launch_copy(n, have_x ? S.xbuf(last_x) : ws->r0, out->x_final_dev, s));
+        tail_launch = true;
+      }
     }
     if (deferred >= 0) {  // U_{k-2}'s residual, on its own if the run ended before U_{k-1}
-      if (!deferred_queued) ST_TRY(S.enqueue_residual(deferred));
+      if (!deferred_queued) {
+        ST_TRY(S.enqueue_residual(deferred));
+        tail_launch = true;
+      }
       ST_TRY(S.wait_update(deferred));
       out->res_host[n_res++] = S.residual(deferred);
       if (stamps) stamps[k + deferred] = now_s();
@@ -3157,10 +3194,20 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       out->res_host[n_res++] = S.residual(pending);
       if (stamps) stamps[k + pending] = now_s();
     }
+    PHASE(7);
     // speculative Arnoldi steps finish before x / ws are used
-    // (event spin: a blocking synchronize wakes the host up tens of us late, per solve)
-    HIP_TRY(hipEventRecord(c->ev_gram, s));
-    ST_TRY(wait_event(c->ev_gram));
+    // (event spin: a blocking synchronize wakes the host up tens of us late, per solve).
+    // Not needed when the residual the host has just read was published by the last kernel on
+    // the stream and the side stream is idle: every kernel before it has completed (in-order
+    // stream), so no H column or residual of this solve can still land in a pinned slot the next
+    // solve arms, and everything the caller may read later is stream-ordered (C3: 12 us of GPU
+    // idle per solve)
+    const bool drained = !tail_launch && !c->dist_on() && !o->pre_ilu && hipStreamQuery(c->stream2) == hipSuccess;
+    if (!drained) {
+      HIP_TRY(hipEventRecord(c->ev_gram, s));
+      ST_TRY(wait_event(c->ev_gram));
+    }
+    PHASE(8);
     prof_drain(c);
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
     if (const unsigned ce = *reinterpret_cast<volatile unsigned*>(c->chain_err)) {  // never on a healthy device
@@ -3183,6 +3230,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     out->steps = steps;
     out->n_res = n_res;
     *ws_out = guard.release();
+    PHASE(9);
+    phase_report(10);
     return SPIS_OK;
   })
 }

@@ -1,0 +1,72 @@
+"""GPU: the host time of a C3 solve call as the bench makes it (device matrix, vectors and
+constraints resident), split into the Python wrapper's phases (solvers._CHECKPOINTS) and
+spis_solve's own (a library built with -DSPIS_HOST_PHASES: `make phases`).
+
+    SPIS_LIBRARY=tools/libspis_phases.so python tools/host_phases.py [solves]
+"""
+import argparse
+import gc
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from structurepreservingiterativesolvers_amd import solvers  # noqa: E402
+from structurepreservingiterativesolvers_amd.device import (DeviceVector, device_constraints,  # noqa: E402
+                                                            device_matrix, get_context)
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 80
+wl = bench.build_workload(argparse.Namespace(config="c3", M=None, cycles=10))
+ctx = get_context(0)
+Ad = device_matrix(wl["A"], ctx=ctx)
+bd = DeviceVector.from_host(wl["b"], ctx=ctx)
+x0d = DeviceVector.from_host(np.zeros(Ad.shape[0]), ctx=ctx)
+conlist = device_constraints(wl["conlist"], ctx=ctx)
+
+
+def solve():
+    return solvers.cgmres(Ad, bd, x0d, 30, tol=1e-19, conlist=conlist)
+
+
+for _ in range(5):
+    solve()
+gc.collect()
+gc.freeze()
+import ctypes as C  # noqa: E402
+
+t0_fn = getattr(ctx.L, "spis_debug_phase_t0", None)
+if t0_fn is not None:
+    t0_fn.restype = C.c_double
+    t0_fn.argtypes = []
+solvers._CHECKPOINTS = cps = []
+marks = []
+entry = []
+for _ in range(reps):
+    t = time.perf_counter()
+    _, d = solve()
+    marks.append((t, time.perf_counter(), d["x"].stamps[4 * 30], d["x"].stamps[4 * 30 + 1]))
+    entry.append(t0_fn() if t0_fn is not None else np.nan)
+solvers._CHECKPOINTS = None
+ph = np.array(cps).reshape(reps, 5)
+m = np.array(marks)
+print("per call %.1f us, between the C stamps %.1f us" % (1e6 * np.mean(m[:, 1] - m[:, 0]),
+                                                         1e6 * np.mean(m[:, 3] - m[:, 2])))
+print("cgmres entry -> _run entry %.1f us" % (1e6 * np.mean(ph[:, 0] - m[:, 0])))
+for i, name in enumerate(["setup (matrix, vectors, constraints, opts)", "buffers + scratch", "spis_solve call",
+                          "results + IterateList"]):
+    print("%-44s %.1f us" % (name, 1e6 * np.mean(ph[:, i + 1] - ph[:, i])))
+print("spis_solve call: entry -> t_start %.1f us, t_end -> return %.1f us" % (
+    1e6 * np.mean(m[:, 2] - ph[:, 2]), 1e6 * np.mean(ph[:, 3] - m[:, 3])))
+e = np.array(entry)
+print("python -> C entry %.1f us, C entry -> t_start %.1f us" % (1e6 * np.mean(e - ph[:, 2]), 1e6 * np.mean(m[:, 2] - e)))
+# the ctypes call alone: spis_solve with a null context returns at its argument check
+opts, out, ws = solvers._lib.SolveOpts(), solvers._lib.SolveOut(), C.c_void_p()
+t = time.perf_counter()
+for _ in range(2000):
+    ctx.L.spis_solve(None, None, C.c_void_p(5), C.c_void_p(6), C.byref(opts), C.byref(out), C.byref(ws))
+print("null-context spis_solve call %.2f us" % (1e6 * (time.perf_counter() - t) / 2000))
+print("_run return -> cgmres return + assignment %.1f us" % (1e6 * np.mean(m[:, 1] - ph[:, 4])), flush=True)
