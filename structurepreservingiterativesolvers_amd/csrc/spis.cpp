@@ -2751,10 +2751,11 @@ struct Solver {
 // tools/host_phases.py: a build with -DSPIS_HOST_PHASES (make phases) prints the mean host time
 // of spis_solve's phases every 40 calls (the product build compiles the marks away)
 #ifdef SPIS_HOST_PHASES
-static double g_phase_t[12], g_phase_acc[12];
+static double g_phase_t[20], g_phase_acc[20];
 static int g_phase_calls = 0;
 #define PHASE(i) (g_phase_t[i] = now_s())
-extern "C" double spis_debug_phase_t0() { return g_phase_t[0]; }  // the last call's entry time
+#define PHASE_IF(cond, i) ((cond) ? (void)(g_phase_t[i] = now_s()) : (void)0)
+extern "C" double spis_debug_phase_t(int i) { return g_phase_t[i]; }  // the last call's marks
 static void phase_report(int np) {  // the first 10 calls (allocations, warm-up) are not counted
   if (++g_phase_calls <= 10) return;
   for (int i = 1; i < np; ++i) g_phase_acc[i] += g_phase_t[i] - g_phase_t[i - 1];
@@ -2766,6 +2767,7 @@ static void phase_report(int np) {  // the first 10 calls (allocations, warm-up)
 }
 #else
 #define PHASE(i) ((void)0)
+#define PHASE_IF(cond, i) ((void)0)
 static void phase_report(int) {}
 #endif
 
@@ -2938,6 +2940,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (L) {
         bool ok = false;
         ST_TRY(S.wait_hcol(j, &ok));
+        PHASE_IF(j == k - 1, 10);
         if (!ok) {  // the chain failed (c->chain_err): reported at the end of the solve
           (void)hipStreamSynchronize(s);
           break;
@@ -2976,8 +2979,11 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       if (L && gram_queued == j && safety != kSafetyTrue && !o->timing && spec_kkt != j) {
         const double* hp = c->pinned + S.hoff(j);
         if (hp[j + 1] != 0.0) {
+          PHASE_IF(j == k - 1, 11);
           ST_TRY(con_step_wait(c, gram_step));
+          PHASE_IF(j == k - 1, 12);
           con_step_assemble(c, ws, o->constraints, gram_step, cons.data());  // (gram_step.m constraints)
+          PHASE_IF(j == k - 1, 13);
           if (!col_added) {
             for (int i = 0; i < j + 2; ++i) hcol[i] = hp[i];
             qr.add_column(j, hcol.data());
@@ -2987,6 +2993,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           for (int a = 0; a < j; ++a) y0[a] = yk[a];
           spec_kr = kkt_newton(j + 1, qr.R(), qr.ld(), qr.g(), gram_step.m, cons.data(), y0.data(), ycon.data());
           spec_kkt = j;
+          PHASE_IF(j == k - 1, 14);
         }
       }
       ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : (deferred == j - 1 ? SPIS_OK : S.wait_update(j - 1)));
@@ -3134,7 +3141,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         }
         // x_j: from c_{j+1} (fused), else a GEMV beside c_{j+1} on the side stream, or after it
         // on the main stream when c_{j+1} computed x_j from the speculative unconstrained y_j
+        PHASE_IF(j == k - 1, 15);
         if (need_gemv && !gemv_done) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));
+        PHASE_IF(j == k - 1, 16);
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
           ST_TRY(S.enqueue_dual(j, j + 2));

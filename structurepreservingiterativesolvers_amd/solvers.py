@@ -152,7 +152,8 @@ def _constraint_desc(const, n, ctx, checks=None):
             vd = device_vector(v, ctx=ctx)
             keep.append(vd)
             vh = vd.ptr
-    c = float(np.asarray(getattr(const, "c", 0.0)))
+    c = getattr(const, "c", 0.0)
+    c = c if type(c) is float else float(np.asarray(c))
     return _lib.ConstraintDesc(Mh, vh, c), keep
 
 
@@ -262,7 +263,7 @@ def _precond_setup(pre, n, ctx, keep, checks=None):
     ``device_ilu`` option decides (single GPU); other objects with ``.solve``, non-sparse ``@``
     operators and host-chosen SuperLU objects go through the host callback (``solvers.py:152-161``)."""
     if pre is None:
-        return None, _lib.PRECOND_FN(), None
+        return None, _NO_PRE, None
     if sps.issparse(pre) and not hasattr(pre, "solve"):
         dm = device_matrix(pre, ctx=ctx, checks=checks)
         keep.append(dm)
@@ -378,7 +379,8 @@ def _as_slsqp(cc):
 # the call
 # ------------------------------------------------------------------------------------------------
 _OUT = threading.local()
-_NO_CONLS = _lib.CONLS_FN()  # the null callback (class-form or no constraints)
+_NO_CONLS = _lib.CONLS_FN()  # the null callbacks (class-form or no constraints; no host preconditioner)
+_NO_PRE = _lib.PRECOND_FN()
 
 
 def _out_buffers(k):

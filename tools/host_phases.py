@@ -33,15 +33,15 @@ def solve():
 
 
 for _ in range(5):
-    solve()
+    _, d = solve()
 gc.collect()
 gc.freeze()
 import ctypes as C  # noqa: E402
 
-t0_fn = getattr(ctx.L, "spis_debug_phase_t0", None)
-if t0_fn is not None:
-    t0_fn.restype = C.c_double
-    t0_fn.argtypes = []
+t_fn = getattr(ctx.L, "spis_debug_phase_t", None)
+if t_fn is not None:
+    t_fn.restype = C.c_double
+    t_fn.argtypes = [C.c_int]
 solvers._CHECKPOINTS = cps = []
 marks = []
 entry = []
@@ -49,7 +49,7 @@ for _ in range(reps):
     t = time.perf_counter()
     _, d = solve()
     marks.append((t, time.perf_counter(), d["x"].stamps[4 * 30], d["x"].stamps[4 * 30 + 1]))
-    entry.append(t0_fn() if t0_fn is not None else np.nan)
+    entry.append([t_fn(i) for i in range(17)] if t_fn is not None else [np.nan] * 17)
 solvers._CHECKPOINTS = None
 ph = np.array(cps).reshape(reps, 5)
 m = np.array(marks)
@@ -61,8 +61,17 @@ for i, name in enumerate(["setup (matrix, vectors, constraints, opts)", "buffers
     print("%-44s %.1f us" % (name, 1e6 * np.mean(ph[:, i + 1] - ph[:, i])))
 print("spis_solve call: entry -> t_start %.1f us, t_end -> return %.1f us" % (
     1e6 * np.mean(m[:, 2] - ph[:, 2]), 1e6 * np.mean(ph[:, 3] - m[:, 3])))
-e = np.array(entry)
+P = np.array(entry)
+e = P[:, 0]
 print("python -> C entry %.1f us, C entry -> t_start %.1f us" % (1e6 * np.mean(e - ph[:, 2]), 1e6 * np.mean(m[:, 2] - e)))
+dP = 1e6 * np.diff(P[:, :10], axis=1)
+print("spis_solve marks, per call (us): mean", np.round(dP.mean(axis=0), 1), "max", np.round(dP.max(axis=0), 1))
+print("t_start - mark 4 (us): mean %.2f" % (1e6 * np.mean(m[:, 2] - P[:, 4])))
+# the last iteration (j = k - 1): H column read (10), KKT block (11 wait start, 12 values in,
+# 13 assembled, 14 KKT solved), the GEMV enqueue (15, 16)
+L10 = 1e6 * np.diff(P[:, 10:17], axis=1)
+print("last iteration, mark 10 -> 16 deltas (us): mean", np.round(L10.mean(axis=0), 1), "median",
+      np.round(np.median(L10, axis=0), 1))
 # the ctypes call alone: spis_solve with a null context returns at its argument check
 opts, out, ws = solvers._lib.SolveOpts(), solvers._lib.SolveOut(), C.c_void_p()
 t = time.perf_counter()
