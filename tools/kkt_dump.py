@@ -1,0 +1,41 @@
+"""GPU: C3's forced last constrained step as the host KKT solve received it (Hessenberg, beta,
+constraint terms, warm start, the device run's y and LS message), saved for CPU profiling of
+kkt_newton (tools/kkt_prof.py).
+
+    python tools/kkt_dump.py OUT.npz
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from structurepreservingiterativesolvers_amd import solvers  # noqa: E402
+from structurepreservingiterativesolvers_amd.device import DeviceVector, device_constraints, device_matrix, get_context  # noqa: E402
+
+out = sys.argv[1]
+wl = bench.build_workload(argparse.Namespace(config="c3", M=None, cycles=1))
+ctx = get_context(0)
+A = device_matrix(wl["A"], ctx=ctx)
+n = wl["A"].shape[0]
+bd = DeviceVector.from_host(wl["b"], ctx=ctx)
+x0d = DeviceVector.from_host(np.zeros(n), ctx=ctx)
+cons = device_constraints(wl["conlist"], ctx=ctx)
+k = 30
+_, d = solvers.cgmres(A, bd, x0d, k, tol=1e-19, conlist=cons)
+xs = d["x"]
+ys = xs.y
+p = k
+H = xs.hessenberg(p)
+terms = [xs.constraint_terms(ci) for ci in range(len(cons))]
+t0 = np.array([t[1] for t in terms])
+t1 = np.stack([t[2] for t in terms])
+t2 = np.stack([t[3] for t in terms])
+y0 = np.zeros(p)
+y0[:p - 1] = ys[p - 2]
+np.savez(out, H=H, beta=xs.beta, term0=t0, term1=t1, term2=t2, y0=y0, y=ys[p - 1],
+         branch=np.array([b for _, b in xs.trace][-1] == "con"), p_terms=np.array([t[0] for t in terms]))
+print("saved", out, "trace tail", xs.trace[-3:], "terms p", [t[0] for t in terms])
