@@ -3344,6 +3344,72 @@ __global__ __launch_bounds__(kBlock) void transpose_basis_kernel(int64_t n, int 
   if (vpart != nullptr && threadIdx.x < nl) vpart[static_cast<int64_t>(blockIdx.x) * nl + threadIdx.x] = lin;
 }
 
+// K7t's transpose (perm order, np1 <= 32, Ut rows of 32 doubles): the same tiles, rows and linear
+// terms as transpose_basis_kernel (bitwise: Ut is a copy, every linear partial sums its tiles' rows
+// in the same order), software-pipelined: the next tile's 16-B loads are issued before this tile's
+// rows are stored (16-B stores), so each block keeps one tile in flight while it writes the previous
+// one (the one-tile-at-a-time form ran 94 us at C3, 504 MB).
+__global__ __launch_bounds__(kBlock) void transpose_basis_pipe_kernel(int64_t n, int p, const double* __restrict__ Z,
+                                                                      int64_t pitch, const double* __restrict__ x0,
+                                                                      double* __restrict__ Ut, int nvv,
+                                                                      const double* __restrict__ v0,
+                                                                      const double* __restrict__ v1,
+                                                                      const double* __restrict__ v2,
+                                                                      const double* __restrict__ v3,
+                                                                      double* __restrict__ vpart) {
+  __shared__ double tile[32 * 65];
+  __shared__ double s_v[4 * 64];
+  const int np1 = p + 1;
+  const double* vc = (threadIdx.x >> 6) == 0 ? v0 : (threadIdx.x >> 6) == 1 ? v1 : (threadIdx.x >> 6) == 2 ? v2 : v3;  // this wave's v (nvv > 0)
+  const int nl = nvv * np1;
+  const int tc = threadIdx.x / np1, ta = threadIdx.x - tc * np1;
+  double lin = 0.0;
+  const int64_t ntiles = (n + 63) / 64;
+  // loader slot q of this thread: vector a = wave + 4 q (wave-uniform), row = lane
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  double nx[8];
+  double nvx = 0.0;
+  auto load = [&](int64_t tb) {
+    const int64_t g = tb * 64 + ln;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int a = wv + 4 * q;
+      const double* src = a < p ? Z + a * pitch : x0;
+      nx[q] = (a < np1 && g < n) ? src[g] : 0.0;
+    }
+    if (nvv > 0) {
+      const int c = threadIdx.x >> 6, r = threadIdx.x & 63;
+      nvx = (c < nvv && tb * 64 + r < n) ? vc[tb * 64 + r] : 0.0;
+    }
+  };
+  int64_t tb = blockIdx.x;
+  if (tb < ntiles) load(tb);
+  for (; tb < ntiles; tb += gridDim.x) {
+    const int64_t r0 = tb * 64;
+    const int rows = static_cast<int>(n - r0 < 64 ? n - r0 : 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tile[(wv + 4 * q) * 65 + ln] = nx[q];
+    if (nvv > 0) s_v[threadIdx.x] = nvx;  // (c < 4: all 256 slots; unused ones never read)
+    __syncthreads();
+    if (tb + gridDim.x < ntiles) load(tb + gridDim.x);
+    double* out = Ut + r0 * 32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // row r, positions (2 m, 2 m + 1) = columns (m, m + 16)
+      const int idx = threadIdx.x + kBlock * q;
+      const int r = idx >> 4, m = idx & 15;
+      if (r < rows) {
+        const double lo = m < np1 ? tile[m * 65 + r] : 0.0;
+        const double hi = m + 16 < np1 ? tile[(m + 16) * 65 + r] : 0.0;
+        *reinterpret_cast<double2*>(out + r * 32 + 2 * m) = make_double2(lo, hi);
+      }
+    }
+    if (threadIdx.x < nl)
+      for (int r = 0; r < rows; ++r) lin += tile[ta * 65 + r] * s_v[tc * 64 + r];
+    __syncthreads();
+  }
+  if (vpart != nullptr && threadIdx.x < nl) vpart[static_cast<int64_t>(blockIdx.x) * nl + threadIdx.x] = lin;
+}
+
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const unsigned long long bits = __double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readlane(static_cast<unsigned>(bits), lane);
@@ -3564,9 +3630,15 @@ hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t
   for (int c = 0; c < nvv; ++c) vv[c] = v[c];
   const int64_t ntiles = (n + 63) / 64;
   const int g = static_cast<int>(ntiles < kTransposeGrid ? (ntiles < 1 ? 1 : ntiles) : kTransposeGrid);
-  hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
-                     static_cast<size_t>(np1) * 65 * sizeof(double) + 4 * 64 * sizeof(double), s, n, p, Z, pitch,
-                     x0, Ut, true, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
+  // SPIS_TRANSPOSE_PIPE=0: the one-tile-at-a-time kernel (A/B; bitwise the same Ut and terms)
+  const char* tp = std::getenv("SPIS_TRANSPOSE_PIPE");
+  if ((tp == nullptr || std::atoi(tp) != 0) && aligned16d(Ut))
+    hipLaunchKernelGGL(transpose_basis_pipe_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock), 0, s, n, p, Z, pitch,
+                       x0, Ut, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
+  else
+    hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
+                       static_cast<size_t>(np1) * 65 * sizeof(double) + 4 * 64 * sizeof(double), s, n, p, Z, pitch,
+                       x0, Ut, true, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nvv == 0) return e;
   const int npairs = nvv * np1;

@@ -733,6 +733,37 @@ def test_incremental_constraint_gram(spis, method, monkeypatch):
             assert abs(val) <= 1e-10 * max(1.0, abs(float(con.c))), val
 
 
+@pytest.mark.parametrize("M", [40, 97])
+def test_pipelined_transpose_bit_identical(spis, M, monkeypatch):
+    """K7t's transpose with the next tile's loads in flight (transpose_basis_pipe_kernel) against the
+    one-tile-at-a-time kernel (SPIS_TRANSPOSE_PIPE=0): Ut is a copy and every linear-term partial
+    sums its tiles' rows in the same order, so the forced constrained step's terms, the branch, the
+    iterates and the residuals are bitwise equal.  swe with mass + energy + the synthetic third
+    constraint (a linear term v); M = 97 gives N = 112,908, not a multiple of the 64-row tile."""
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=M)
+    n = dic["A"].shape[0]
+    x0 = np.zeros(n)
+    cons = swe_ls.constraints(dic, x0)
+    D, c3 = sa.extra_constraint(n, dic["z0"], seed=2)
+    cons.append(swe_ls._Constraint(D, np.random.default_rng(M).standard_normal(n) * 1e-3, c3))
+    runs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("SPIS_TRANSPOSE_PIPE", pipe)
+        x, d = solvers.cgmres(dic["A"], dic["b"], x0, 20, tol=1e-19, conlist=cons)
+        its = d["x"]
+        runs.append((np.asarray(x), np.asarray(d["res"]), list(its.trace),
+                     [its.constraint_terms(ci) for ci in range(len(cons))]))
+    (xa, ra, ta, Ta), (xb, rb, tb, Tb) = runs
+    assert ta == tb and ta[-1][1] in ("con", "fallback")
+    assert np.array_equal(xa, xb) and np.array_equal(ra, rb)
+    for (pa, a0, a1, a2), (pb, b0, b1, b2) in zip(Ta, Tb):
+        assert pa == pb and a0 == b0 and np.array_equal(a1, b1) and np.array_equal(a2, b2)
+
+
 def test_lkdv_vs_oracle_medium(spis):
     import oracle
     from structurepreservingiterativesolvers_amd.lkdv import LinearSolver as lkdv_ls
