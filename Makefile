@@ -32,9 +32,13 @@ build/hash.o: $(SRC)/hash.cpp include/spis.h
 	@mkdir -p build
 	g++ $(CXXFLAGS) -c $< -o $@
 
+# the host least squares on x86-64-v3 (AVX2, FMA) with contraction off: the loops vectorise, every
+# product is rounded then added as written, so results are bitwise the baseline build's
+LSQFLAGS := -march=x86-64-v3 -ffp-contract=off
+
 build/lsq.o: $(SRC)/lsq.cpp $(SRC)/lsq.h include/spis.h
 	@mkdir -p build
-	g++ $(CXXFLAGS) -c $< -o $@
+	g++ $(CXXFLAGS) $(LSQFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
@@ -42,7 +46,7 @@ $(LIB): $(OBJS)
 # host-only build of the small dense LS for CPU unit tests (no HIP runtime needed)
 $(PKG)/liblsq_host.so: $(SRC)/lsq.cpp $(SRC)/lsq.h $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_plan.h $(SRC)/ilu_capi.cpp \
                        $(SRC)/slab_order.h $(SRC)/col16.h $(SRC)/slab_capi.cpp
-	g++ $(CXXFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp $(SRC)/slab_capi.cpp
+	g++ $(CXXFLAGS) $(LSQFLAGS) -shared -o $@ $(SRC)/lsq.cpp $(SRC)/lsq_capi.cpp $(SRC)/ilu_plan.cpp $(SRC)/ilu_capi.cpp $(SRC)/slab_capi.cpp
 
 clean:
 	rm -rf build $(LIB) $(PKG)/liblsq_host.so

@@ -214,10 +214,17 @@ void grad_scale(const KKTState& st, const double* y, const double* lam, const do
 // the explicit null-space basis and the products N'(W N) would cost 2 p^3), whose trailing
 // (p - m) block is the reduced Hessian; Cholesky with a shift of shift_rel times its largest
 // diagonal entry.
-bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, double delta, double shift_rel) {
+bool reduced_pd(const std::vector<double>& W_in, const std::vector<double>& Jt_in, int p, int m, double delta,
+                double shift_rel) {
   if (m >= p) return true;
+  // (scratch reused per thread; every sum below keeps the operand order of the row-by-row form)
+  thread_local std::vector<double> W, Jt, v, u, tw, Lc, tr;
+  W.assign(W_in.begin(), W_in.end());
+  Jt.assign(Jt_in.begin(), Jt_in.end());
+  v.assign(p, 0.0);
+  u.assign(p, 0.0);
+  tw.assign(p, 0.0);
   for (int a = 0; a < p; ++a) W[static_cast<size_t>(a) * p + a] += delta;
-  std::vector<double> v(p), u(p), tw(p);
   for (int i = 0; i < m; ++i) {
     double* col = Jt.data() + static_cast<size_t>(i) * p;
     double nrm = 0.0;
@@ -240,54 +247,79 @@ bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, dou
       for (int a = i; a < p; ++a) x[a] -= t * v[a];
     }
     // W <- H W H with H = I - s2 v v' (W symmetric up to rounding: both sides explicitly)
-    // W <- W H: row a -= s2 (W_a . v) v' (the row sums formed side by side, b ascending)
-    std::fill(tw.begin(), tw.end(), 0.0);
-    for (int b = i; b < p; ++b) {
-      const double vb = v[b];
-      for (int a = 0; a < p; ++a) tw[a] += W[static_cast<size_t>(a) * p + b] * vb;
+    // W <- W H: row a -= s2 (W_a . v) v', each row's sum over b ascending (four rows side by side)
+    int a = 0;
+    for (; a + 3 < p; a += 4) {
+      const double* r0 = W.data() + static_cast<size_t>(a) * p;
+      const double* r1 = r0 + p;
+      const double* r2 = r1 + p;
+      const double* r3 = r2 + p;
+      double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+      for (int b = i; b < p; ++b) {
+        const double vb = v[b];
+        t0 += r0[b] * vb;
+        t1 += r1[b] * vb;
+        t2 += r2[b] * vb;
+        t3 += r3[b] * vb;
+      }
+      tw[a] = t0;
+      tw[a + 1] = t1;
+      tw[a + 2] = t2;
+      tw[a + 3] = t3;
     }
-    for (int a = 0; a < p; ++a) {
-      double* row = W.data() + static_cast<size_t>(a) * p;
-      const double t = tw[a] * s2;
+    for (; a < p; ++a) {
+      const double* r0 = W.data() + static_cast<size_t>(a) * p;
+      double t0 = 0.0;
+      for (int b = i; b < p; ++b) t0 += r0[b] * v[b];
+      tw[a] = t0;
+    }
+    for (int a2 = 0; a2 < p; ++a2) {
+      double* row = W.data() + static_cast<size_t>(a2) * p;
+      const double t = tw[a2] * s2;
       for (int b = i; b < p; ++b) row[b] -= t * v[b];
     }
     std::fill(u.begin(), u.end(), 0.0);  // W <- H W: W -= s2 v (v' W)
-    for (int a = i; a < p; ++a) {
-      const double va = v[a];
-      const double* row = W.data() + static_cast<size_t>(a) * p;
+    for (int a2 = i; a2 < p; ++a2) {
+      const double va = v[a2];
+      const double* row = W.data() + static_cast<size_t>(a2) * p;
       for (int b = 0; b < p; ++b) u[b] += va * row[b];
     }
-    for (int a = i; a < p; ++a) {
-      double* row = W.data() + static_cast<size_t>(a) * p;
-      const double f = s2 * v[a];
+    for (int a2 = i; a2 < p; ++a2) {
+      double* row = W.data() + static_cast<size_t>(a2) * p;
+      const double f = s2 * v[a2];
       for (int b = 0; b < p; ++b) row[b] -= f * u[b];
     }
   }
+  // Cholesky of the trailing (p - m) block with a shift of shift_rel times its largest diagonal
+  // entry, in place, column-major (Lc[c][r] = entry (r, c)): each column's update runs down a
+  // contiguous column, every entry's sum over k ascending as in the row-major form
   const int nz = p - m;
-  std::vector<double> Rm(static_cast<size_t>(nz) * nz);
+  Lc.resize(static_cast<size_t>(nz) * nz);
+  tr.resize(nz);
   double dmax = 0.0;
-  for (int c = 0; c < nz; ++c)
-    for (int d = 0; d < nz; ++d) {
-      const double t = W[static_cast<size_t>(m + c) * p + m + d];
-      Rm[static_cast<size_t>(c) * nz + d] = t;
-      if (c == d) dmax = std::max(dmax, std::fabs(t));
-    }
+  for (int c = 0; c < nz; ++c) {
+    double* lc = Lc.data() + static_cast<size_t>(c) * nz;
+    for (int r = 0; r < nz; ++r) lc[r] = W[static_cast<size_t>(m + r) * p + m + c];
+    dmax = std::max(dmax, std::fabs(lc[c]));
+  }
   const double shift = shift_rel * dmax;
-  std::vector<double> tr(nz);
-  for (int c = 0; c < nz; ++c) {  // in-place Cholesky
-    const double* rc = Rm.data() + static_cast<size_t>(c) * nz;
-    double d = rc[c] + shift;
-    for (int k = 0; k < c; ++k) d -= rc[k] * rc[k];
+  for (int c = 0; c < nz; ++c) {
+    double* lc = Lc.data() + static_cast<size_t>(c) * nz;
+    double d = lc[c] + shift;
+    for (int k = 0; k < c; ++k) {
+      const double ck = Lc[static_cast<size_t>(k) * nz + c];
+      d -= ck * ck;
+    }
     if (!(d > 0.0)) return false;
     d = std::sqrt(d);
-    Rm[static_cast<size_t>(c) * nz + c] = d;
-    // column c below the diagonal: one sum per row r, k ascending, formed side by side
-    for (int r = c + 1; r < nz; ++r) tr[r] = Rm[static_cast<size_t>(r) * nz + c];
+    lc[c] = d;
+    for (int r = c + 1; r < nz; ++r) tr[r] = lc[r];
     for (int k = 0; k < c; ++k) {
-      const double ck = rc[k];
-      for (int r = c + 1; r < nz; ++r) tr[r] -= Rm[static_cast<size_t>(r) * nz + k] * ck;
+      const double* lk = Lc.data() + static_cast<size_t>(k) * nz;
+      const double ck = lk[c];
+      for (int r = c + 1; r < nz; ++r) tr[r] -= lk[r] * ck;
     }
-    for (int r = c + 1; r < nz; ++r) Rm[static_cast<size_t>(r) * nz + c] = tr[r] / d;
+    for (int r = c + 1; r < nz; ++r) lc[r] = tr[r] / d;
   }
   return true;
 }
@@ -296,14 +328,13 @@ bool reduced_pd(std::vector<double> W, std::vector<double> Jt, int p, int m, dou
 void lagrangian_hessian(const KKTState& st, const double* lam, const std::vector<double>& J, std::vector<double>& W,
                         std::vector<double>& Jt) {
   const int p = st.p, m = st.m;
-  W.resize(static_cast<size_t>(p) * p);
+  W.assign(st.B.begin(), st.B.end());  // each entry B + lam_0 S_0 + lam_1 S_1 ..., i ascending
   Jt.resize(static_cast<size_t>(p) * m);
-  for (int a = 0; a < p; ++a)
-    for (int b = 0; b < p; ++b) {
-      double w = st.B[static_cast<size_t>(a) * p + b];
-      for (int i = 0; i < m; ++i) w += lam[i] * st.S[i][static_cast<size_t>(a) * p + b];
-      W[static_cast<size_t>(a) * p + b] = w;
-    }
+  for (int i = 0; i < m; ++i) {
+    const double li = lam[i];
+    const double* Si = st.S[i].data();
+    for (size_t ab = 0; ab < static_cast<size_t>(p) * p; ++ab) W[ab] += li * Si[ab];
+  }
   for (int i = 0; i < m; ++i)
     for (int a = 0; a < p; ++a) Jt[static_cast<size_t>(i) * p + a] = J[static_cast<size_t>(i) * p + a];
 }
@@ -341,11 +372,6 @@ Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& l
     }
     double t = 0.0;
     for (int a = 0; a < p; ++a) t += fr[a] * fr[a];
-    return t;
-  };
-  auto viol = [&](const double* v) {
-    double t = 0.0;
-    for (int i = 0; i < m; ++i) t += std::fabs(st.cval(cons, i, v) + st.tau[i]);
     return t;
   };
   int it = 0;
@@ -416,7 +442,8 @@ Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& l
     double lmax = 0.0;
     for (int i = 0; i < m; ++i) lmax = std::max(lmax, std::fabs(lp[i]));
     mu = std::max(mu, 2.0 * lmax);
-    const double v0 = viol(y);
+    double v0 = 0.0;  // viol(y): F holds c_i(y) + tau_i (the residual at y, the same tau)
+    for (int i = 0; i < m; ++i) v0 += std::fabs(F[p + i]);
     const double phi0 = fval(y) + mu * v0;
     double dd = 0.0;  // directional derivative of the merit along d (J d = -(c + tau))
     for (int a = 0; a < p; ++a) dd += gf[a] * d[a];
@@ -429,7 +456,9 @@ Run sqp_run(KKTState& st, const QuadCon* cons, double* y, std::vector<double>& l
       st.residual(cons, yn.data(), ln.data(), Fn.data(), J);
       fnew = norm2(Fn.data(), n);
       if (std::isfinite(fnew)) {
-        const double phin = fval(yn.data()) + mu * viol(yn.data());
+        double vn = 0.0;  // viol(yn) from Fn (c_i(yn) + tau_i)
+        for (int i = 0; i < m; ++i) vn += std::fabs(Fn[p + i]);
+        const double phin = fval(yn.data()) + mu * vn;
         if ((dd < 0.0 && phin <= phi0 + 1e-4 * alpha * dd) || (delta == 0.0 && fnew <= (1.0 - 1e-4 * alpha) * fn)) {
           ok = true;
           break;

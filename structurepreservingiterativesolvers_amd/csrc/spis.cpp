@@ -2751,7 +2751,7 @@ struct Solver {
 // tools/host_phases.py: a build with -DSPIS_HOST_PHASES (make phases) prints the mean host time
 // of spis_solve's phases every 40 calls (the product build compiles the marks away)
 #ifdef SPIS_HOST_PHASES
-static double g_phase_t[20], g_phase_acc[20];
+static double g_phase_t[32], g_phase_acc[32];
 static int g_phase_calls = 0;
 #define PHASE(i) (g_phase_t[i] = now_s())
 #define PHASE_IF(cond, i) ((cond) ? (void)(g_phase_t[i] = now_s()) : (void)0)
@@ -2939,8 +2939,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       bool fused = false, col_added = false;
       if (L) {
         bool ok = false;
+        PHASE_IF(j == 10, 20);
         ST_TRY(S.wait_hcol(j, &ok));
         PHASE_IF(j == k - 1, 10);
+        PHASE_IF(j == 10, 21);
         if (!ok) {  // the chain failed (c->chain_err): reported at the end of the solve
           (void)hipStreamSynchronize(s);
           break;
@@ -2959,7 +2961,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
             qr.solve(j + 1, yspec.data());
             fused = true;
           }
+          PHASE_IF(j == 10, 22);
           ST_TRY(S.enqueue_chain(j + 1, j >= 1 ? j - 1 : -1, fused ? yspec.data() : nullptr));
+          PHASE_IF(j == 10, 23);
         } else if (brk && j >= 1 && j + 1 < k) {  // no c_{j+1}: U_{j-1}'s residual on its own
           ST_TRY(S.enqueue_finalize(j - 1));
         }
@@ -2996,7 +3000,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           PHASE_IF(j == k - 1, 14);
         }
       }
+      PHASE_IF(j == 10, 24);
       ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : (deferred == j - 1 ? SPIS_OK : S.wait_update(j - 1)));
+      PHASE_IF(j == 10, 25);
       prof_drain(c);
       if (pending >= 0 && pending != deferred) {  // finish iteration j-1: true residual + stop test (:290-297)
         out->res_host[n_res++] = S.residual(pending);
@@ -3146,7 +3152,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         PHASE_IF(j == k - 1, 16);
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
+          PHASE_IF(j == 10, 26);
           ST_TRY(S.enqueue_dual(j, j + 2));
+          PHASE_IF(j == 10, 27);
         } else {
           // the forced constrained last step's reduction first (its inputs, q_0 .. q_{k-1} and
           // x0, are complete): the host's KKT then runs while the GPU computes this residual

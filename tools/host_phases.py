@@ -20,7 +20,8 @@ from structurepreservingiterativesolvers_amd.device import (DeviceVector, device
                                                             device_matrix, get_context)
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 80
-wl = bench.build_workload(argparse.Namespace(config="c3", M=None, cycles=10))
+cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
+wl = bench.build_workload(argparse.Namespace(config=cfg, M=None, cycles=10))
 ctx = get_context(0)
 Ad = device_matrix(wl["A"], ctx=ctx)
 bd = DeviceVector.from_host(wl["b"], ctx=ctx)
@@ -29,7 +30,7 @@ conlist = device_constraints(wl["conlist"], ctx=ctx)
 
 
 def solve():
-    return solvers.cgmres(Ad, bd, x0d, 30, tol=1e-19, conlist=conlist)
+    return solvers.cgmres(Ad, bd, x0d, 30, tol=1e-19, conlist=conlist)  # (C4's lifted constraints: class form)
 
 
 for _ in range(5):
@@ -49,7 +50,7 @@ for _ in range(reps):
     t = time.perf_counter()
     _, d = solve()
     marks.append((t, time.perf_counter(), d["x"].stamps[4 * 30], d["x"].stamps[4 * 30 + 1]))
-    entry.append([t_fn(i) for i in range(17)] if t_fn is not None else [np.nan] * 17)
+    entry.append([t_fn(i) for i in range(28)] if t_fn is not None else [np.nan] * 28)
 solvers._CHECKPOINTS = None
 ph = np.array(cps).reshape(reps, 5)
 m = np.array(marks)
@@ -72,6 +73,11 @@ print("t_start - mark 4 (us): mean %.2f" % (1e6 * np.mean(m[:, 2] - P[:, 4])))
 L10 = 1e6 * np.diff(P[:, 10:17], axis=1)
 print("last iteration, mark 10 -> 16 deltas (us): mean", np.round(L10.mean(axis=0), 1), "median",
       np.round(np.median(L10, axis=0), 1))
+# iteration 10: wait for H[:, 10] (20 -> 21), Givens (-> 22), enqueue c_11 (-> 23), LS and
+# branch (-> 24), wait for res_9 (-> 25), (-> 26), enqueue the dual (-> 27)
+L20 = 1e6 * np.diff(P[:, 20:28], axis=1)
+print("iteration 10, mark 20 -> 27 deltas (us): mean", np.round(L20.mean(axis=0), 1), "median",
+      np.round(np.median(L20, axis=0), 1))
 # the ctypes call alone: spis_solve with a null context returns at its argument check
 opts, out, ws = solvers._lib.SolveOpts(), solvers._lib.SolveOut(), C.c_void_p()
 t = time.perf_counter()

@@ -1,8 +1,8 @@
-"""GPU: C3's forced last constrained step as the host KKT solve received it (Hessenberg, beta,
+"""GPU: C3's (or another configuration's) forced last constrained step as the host KKT solve received it (Hessenberg, beta,
 constraint terms, warm start, the device run's y and LS message), saved for CPU profiling of
 kkt_newton (tools/kkt_prof.py).
 
-    python tools/kkt_dump.py OUT.npz
+    python tools/kkt_dump.py OUT.npz [cfg]
 """
 import argparse
 import os
@@ -17,7 +17,8 @@ from structurepreservingiterativesolvers_amd import solvers  # noqa: E402
 from structurepreservingiterativesolvers_amd.device import DeviceVector, device_constraints, device_matrix, get_context  # noqa: E402
 
 out = sys.argv[1]
-wl = bench.build_workload(argparse.Namespace(config="c3", M=None, cycles=1))
+cfg = sys.argv[2] if len(sys.argv) > 2 else "c3"
+wl = bench.build_workload(argparse.Namespace(config=cfg, M=None, cycles=1))
 ctx = get_context(0)
 A = device_matrix(wl["A"], ctx=ctx)
 n = wl["A"].shape[0]
