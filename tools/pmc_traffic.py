@@ -98,7 +98,7 @@ def reduce(cfg, fetch_csv, write_csv, out):
         "kernel_names": sorted({names[d] for d in solver_dual} | {names[d] for d in mgs}),
     }
     # the constrained step's full reduction (round 5): the basis transpose and the K7t / K7m Gram
-    for key, pat in (("transpose", "transpose_basis_kernel"), ("gram_sym", "constraint_gram_sym_kernel"),
+    for key, pat in (("transpose", "transpose_basis"), ("gram_sym", "constraint_gram_sym_kernel"),
                      ("gram_mfma", "constraint_gram_mfma_kernel")):
         ds = [d for d in byte if d <= end_solver and pat in names[d]]
         if ds:
