@@ -235,7 +235,78 @@ def build_workload(args):
             "desc": f"lkdvRK GL(3) block-stage (config C4, M={M}), 3 invariants lifted to (M, v, c) form"}
 
 
+def spawn_ranks(n, script=None, argv=None):
+    """``bench.py --gpus N`` started without a launcher: start the N ranks as child processes of
+    this one (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1 rendezvous), forward rank 0's
+    JSON line and return the exit status (non-zero if any rank failed).  Runs before anything here
+    touches HIP: this process only waits on its children."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+
+    def die_with_parent():  # a rank outlives no parent (PR_SET_PDEATHSIG = SIGKILL)
+        import ctypes
+
+        ctypes.CDLL(None).prctl(1, signal.SIGKILL)
+
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPIS_BENCH_LAUNCH="bench.py spawn")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)]
+                                      + list(sys.argv[1:] if argv is None else argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      preexec_fn=die_with_parent))
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    out = []  # rank 0's stdout, drained as it comes so a full pipe never stalls the rank
+    import threading
+
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read().decode()), daemon=True)
+    reader.start()
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.poll() not in (None, 0):
+                failed = (r, p.returncode)
+                break
+        else:
+            time.sleep(0.2)
+    if failed is None:
+        failed = next(((r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0), None)
+    if failed is not None:  # a rank died: its peers would wait in a collective forever
+        stop_all()
+        print(f"bench.py: rank {failed[0]} of {n} exited with status {failed[1]}", file=sys.stderr)
+        return failed[1] if failed[1] > 0 else 1
+    reader.join()
+    sys.stdout.write("".join(out))
+    sys.stdout.flush()
+    return 0
+
+
 def main():
+    if "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+        # --gpus N > 1 with no launcher: this process becomes the parent of N ranks
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        known, _ = pre.parse_known_args()
+        if known.gpus > 1:
+            sys.exit(spawn_ranks(known.gpus))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)

@@ -204,6 +204,10 @@ int spis_comm_unique_id(uint8_t id_out[128]);
 int spis_comm_init(spis_context* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int spis_comm_allreduce_sum(spis_context* ctx, double* buf_dev, int64_t count);
 int spis_comm_barrier(spis_context* ctx);
+/* The rank count of the context's communicator as the transport itself reports it: RCCL's
+ * ncclCommCount for spis_comm_init, the count given to spis_comm_init_host for the host
+ * transport (*transport_out 1 = RCCL, 2 = host), 0 ranks / transport 0 with no communicator. */
+int spis_comm_size(spis_context* ctx, int32_t* nranks_out, int32_t* transport_out);
 
 /* The same several-rank code path with the collectives done by a host callback instead of RCCL
  * (operands staged through host memory, the stream drained first).  For rehearsing several ranks

@@ -132,6 +132,7 @@ SIGNATURES = [
     ("spis_comm_init", C.c_int, [_VP, _I32, _I32, C.POINTER(C.c_uint8)]),
     ("spis_comm_allreduce_sum", C.c_int, [_VP, _VP, _I64]),
     ("spis_comm_barrier", C.c_int, [_VP]),
+    ("spis_comm_size", C.c_int, [_VP, _PI32, _PI32]),
     ("spis_comm_init_host", C.c_int, [_VP, _I32, _I32, HOST_COLL_FN, _VP]),
     ("spis_csr_upload", C.c_int, [_VP, _I64, _I64, _I64, _PI32, _PI32, _PD, C.POINTER(HaloDesc), C.POINTER(_VP)]),
     ("spis_matrix_destroy", C.c_int, [_VP]),

@@ -885,6 +885,24 @@ extern "C" int spis_comm_allreduce_sum(spis_context* c, double* buf, int64_t cou
   })
 }
 
+extern "C" int spis_comm_size(spis_context* c, int32_t* nranks_out, int32_t* transport_out) {
+  ABI_GUARD({
+    if (!c || !nranks_out || !transport_out) return fail(SPIS_ERR_ARG, "null argument");
+    *nranks_out = 0;
+    *transport_out = 0;
+    if (c->comm) {
+      int n = 0;
+      NCCL_TRY(ncclCommCount(c->comm, &n));
+      *nranks_out = n;
+      *transport_out = 1;
+    } else if (c->host_coll) {
+      *nranks_out = c->nranks;
+      *transport_out = 2;
+    }
+    return SPIS_OK;
+  })
+}
+
 extern "C" int spis_comm_barrier(spis_context* c) {
   ABI_GUARD({
     if (!c) return fail(SPIS_ERR_ARG, "null context");

@@ -304,6 +304,13 @@ class Comm:
             raise ValueError(f"unknown transport {self.transport!r} (rccl or host)")
         self.ctx.nranks, self.ctx.rank = self.world, self.rank
 
+    def transport_size(self):
+        """(ranks, transport) as the library's communicator reports them (spis_comm_size): RCCL's
+        own ncclCommCount for ``rccl``, the count the host transport was given for ``host``."""
+        n, t = C.c_int32(0), C.c_int32(0)
+        _lib.check(self.ctx.L.spis_comm_size(self.ctx.handle, C.byref(n), C.byref(t)), "spis_comm_size")
+        return int(n.value), {0: None, 1: "rccl", 2: "host"}[int(t.value)]
+
     def allgather(self, obj):
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
@@ -468,6 +475,14 @@ def bench_main(args, metric):
 
     comm = Comm()
     P = comm.world
+    want = getattr(args, "gpus", P)
+    if P != want:
+        raise RuntimeError(f"bench.py --gpus {want} but the process group has {P} rank(s): launch with "
+                           "torch.distributed.run --nproc-per-node N, or without a launcher (bench.py then "
+                           "spawns the N ranks itself)")
+    comm_ranks, comm_transport = comm.transport_size()
+    if comm_ranks != P:
+        raise RuntimeError(f"the {comm_transport} communicator has {comm_ranks} rank(s), the process group {P}")
     config = getattr(args, "config", "c3")
     wl = dist_workload(config, P, args.M)
     A = wl["A"]
@@ -550,6 +565,11 @@ def bench_main(args, metric):
                                                           "host-staged gloo collectives (SPIS_TRANSPORT=host: a "
                                                           "rehearsal of the path, not a measurement)"),
                 "global_iterations_per_s": iters / elapsed,
+                # the communicator's own rank count (ncclCommCount through spis_comm_size)
+                "rccl_ranks": comm_ranks if comm_transport == "rccl" else None,
+                "comm_ranks": comm_ranks,
+                "transport": comm_transport,
+                "launch": os.environ.get("SPIS_BENCH_LAUNCH", "torch.distributed.run"),
             },
             "roofline": {
                 "kernel": kname,

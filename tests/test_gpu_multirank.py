@@ -244,3 +244,27 @@ def test_several_ranks_on_one_gpu_match_oracle(tmp_path, problem, world, M, k, c
             if con.v is not None:
                 val += np.asarray(con.v) @ x
             assert abs(val) <= 1e-11 * max(1.0, abs(float(np.asarray(con.c)))), val
+
+
+@pytest.mark.gpu
+def test_bench_spawns_ranks_without_launcher():
+    """``python bench.py --gpus 2`` with no launcher starts its two ranks itself (bench.spawn_ranks)
+    and measures both: one JSON line, ``n_gpus`` 2 and the communicator's own rank count 2 (the
+    host transport here: two ranks on one GPU, which RCCL refuses).  The mesh is cut to M = 120
+    (N = 172,800) so the test stays inside its time limit."""
+    import json
+
+    env = dict(os.environ, SPIS_DEVICE="0", SPIS_TRANSPORT="host", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
+                        "1", "--no-cpu-baseline", "--M", "120"], env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
+    lines = [ln for ln in p.stdout.decode().splitlines() if ln.strip()]
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["config"]["comm_ranks"] == 2 and d["config"]["transport"] == "host"
+    assert d["config"]["launch"] == "bench.py spawn"
+    assert d["value"] > 0
