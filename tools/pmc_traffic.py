@@ -2,7 +2,7 @@
 before it reports the figures as ``roofline.traffic`` (bench.load_traffic).
 
 GPU box, two separate rocprofv3 passes over the same short bench (MI355X_MICROARCH.md: one
-counter group per pass), then the reduction (tools/r04_pmc.sh runs all three):
+counter group per pass), then the reduction (tools/archive/r04_pmc.sh runs all three):
 
   rocprofv3 --pmc FETCH_SIZE --output-format csv -d D/f -o run -- python tools/pmc_traffic.py run c3
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d D/w -o run -- python tools/pmc_traffic.py run c3
