@@ -137,7 +137,7 @@ def kernels_sha256():
 
 
 def load_traffic(args, c16, pipe):
-    """Per-launch PMC bytes from profiles/r05_traffic_<config>.json (tools/r05_pmc.sh; else r04), with the
+    """Per-launch PMC bytes from profiles/r05_traffic_<config>.json (tools/archive/r05_pmc.sh; else r04), with the
     reason when there are none: the file must have been measured on this csrc/kernels.hip (SHA-256)
     with this run's SpMV and chain options, on the configuration's default size."""
     path = os.path.join(ROOT, "profiles", f"r05_traffic_{args.config}.json")
@@ -214,7 +214,7 @@ def build_workload(args):
             D, c3 = assembly.extra_constraint(len(x0), dic["z0"], seed=2)
             conlist.append(ls._Constraint(D, np.zeros(len(x0)), c3))
             desc += " + synthetic third constraint (seed 2)"
-        return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "desc": desc,
+        return {"A": dic["A"], "b": dic["b"], "conlist": conlist, "desc": desc, "dic": dic,
                 "cycles": args.cycles if args.config == "c5" else 1}
     if args.config == "c2":
         from structurepreservingiterativesolvers_amd.lkdv import LinearSolver as ls
@@ -299,6 +299,49 @@ def spawn_ranks(n, script=None, argv=None):
     return 0
 
 
+def wrapper_rate(wl, args, reps=10, warm=3):
+    """SURVEY §8(d)'s it/s as defined there: ``dict['steps']`` / wall time of the drop-in call
+    ``swe.LinearSolver.cgmresWrapper(dic, x0, k, tol)`` (reference ``swe/LinearSolver.py:12-49``) on
+    host SciPy/NumPy inputs, warm (the operator uploads cached by the warm-up calls, as a
+    time-stepping caller sees them; only the matrix upload is excluded).  Each call still uploads
+    b, x0 and the constraint vectors, re-verifies the cached matrices against their full contents
+    and downloads x; the host phases are reported beside the rate (solvers._PHASES)."""
+    from structurepreservingiterativesolvers_amd import device, solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as ls
+
+    dic = wl["dic"]
+    x0 = np.zeros(dic["A"].shape[0])
+    d = None
+    for _ in range(warm):
+        _, d = ls.cgmresWrapper(dic, x0, args.k, tol=args.tol)
+    solvers._PHASES = {}
+    iters = 0
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, d = ls.cgmresWrapper(dic, x0, args.k, tol=args.tol)
+        iters += d["steps"]
+    el = time.perf_counter() - t0
+    ph, solvers._PHASES = solvers._PHASES, None
+    t1 = time.perf_counter()
+    for M in (dic["A"], dic["L"]):
+        device.content_digest(M)
+    hash_ms = 1e3 * (time.perf_counter() - t1)
+    per = {k: 1e3 * v / reps for k, v in ph.items()}
+    return {
+        "call": f"swe.LinearSolver.cgmresWrapper(dic, x0=zeros, k={args.k}, tol={args.tol:g}) on SciPy/NumPy inputs",
+        "value": iters / el,
+        "unit": "iterations/s",
+        "ms_per_call": 1e3 * el / reps,
+        "calls": reps,
+        "h2d_ms": per.get("h2d", 0.0),
+        "verify_ms": hash_ms,
+        "verify_wait_ms": per.get("verify_wait", 0.0),
+        "d2h_ms": per.get("d2h", 0.0),
+        "phases_ms": per,
+        "verify_threads": device._HASH_THREADS,
+    }
+
+
 def main():
     if "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
         # --gpus N > 1 with no launcher: this process becomes the parent of N ranks
@@ -322,6 +365,7 @@ def main():
                          "step i, every step constrained)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wrapper", action="store_true", help="skip the drop-in wrapper call's rate (c3)")
     ap.add_argument("--no-cold", action="store_true", help="skip the standalone cold-cache SpMV timing")
     ap.add_argument("--force-distributed", action="store_true",
                     help="use the row-partitioned RCCL path even for one rank (plumbing check)")
@@ -450,7 +494,7 @@ def main():
              "xcd_natural": "spmv_pipe_kernel<2048, 4> (XCD-local walk, natural block order)"}[pipe]
     if c16 and pipe != "off":
         kname = kname.replace(", 4>", ", 4, true>").replace(")", ", 16-bit columns)")
-    # PMC traffic (profiles/r04_traffic_<config>.json, tools/r04_pmc.sh): used only when it was
+    # PMC traffic (profiles/r04_traffic_<config>.json, tools/archive/r04_pmc.sh): used only when it was
     # measured on this kernels.hip and these SpMV / chain options (load_traffic checks both)
     tr, tr_note = load_traffic(args, c16, pipe)
     if fused:  # the SpMV of the north star: true residual of x_j fused with the Arnoldi SpMV of z_{j+2}
@@ -550,6 +594,9 @@ def main():
             "host_outside_solve_us": 1e6 * outside / args.steps,
         },
     }
+    if args.config == "c3" and args.method == "cgmres" and not args.no_wrapper:
+        out["wrapper"] = wrapper_rate(wl, args)
+        out["wrapper"]["frac_of_value"] = out["wrapper"]["value"] / out["value"]
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, conlist, args.k, args.tol, args.cpu_budget, args.method)
     print(json.dumps(out))

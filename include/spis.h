@@ -99,6 +99,11 @@ int spis_context_stream(spis_context* ctx, void** stream_out);
  * a second host thread beside spis_solve.  The bytes are hashed in 1 MiB pieces on up to
  * `threads` threads; the digest does not depend on the thread count. */
 int spis_host_hash(const void* data, int64_t bytes, int32_t threads, uint64_t* out);
+/* Whether any of `count` host fp64 entries is nonzero: in numpy's truthiness when `bitwise` is 0
+ * (-0.0 is zero, NaN is not: the wrappers drop an all-zero constraint vector), any bit set when 1
+ * (an x0 of +0.0 entries needs no upload).  Stops at the first nonzero entry; up to `threads`
+ * threads. */
+int spis_host_nonzero(const double* data, int64_t count, int32_t bitwise, int32_t threads, int32_t* any_out);
 
 /* ---- live kernel timing ------------------------------------------------------
  * spis_profile_enable(ctx, period): period > 0 makes spis_solve record HIP
@@ -193,7 +198,24 @@ enum spis_option {
   SPIS_OPT_NT_BASIS = 10,
   SPIS_OPT_COL16 = 11,
   SPIS_OPT_DIST_MGS = 12,
-  SPIS_OPT_SLAB_KEY = 16
+  SPIS_OPT_SLAB_KEY = 16,
+  /* A/B switches of parity tests (each is bitwise-neutral; the default 1 is the fast form): the
+   * constraint terms from cached increments (0 = the full reduction at every constrained step),
+   * the x0 = 0 test that skips the r0 SpMV's matrix read (0 = always the full SpMV), and the
+   * pipelined basis transpose of K7t (0 = the one-tile-at-a-time kernel).  Each starts from the
+   * environment variable of the same name (SPIS_GRAM_INC, SPIS_X0_ZERO_TEST,
+   * SPIS_TRANSPOSE_PIPE) read once when the context is created. */
+  SPIS_OPT_GRAM_INC = 17,
+  SPIS_OPT_X0_ZERO_TEST = 18,
+  SPIS_OPT_TRANSPOSE_PIPE = 19,
+  /* A/B switches of the one-reduce MGS (K2w / K2s; each from its environment variable at context
+   * creation, SPIS_K2W_*): the small-N threshold below which mode 3 takes K2s (-1 = where K2s
+   * fits, 0 = K2q at every N), the dots' fold into the dot pass (1 = on), the nontemporal window
+   * (-1 = auto) and the one-launch K2s (1 = on). */
+  SPIS_OPT_K2W_SMALL_N = 20,
+  SPIS_OPT_K2W_FOLD = 21,
+  SPIS_OPT_K2W_TW = 22,
+  SPIS_OPT_K2W_ONEPASS = 23
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

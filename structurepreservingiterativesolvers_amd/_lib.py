@@ -32,6 +32,13 @@ OPT_NT_BASIS = 10
 OPT_COL16 = 11
 OPT_DIST_MGS = 12
 OPT_SLAB_KEY = 16
+OPT_GRAM_INC = 17
+OPT_X0_ZERO_TEST = 18
+OPT_TRANSPOSE_PIPE = 19
+OPT_K2W_SMALL_N = 20
+OPT_K2W_FOLD = 21
+OPT_K2W_TW = 22
+OPT_K2W_ONEPASS = 23
 MESSAGES = {
     0: "Optimization terminated successfully",
     2: "More equality constraints than independent variables",
@@ -124,6 +131,7 @@ SIGNATURES = [
     ("spis_context_synchronize", C.c_int, [_VP]),
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
     ("spis_host_hash", C.c_int, [_VP, _I64, _I32, C.POINTER(C.c_uint64)]),
+    ("spis_host_nonzero", C.c_int, [_VP, _I64, _I32, _I32, _PI32]),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),
     ("spis_spmv_bench", C.c_int, [_VP, _VP, _I32, _I32, _I32, _PD]),

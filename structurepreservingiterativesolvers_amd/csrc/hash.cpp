@@ -1,4 +1,5 @@
-// hash.cpp — content digest of host arrays (spis_host_hash, include/spis.h).
+// hash.cpp — host-array scans of the drop-in boundary (include/spis.h): the content digest of
+// cached uploads (spis_host_hash) and the all-zero test of input vectors (spis_host_nonzero).
 //
 // The drop-in keeps one HBM copy per SciPy matrix object (device.py): the reference's callers
 // hand the same csr_matrix to solvers.cgmres on every call (e.g. lkdv/Evolve.py:41 through
@@ -8,11 +9,23 @@
 // in-place edit of any entry is caught and the solve redone on the new values.
 //
 // The digest: the bytes are cut into 1 MiB pieces; each piece is hashed by 4 independent 64-bit
-// multiply-xor lanes (memory-bound: ~6 GB/s per thread), and the piece digests are folded in piece
-// order, so the result does not depend on how many threads ran.
+// multiply-xor lanes, and the piece digests are folded in piece order, so the result does not
+// depend on how many threads ran.  The pieces are handed out one at a time from an atomic counter
+// to a persistent pool of workers (created on first use; a call that finds the pool busy — the
+// verifier thread and the caller's thread hashing at once — runs on its own thread), so a scan of
+// the C3 operator (~154 MB) pays no thread start-up and no core waits on a slower one's share.
+//
+// The zero test (spis_host_nonzero) is numpy's truthiness of every fp64 entry (-0.0 counts as
+// zero, NaN as nonzero; solvers.py drops an all-zero constraint vector, its v.Z term being 0) or
+// bitwise (solvers.py passes an x0 of +0.0 entries as the shared device zero vector, no upload;
+// -0.0 entries keep their sign through x_j = Z y + x0).  It stops at the first nonzero entry.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -59,36 +72,145 @@ uint64_t piece_digest(const unsigned char* p, int64_t n, uint64_t index) {
   return mix(mix(a0) ^ mix(a1 + 1) ^ mix(a2 + 2) ^ mix(a3 + 3) ^ mix(static_cast<uint64_t>(n)));
 }
 
+// any entry of p[0 .. n) nonzero: in numpy's sense (bits << 1) != 0 (the sign bit alone is
+// -0.0), or bitwise (any bit set: -0.0 counts)
+bool piece_nonzero(const uint64_t* p, int64_t n, bool bitwise) {
+  uint64_t acc = 0;
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    acc |= p[i] | p[i + 1] | p[i + 2] | p[i + 3] | p[i + 4] | p[i + 5] | p[i + 6] | p[i + 7];
+  for (; i < n; ++i) acc |= p[i];
+  return (bitwise ? acc : acc << 1) != 0;  // (a | b) << 1 == (a << 1) | (b << 1): sign bits dropped
+}
+
+// Persistent workers running one job at a time: job(piece) for piece = 0 .. n_pieces - 1, each
+// piece claimed from an atomic counter by whichever thread (the caller included) is free.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool();  // never destroyed: workers may outlive static destructors
+    return *p;
+  }
+
+  // false when another caller holds the pool (the caller then runs the job alone)
+  bool run(int threads, int64_t n_pieces, const std::function<void(int64_t)>& job) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    const int helpers = std::max(0, std::min<int>(threads, kMaxThreads) - 1);
+    if (!ensure(helpers)) return false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &job;
+      n_ = n_pieces;
+      next_.store(0);
+      active_ = helpers;
+      want_ = helpers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+
+ private:
+  static constexpr int kMaxThreads = 32;
+
+  bool ensure(int helpers) {
+    try {
+      while (static_cast<int>(workers_.size()) < helpers) {
+        const int id = static_cast<int>(workers_.size());
+        workers_.emplace_back([this, id] { loop(id); });
+        workers_.back().detach();
+      }
+    } catch (...) {
+      return static_cast<int>(workers_.size()) >= helpers;
+    }
+    return true;
+  }
+
+  void work() {
+    for (int64_t k = next_.fetch_add(1); k < n_; k = next_.fetch_add(1)) (*job_)(k);
+  }
+
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= want_) continue;  // not needed for this job
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--active_ == 0) done_cv_.notify_all();
+    }
+  }
+
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int64_t)>* job_ = nullptr;
+  int64_t n_ = 0;
+  std::atomic<int64_t> next_{0};
+  int active_ = 0, want_ = 0;
+  uint64_t gen_ = 0;
+};
+
+void for_pieces(int threads, int64_t n_pieces, const std::function<void(int64_t)>& job) {
+  if (threads > 1 && n_pieces >= 4 && Pool::get().run(threads, n_pieces, job)) return;
+  for (int64_t k = 0; k < n_pieces; ++k) job(k);
+}
+
 }  // namespace
 
 extern "C" int spis_host_hash(const void* data, int64_t bytes, int32_t threads, uint64_t* out) {
   if (!out || bytes < 0 || (bytes > 0 && !data)) return SPIS_ERR_ARG;
   const unsigned char* p = static_cast<const unsigned char*>(data);
   const int64_t np = (bytes + kPiece - 1) / kPiece;
-  std::vector<uint64_t> d(static_cast<size_t>(std::max<int64_t>(np, 1)), 0);
-  auto run = [&](int64_t k0, int64_t k1) {
-    for (int64_t k = k0; k < k1; ++k) {
+  try {
+    std::vector<uint64_t> d(static_cast<size_t>(std::max<int64_t>(np, 1)), 0);
+    for_pieces(threads, np, [&](int64_t k) {
       const int64_t o = k * kPiece;
       d[k] = piece_digest(p + o, std::min(kPiece, bytes - o), static_cast<uint64_t>(k));
-    }
-  };
-  int nt = std::max(1, std::min<int>(threads, static_cast<int>(np / 4)));  // >= 4 MiB per thread
-  try {
-    if (nt <= 1) {
-      run(0, np);
-    } else {
-      std::vector<std::thread> th;
-      const int64_t per = (np + nt - 1) / nt;
-      for (int t = 1; t < nt; ++t)
-        th.emplace_back(run, std::min(np, t * per), std::min(np, (t + 1) * per));
-      run(0, std::min(np, per));
-      for (auto& x : th) x.join();
-    }
+    });
+    uint64_t h = mix(static_cast<uint64_t>(bytes) ^ 0x5350495348415348ull);
+    for (int64_t k = 0; k < np; ++k) h = mix(h ^ d[k]) + 0x9E3779B97F4A7C15ull;
+    *out = h;
   } catch (...) {
     return SPIS_ERR_STATE;
   }
-  uint64_t h = mix(static_cast<uint64_t>(bytes) ^ 0x5350495348415348ull);
-  for (int64_t k = 0; k < np; ++k) h = mix(h ^ d[k]) + 0x9E3779B97F4A7C15ull;
-  *out = h;
+  return SPIS_OK;
+}
+
+extern "C" int spis_host_nonzero(const double* data, int64_t count, int32_t bitwise, int32_t threads,
+                                 int32_t* any_out) {
+  if (!any_out || count < 0 || (count > 0 && !data)) return SPIS_ERR_ARG;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(data);
+  constexpr int64_t kHead = 4096;  // most nonzero vectors show it in the first entries
+  if (piece_nonzero(w, std::min(count, kHead), bitwise != 0)) {
+    *any_out = 1;
+    return SPIS_OK;
+  }
+  if (count <= kHead) {
+    *any_out = 0;
+    return SPIS_OK;
+  }
+  constexpr int64_t kEl = kPiece / 8;
+  const int64_t rest = count - kHead, np = (rest + kEl - 1) / kEl;
+  std::atomic<int> found{0};
+  try {
+    for_pieces(threads, np, [&](int64_t k) {
+      if (found.load(std::memory_order_relaxed)) return;
+      const int64_t o = kHead + k * kEl;
+      if (piece_nonzero(w + o, std::min(kEl, count - o), bitwise != 0)) found.store(1, std::memory_order_relaxed);
+    });
+  } catch (...) {
+    return SPIS_ERR_STATE;
+  }
+  *any_out = found.load();
   return SPIS_OK;
 }

@@ -232,9 +232,11 @@ hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double
 // Ut in the perm order plus the linear terms Gv[c][a] = sum_r U[r][a] v_c[r] (vpart: partials of
 // kTransposeGrid x nvv np1; Gv: nvv x np1); np1 <= 32, nvv <= 4
 constexpr int kTransposeGrid = 2048;
+// pipe: the pipelined transpose (transpose_basis_pipe_kernel) when Ut is 16-byte aligned, else the
+// one-tile-at-a-time kernel (bitwise the same Ut and terms)
 hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                       double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
-                                      hipStream_t s, bool pin = false);
+                                      hipStream_t s, bool pin = false, bool pipe = true);
 hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, const GramSplit* split,
                                        const double* Ut, int nvv, const double* const* v, double* partials,
                                        double* G, hipStream_t s);

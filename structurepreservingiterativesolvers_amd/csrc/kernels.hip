@@ -1125,29 +1125,47 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     for (int k = 0; k < PER; ++k)
       if (data && p0 + k * DT < npair) r[k] = ld_basis(v2 + p0 + k * DT, nt);
   };
+  // start-up: the data workgroups issue their loads in the order of need (loads complete in issue
+  // order): x0 (stored to LDS as soon as it arrives: that wait covers x0 alone), w and q_1, q_2
+  // (step 0's dots), q_0 (step 1's update), the rest of the ring.  h_0 = q_0 . w (the SpMV's
+  // partials) and the piggybacked residual are summed by the gatherer, which has no basis loads to
+  // queue behind; h_0 reaches the data workgroups through the exchange slots (E_0) when step 1's
+  // update needs it.  The first exchange then starts after four vectors have arrived, not after
+  // six vectors and two partial sums behind them.
   if (!agg) {
+    double2 xr[PER];
+    if (FX) load(xr, x0, NT && tw == 0);
     if (FX && data) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) s_acc[k * DT + tid] = make_double2(0.0, 0.0);
     }
     load(y, w, NT);
 #pragma unroll
-    for (int m = 0; m < NS - 1; ++m)
+    for (int m = 1; m < NS - 1; ++m)
       if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch, NT && m >= tw);
-    if (FX && data) {  // x0 into LDS now (added at the end: its load latency off the tail)
-      const double2* x02 = reinterpret_cast<const double2*>(x0);
+    load(S[0], Q, NT && 0 >= tw);
+    if (FX && data) {  // x0 into LDS (added at the end: its load latency off the tail)
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (p0 + k * DT < npair) s_x0[k * DT + tid] = ld_basis(x02 + p0 + k * DT, NT && tw == 0);
+        if (p0 + k * DT < npair) s_x0[k * DT + tid] = xr[k];
     }
   }
   if (tid == 0) s_fail = 0;
   const int tr_row = blockIdx.x == 0 ? 0 : agg ? 2 : static_cast<int>(blockIdx.x) == GD - 1 ? 1 : -1;
   if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 0);
-  const double h0 = chain_sum_partials(part_in, n_in, s_wave);
-  if (xpart != nullptr && blockIdx.x == 0) {  // piggybacked reduction (the previous update's residual)
-    const double t = chain_sum_partials(xpart, n_x, s_wave);
-    if (tid == 0) publish(x_out, t, flag, seq);
+  double h0 = 0.0;  // data workgroups: from E_0 (wait_h(0)) at their first update
+  if (agg) {
+    h0 = chain_sum_partials(part_in, n_in, s_wave);
+    if (xpart != nullptr) {  // piggybacked reduction (the previous update's residual)
+      const double t = chain_sum_partials(xpart, n_x, s_wave);
+      if (tid == 0) publish(x_out, t, flag, seq);
+    }
+    if (tid == 0) {  // E_0: h_0 in h slot 0 under tag base (slot 0's next use, E_4, is published
+                     // after every workgroup has read h_0 at its step 1, before its E_4 partials)
+      const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(h0));
+      chain_store(hslots, base, static_cast<unsigned>(bits));
+      chain_store(hslots + 1, base, static_cast<unsigned>(bits >> 32));
+    }
   }
   if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 1);
 
@@ -1341,8 +1359,8 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     constexpr int R = decltype(RC)::value;
     constexpr int RM = (R + NS - 1) % NS;  // q_{i-1}, then q_{i+NS-1}
     if (i >= 1) {
-      double hu = h0;
-      if (i - 1 >= 1 && !wait_h(i - 1, &hu)) return false;
+      double hu = 0.0;
+      if (!wait_h(i - 1, &hu)) return false;  // (i = 1: h_0 from E_0)
       update(hu, S[RM]);
     }
     if (i == j) {  // last: subtract h_j q_j, ||w||^2 through the gatherer, normalise
@@ -1357,8 +1375,8 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
             xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
           }
       }
-      double hj = h0;
-      if (j >= 1 && !wait_h(j, &hj)) return false;
+      double hj = 0.0;
+      if (!wait_h(j, &hj)) return false;  // (j = 0: h_0 from E_0)
       update(hj, S[R]);
       double v[NV];
 #pragma unroll
@@ -3623,16 +3641,14 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 
 hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                       double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
-                                      hipStream_t s, bool pin) {
+                                      hipStream_t s, bool pin, bool pipe) {
   const int np1 = p + 1;
   if (np1 > 32 || nvv < 0 || nvv > 4 || nvv * np1 > kBlock) return hipErrorInvalidValue;
   const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int c = 0; c < nvv; ++c) vv[c] = v[c];
   const int64_t ntiles = (n + 63) / 64;
   const int g = static_cast<int>(ntiles < kTransposeGrid ? (ntiles < 1 ? 1 : ntiles) : kTransposeGrid);
-  // SPIS_TRANSPOSE_PIPE=0: the one-tile-at-a-time kernel (A/B; bitwise the same Ut and terms)
-  const char* tp = std::getenv("SPIS_TRANSPOSE_PIPE");
-  if ((tp == nullptr || std::atoi(tp) != 0) && aligned16d(Ut))
+  if (pipe && aligned16d(Ut))
     hipLaunchKernelGGL(transpose_basis_pipe_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock), 0, s, n, p, Z, pitch,
                        x0, Ut, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
   else

@@ -159,6 +159,12 @@ struct spis_context {
   int nt_basis = 2;                 // the chain's basis loads nontemporal (SPIS_OPT_NT_BASIS): 0 off, 1 on, 2 auto
   int col16 = 1;                    // the pipelined SpMV on the 16-bit column copy: 1 beyond the Infinity Cache, 2 always (SPIS_OPT_COL16)
   int slab_key = 1;                 // SPIS_OPT_SLAB_KEY: slab order's blocks by position within a slab (at upload)
+  // A/B switches, read from the environment once at context creation (SPIS_OPT_GRAM_INC,
+  // SPIS_OPT_X0_ZERO_TEST, SPIS_OPT_TRANSPOSE_PIPE; the K2w ones for tools/chainbench only)
+  bool gram_inc = true, x0_zero_test = true, transpose_pipe = true;
+  bool k2w_fold = true, k2w_onepass = true;
+  int k2w_tw = -1;
+  int64_t k2w_small_n = -1;
   int spmv_pipe = 5;                // solver SpMVs: 0 = K1/K1d; K1p/K1dp 1 = grid-stride, 2 = XCD-local walk; 5 = auto (2 or 1); 7 = 2 on the natural block order
   // U_j's GEMV on stream2 beside A_{j+1}'s chain when the chain does not carry it (outside L mode,
   // or a constrained LS_j); the dual SpMV waits for it through a stream write / wait on a device word
@@ -602,6 +608,17 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     // (a system-scope one writes back and invalidates L2 at every iteration, ~8 us each);
     // (SPIS_EVENT_MODE below selects the scope for measurements)
     // SPIS_EVENT_MODE: 0 system-scope release, 1 device scope (default), 2 no release fence
+    auto env_flag = [](const char* name, bool dflt) {
+      const char* v = std::getenv(name);
+      return v == nullptr ? dflt : std::atoi(v) != 0;
+    };
+    c->gram_inc = env_flag("SPIS_GRAM_INC", true);
+    c->x0_zero_test = env_flag("SPIS_X0_ZERO_TEST", true);
+    c->transpose_pipe = env_flag("SPIS_TRANSPOSE_PIPE", true);
+    c->k2w_fold = env_flag("SPIS_K2W_FOLD", true);
+    c->k2w_onepass = env_flag("SPIS_K2W_ONEPASS", true);
+    if (const char* v = std::getenv("SPIS_K2W_TW")) c->k2w_tw = std::atoi(v);
+    if (const char* v = std::getenv("SPIS_K2W_SMALL_N")) c->k2w_small_n = std::atoll(v);
     const char* se = std::getenv("SPIS_EVENT_MODE");
     const int mode = se ? std::atoi(se) : 1;
     const unsigned evf = hipEventDisableTiming | (mode == 1 ? hipEventReleaseToDevice : 0u) |
@@ -743,6 +760,26 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_SLAB_KEY:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "slab_key %lld: 0 or 1", (long long)value);
         c->slab_key = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_GRAM_INC:
+      case SPIS_OPT_X0_ZERO_TEST:
+      case SPIS_OPT_TRANSPOSE_PIPE:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "option %d takes 0 or 1", option);
+        (option == SPIS_OPT_GRAM_INC ? c->gram_inc : option == SPIS_OPT_X0_ZERO_TEST ? c->x0_zero_test
+                                                                                      : c->transpose_pipe) = value == 1;
+        return SPIS_OK;
+      case SPIS_OPT_K2W_SMALL_N:
+        if (value < -1) return fail(SPIS_ERR_ARG, "k2w small n %lld: >= -1", (long long)value);
+        c->k2w_small_n = value;
+        return SPIS_OK;
+      case SPIS_OPT_K2W_TW:
+        if (value < -1 || value > kMaxK) return fail(SPIS_ERR_ARG, "k2w tw %lld: -1 .. %d", (long long)value, kMaxK);
+        c->k2w_tw = static_cast<int>(value);
+        return SPIS_OK;
+      case SPIS_OPT_K2W_FOLD:
+      case SPIS_OPT_K2W_ONEPASS:
+        if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "option %d takes 0 or 1", option);
+        (option == SPIS_OPT_K2W_FOLD ? c->k2w_fold : c->k2w_onepass) = value == 1;
         return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }
@@ -1654,7 +1691,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     double* dstd = static_cast<double*>(dp);
     if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
     HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart, dstd + voff, st,
-                                       true));
+                                       true, c->transpose_pipe));
     for (const Launch& L : plan)
       HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, dstd + static_cast<size_t>(L.ci) * np1 * np1,
                                          st, true));
@@ -1663,7 +1700,7 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
   if (tsym) {  // Ut + the linear terms in one pass over the basis
     if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
     HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart,
-                                       c->cg_G + 64 * 64, st));
+                                       c->cg_G + 64 * 64, st, false, c->transpose_pipe));
     if (nv > 0) ST_TRY(allreduce_on(c, c->cg_G + 64 * 64, static_cast<int64_t>(nv) * np1, st));  // local rows' sums
     if (nv > 0)
       HIP_TRY(hipMemcpyAsync(dst + voff, c->cg_G + 64 * 64, sizeof(double) * nv * np1, hipMemcpyDeviceToHost, st));
@@ -1856,7 +1893,7 @@ struct ConStep {
 
 static bool con_inc_eligible(spis_context* c, spis_workspace* ws, int m, const spis_constraint_desc* cons, int p) {
   if (!fused_con_ok(c, p, m, cons) || p + 2 > kMdMax || static_cast<int>(ws->con.size()) < m) return false;
-  if (std::getenv("SPIS_GRAM_INC") != nullptr && std::atoi(std::getenv("SPIS_GRAM_INC")) == 0) return false;
+  if (!c->gram_inc) return false;
   for (int ci = 0; ci < m; ++ci) {
     spis_matrix* M = cons[ci].M;
     if (M == nullptr || M->all_zero) continue;
@@ -2313,13 +2350,13 @@ struct Solver {
   int gs;  // SpMV partial count
   int gb;  // BLAS-1 partial count
   std::vector<double> hostq, hostz;
-  // A/B switches (tests and tools/r04_*.sh): the K2w fold, its temporal window, K2s, and the
-  // small-N threshold for K2w at SPIS_OPT_MGS_CHAIN 3 (0: K2q at every N)
-  const bool k2w_fold = std::getenv("SPIS_K2W_FOLD") == nullptr || std::atoi(std::getenv("SPIS_K2W_FOLD")) != 0;
-  const int k2w_tw = std::getenv("SPIS_K2W_TW") != nullptr ? std::atoi(std::getenv("SPIS_K2W_TW")) : -1;
-  const bool k2w_onepass = std::getenv("SPIS_K2W_ONEPASS") == nullptr || std::atoi(std::getenv("SPIS_K2W_ONEPASS")) != 0;
-  const int64_t k2w_small_n = std::getenv("SPIS_K2W_SMALL_N") != nullptr ? std::atoll(std::getenv("SPIS_K2W_SMALL_N"))
-                                                                         : -1;  // -1: where K2s fits
+  // A/B switches (the context's, from the environment at its creation): the K2w fold, its
+  // temporal window, K2s, and the small-N threshold for K2w at SPIS_OPT_MGS_CHAIN 3 (0: K2q at
+  // every N; -1: where K2s fits)
+  const bool k2w_fold = c->k2w_fold;
+  const int k2w_tw = c->k2w_tw;
+  const bool k2w_onepass = c->k2w_onepass;
+  const int64_t k2w_small_n = c->k2w_small_n;
 
   double* Qv(int i) const { return ws->Q + static_cast<int64_t>(i) * ws->pitch; }
   double* Zv(int i) const { return ws->Zb + static_cast<int64_t>(i) * ws->pitch; }
@@ -2818,6 +2855,16 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     ST_TRY(get_workspace(c, n, n + A->n_ghost, k, sep_z, &ws));
     PHASE(2);
     std::unique_ptr<spis_workspace, int (*)(spis_workspace*)> guard(ws, spis_workspace_release);
+    // side-stream work (a constrained step's increments beside the chain, a GEMV) reads the
+    // workspace and x0 and writes the constraint caches and the pinned slots the next solve arms:
+    // it completes before the solve returns on every path, the early exits included (destroyed
+    // before the guard hands the workspace back)
+    struct SideJoin {
+      hipStream_t st;
+      ~SideJoin() {
+        if (hipStreamQuery(st) == hipErrorNotReady) (void)hipStreamSynchronize(st);
+      }
+    } side_join{c->stream2};
     ws->steps = 0;
     ws->n_iter_y = 0;
     ws->broke_at_start = false;
@@ -2850,9 +2897,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // x0 into a halo'd buffer only when the SpMV reads ghost entries
     // x0 = 0 (the copy sees no nonzero) on a finite single-rank matrix: the r0 SpMV skips the
     // matrix, r0 = b bit for bit (spmv_pipe_kernel MODE 3)
-    // (SPIS_X0_ZERO_TEST=0: always the full SpMV, the A/B of test_x0_zero_fast_path_bit_identical)
+    // (SPIS_OPT_X0_ZERO_TEST 0: always the full SpMV, the A/B of test_x0_zero_fast_path_bit_identical)
     const bool x0_test = !c->dist_on() && A->n_ghost == 0 && A->all_finite && A->dual_view().blk_meta != nullptr &&
-                         (std::getenv("SPIS_X0_ZERO_TEST") == nullptr || std::atoi(std::getenv("SPIS_X0_ZERO_TEST")) != 0);
+                         c->x0_zero_test;
     if (x0_test) {
       if (!c->x0_flag) {
         HIP_TRY(hipMalloc(&c->x0_flag, sizeof(unsigned)));

@@ -71,6 +71,13 @@ _OPTIONS = {
     "col16": (_lib.OPT_COL16, {False: 0, True: 2, "auto": 1}),
     "dist_mgs": (_lib.OPT_DIST_MGS, {"per_step": 0, "one_reduce": 1}),
     "slab_key": (_lib.OPT_SLAB_KEY, None),
+    "gram_inc": (_lib.OPT_GRAM_INC, None),
+    "x0_zero_test": (_lib.OPT_X0_ZERO_TEST, None),
+    "transpose_pipe": (_lib.OPT_TRANSPOSE_PIPE, None),
+    "k2w_small_n": (_lib.OPT_K2W_SMALL_N, int),
+    "k2w_fold": (_lib.OPT_K2W_FOLD, None),
+    "k2w_tw": (_lib.OPT_K2W_TW, int),
+    "k2w_onepass": (_lib.OPT_K2W_ONEPASS, None),
 }
 
 
@@ -109,6 +116,9 @@ def set_option(name, value, ctx=None):
       "per_step" (MGS's j + 2 all-reduces, its rounding);
     * ``slab_key`` (True): matrices uploaded afterwards order the row blocks of a slab by their
       rows' position, so a slab's DoF groups are walked side by side (False: group after group);
+    * ``gram_inc``, ``x0_zero_test``, ``transpose_pipe`` (True), ``k2w_small_n`` (-1), ``k2w_fold``
+      (True), ``k2w_tw`` (-1), ``k2w_onepass`` (True): A/B switches of parity tests, each
+      bitwise-neutral or within roundoff (include/spis.h SPIS_OPT_GRAM_INC ..);
     * ``verify_uploads`` (True): solver calls that take a SciPy matrix check its full content
       against the cached HBM copy (see :func:`device_matrix`); False trusts identity and buffer
       addresses only (then call :func:`invalidate` after an in-place change)."""
@@ -123,7 +133,7 @@ def set_option(name, value, ctx=None):
         _VERIFY = bool(value)
         return
     opt, names = _OPTIONS[name]
-    v = names[value] if names is not None else int(bool(value))
+    v = int(value) if names is int else names[value] if names is not None else int(bool(value))
     _lib.check(ctx.L.spis_set_option(ctx.handle, opt, v), "spis_set_option")
 
 
@@ -302,7 +312,10 @@ def _as_csr(A):
 # ---- upload caches --------------------------------------------------------------------------
 _MATRIX_CACHE: dict = {}
 _VERIFY = True  # set_option("verify_uploads", ...)
-_HASH_THREADS = max(1, min(8, len(os.sched_getaffinity(0))))
+# host threads of the content scans (a persistent pool in libspis, hash.cpp): the C3 operator
+# and energy matrix (~0.3 GB) are re-verified within one solve's time at ~16 threads; a GPU box
+# grants one process about 16 cores
+_HASH_THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
 _ASYNC_MIN_BYTES = 1 << 22  # smaller matrices are re-verified inline (a thread hand-off costs more)
 
 
@@ -325,7 +338,32 @@ def content_digest(A):
 
 
 def _nbytes(A):
+    if isinstance(A, np.ndarray):
+        return A.nbytes
     return A.data.nbytes + A.indices.nbytes + A.indptr.nbytes
+
+
+def vector_digest(v):
+    """Digest of a host vector's full contents (spis_host_hash over every byte) and length."""
+    L = _lib.load_library()
+    out = C.c_uint64()
+    a = np.ascontiguousarray(v, dtype=np.float64)
+    _lib.check(L.spis_host_hash(C.c_void_p(a.ctypes.data), a.nbytes, _HASH_THREADS, C.byref(out)), "spis_host_hash")
+    return hash((a.size, out.value))
+
+
+def host_nonzero(v, bitwise=False):
+    """``bool(np.any(v))`` for a float vector (``bitwise``: any bit set, so -0.0 counts), on the
+    library's scan (stops at the first nonzero entry; an all-zero vector is read on up to
+    _HASH_THREADS threads; numpy's ``any`` reads every entry on one)."""
+    a = np.asarray(v)
+    if a.dtype != np.float64 or not a.flags.c_contiguous or a.ndim != 1:
+        return bool(np.any(a.view(np.uint64) if bitwise and a.dtype == np.float64 else a))
+    L = _lib.load_library()
+    r = C.c_int32(0)
+    _lib.check(L.spis_host_nonzero(C.c_void_p(a.ctypes.data), a.size, 1 if bitwise else 0, _HASH_THREADS,
+                                   C.byref(r)), "spis_host_nonzero")
+    return bool(r.value)
 
 
 class _Checker:
@@ -341,7 +379,7 @@ class _Checker:
         while True:
             chk = self.q.get()
             try:
-                chk.result = content_digest(chk.A) == chk.digest
+                chk.result = chk.digest_fn(chk.A) == chk.digest
             except BaseException as e:  # re-raised by the caller's ok()
                 chk.result = e
             chk.done.set()
@@ -351,27 +389,40 @@ _CHECKER = None
 
 
 class PendingCheck:
-    """The re-verification of one cached object against its digest (``ok()`` waits for it)."""
+    """The re-verification of one cached object against its digest, queued on the verifier thread
+    when it is made (the digests of a call's operators then overlap its uploads and its solve;
+    starting them only at spis_solve measured 0.6 ms of unhidden wait per C3 call on a box whose
+    host hashes A and L in 2.7 ms); ``ok()`` waits for it."""
 
-    def __init__(self, A, digest, cache, key):
-        global _CHECKER
-        self.A, self.digest, self.cache, self.key = A, digest, cache, key
+    def __init__(self, A, digest, cache, key, digest_fn=None):
+        self.A, self.digest = A, digest
+        self.entries = [(cache, key)]  # every cache entry this one digest vouches for
+        self.digest_fn = digest_fn or content_digest
         self.result = None
         self.done = threading.Event()
-        if _CHECKER is None:
-            _CHECKER = _Checker()
-        _CHECKER.q.put(self)
+        self.started = False
+        self.start()
+
+    def start(self):
+        global _CHECKER
+        if not self.started:
+            self.started = True
+            if _CHECKER is None:
+                _CHECKER = _Checker()
+            _CHECKER.q.put(self)
 
     def ok(self):
+        self.start()
         self.done.wait()
         if isinstance(self.result, BaseException):
             raise self.result
-        if not self.result:  # stale: the next lookup rebuilds the entry
-            self.cache.pop(self.key, None)
+        if not self.result:  # stale: the next lookup rebuilds the entries
+            for cache, key in self.entries:
+                cache.pop(key, None)
         return self.result
 
 
-def _cached(cache, key, A, make, checks=None):
+def _cached(cache, key, A, make, checks=None, digest_fn=None, owner=None):
     """Per-object cache entry ``key -> (digest, value)``, evicted when ``A`` is collected (so a later
     object that reuses ``id(A)`` can never hit it).  A hit is re-verified against the full
     contents: inline, or, when ``checks`` is a list and the arrays are large, by a
@@ -383,18 +434,23 @@ def _cached(cache, key, A, make, checks=None):
         if not _VERIFY:
             return hit[1]
         if checks is not None and _nbytes(A) >= _ASYNC_MIN_BYTES:
-            checks.append(PendingCheck(A, hit[0], cache, key))
+            for chk in checks:  # one digest per object and call (the zero test and the upload of
+                # one constraint matrix share it)
+                if chk.A is A and chk.digest == hit[0]:
+                    chk.entries.append((cache, key))
+                    return hit[1]
+            checks.append(PendingCheck(A, hit[0], cache, key, digest_fn))
             return hit[1]
-        dig = content_digest(A)
+        dig = (digest_fn or content_digest)(A)
         if dig == hit[0]:
             return hit[1]
     val = make()
     if hit is None:
         try:
-            weakref.finalize(A, cache.pop, key, None)
+            weakref.finalize(A if owner is None else owner, cache.pop, key, None)
         except TypeError:  # not weak-referenceable: keep until invalidate()
             pass
-    cache[key] = (content_digest(A) if dig is None else dig, val)
+    cache[key] = ((digest_fn or content_digest)(A) if dig is None else dig, val)
     return val
 
 
@@ -519,13 +575,13 @@ def is_zero_matrix(M, checks=None):
         return True
     if M.format not in ("csr", "csc"):
         return not np.any(M.data)
-    return _cached(_ZERO_CACHE, _matrix_key(M), M, lambda: not np.any(M.data), checks)
+    return _cached(_ZERO_CACHE, _matrix_key(M), M, lambda: not host_nonzero(M.data), checks)
 
 
 def invalidate(A=None):
     """Forget cached uploads and zero tests (of ``A``, or all).  Not needed for correctness (every
     call re-verifies the full contents); it frees the HBM copy early."""
-    for cache in (_MATRIX_CACHE, _ZERO_CACHE):
+    for cache in (_MATRIX_CACHE, _ZERO_CACHE, _VECTOR_CACHE):
         if A is None:
             cache.clear()
             continue
@@ -534,9 +590,56 @@ def invalidate(A=None):
 
 
 def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
+    """HBM copy of a host vector for one call (b, a nonzero x0): its buffer comes from the
+    context's pool of released ones (DeviceVector.scratch), so a call pays the copy, not a
+    hipMalloc and a hipFree."""
     if isinstance(v, DeviceVector):
         return v
-    return DeviceVector.from_host(v, ctx=ctx, capacity=capacity)
+    if capacity is not None:
+        return DeviceVector.from_host(v, ctx=ctx, capacity=capacity)
+    a = np.ascontiguousarray(v, dtype=np.float64).reshape(-1)
+    return DeviceVector.scratch(ctx or get_context(), a.size).upload(a)
+
+
+_VECTOR_CACHE: dict = {}
+
+
+def _root(a):
+    while isinstance(a.base, np.ndarray):
+        a = a.base
+    return a
+
+
+def cached_vector(v, ctx=None, checks=None) -> DeviceVector:
+    """HBM copy of a host fp64 vector that is part of the problem definition (a constraint's
+    ``v``: the wrappers pass the same ``omega`` on every call, e.g. ``swe/LinearSolver.py:28``),
+    cached like :func:`device_matrix`: keyed on the array's owner and buffer, evicted with the
+    owner, re-verified against a digest of its full contents on every call."""
+    if isinstance(v, DeviceVector):
+        return v
+    ctx = ctx or get_context()
+    a = np.asarray(v)
+    if a.dtype != np.float64 or not a.flags.c_contiguous or a.ndim != 1:
+        return DeviceVector.from_host(a, ctx=ctx)
+    root = _root(a)
+    key = (id(root), root.ctypes.data, a.ctypes.data, a.size, ctx.device)
+    return _cached(_VECTOR_CACHE, key, a, lambda: DeviceVector.from_host(a, ctx=ctx), checks, vector_digest, root)
+
+
+_ZERO_VECTORS: dict = {}
+
+
+def zero_vector(ctx, n) -> DeviceVector:
+    """A length-``n`` all-zero HBM vector per context, made once: the x0 of a call whose host x0
+    is all zero (the drivers' ``x0 = 0``, e.g. ``swe/TimedSolve.py:37``).  Read-only: no libspis
+    entry point writes its x0 argument."""
+    key = (ctx.token, int(n))
+    z = _ZERO_VECTORS.get(key)
+    if z is None:
+        if len(_ZERO_VECTORS) >= 4:
+            _ZERO_VECTORS.pop(next(iter(_ZERO_VECTORS)))
+        z = _ZERO_VECTORS[key] = DeviceVector.from_host(np.zeros(int(n)), ctx=ctx)
+    return z
 
 
 class DeviceConstraint:

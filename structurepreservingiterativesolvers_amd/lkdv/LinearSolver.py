@@ -9,7 +9,7 @@ import numpy as np
 import scipy.sparse as sps
 
 from .. import solvers
-from .._wrapcache import derived
+from .._wrapcache import derived, zeros
 
 
 class _Constraint:
@@ -19,7 +19,7 @@ class _Constraint:
 
 def constraints(dic, x0):
     A, M, L = dic["A"], dic["M"], dic["L"]
-    zero = np.zeros_like(np.asarray(x0, dtype=np.float64))
+    zero = zeros(len(x0))  # np.zeros_like(x0), shared read-only
     return [
         _Constraint(derived([A], ["zero"], lambda: sps.csr_matrix(A.shape)), np.transpose(dic["omega"]), -dic["m0"]),
         _Constraint(M, zero, -dic["mo0"]),

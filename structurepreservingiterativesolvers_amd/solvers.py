@@ -41,8 +41,9 @@ import scipy.optimize as spo
 import scipy.sparse as sps
 
 from . import _lib
-from .device import (DeviceMatrix, DeviceVector, choose_ilu, device_matrix, device_vector, get_context, is_superlu,
-                     is_zero_matrix)
+from ._wrapcache import is_known_zero
+from .device import (DeviceMatrix, DeviceVector, cached_vector, choose_ilu, device_matrix, device_vector, get_context,
+                     host_nonzero, is_superlu, is_zero_matrix, zero_vector)
 
 log = logging.getLogger("structurepreservingiterativesolvers_amd")
 
@@ -146,10 +147,12 @@ def _constraint_desc(const, n, ctx, checks=None):
             raise ValueError(f"constraint vector has {len(v)} entries, expected {n}")
         keep.append(v)
         vh = v.ptr
-    elif v is not None:
+    elif v is not None and not is_known_zero(v):
         v = np.asarray(v, dtype=np.float64).reshape(-1)
-        if np.any(v):
-            vd = device_vector(v, ctx=ctx)
+        if host_nonzero(v):
+            if len(v) != n:
+                raise ValueError(f"constraint vector has {len(v)} entries, expected {n}")
+            vd = cached_vector(v, ctx=ctx, checks=checks)
             keep.append(vd)
             vh = vd.ptr
     c = getattr(const, "c", 0.0)
@@ -415,7 +418,38 @@ def _cp():
         _CHECKPOINTS.append(time.perf_counter())
 
 
+_PHASES = None  # bench.py: a dict, phase name -> accumulated seconds of the drop-in call's host work
+
+
+def _stamp():
+    if _PHASES is None:
+        return 0.0
+    import time
+
+    return time.perf_counter()
+
+
+def _tick(name, t0):
+    """Accumulate the seconds since ``t0`` under ``name`` when phases are recorded; the new stamp."""
+    if _PHASES is None:
+        return 0.0
+    import time
+
+    t = time.perf_counter()
+    _PHASES[name] = _PHASES.get(name, 0.0) + (t - t0)
+    return t
+
+
 _MAX_STALE_RERUNS = 3
+
+
+def _host_x0(x0, n, ctx):
+    """The device x0 of a host x0: the context's shared zero vector when every entry is +0.0 (the
+    drivers' x0 = 0; no upload), else an upload (-0.0 entries keep their sign in x_j = Z y + x0)."""
+    a = np.asarray(x0)
+    if a.dtype == np.float64 and a.ndim == 1 and a.size == n and not host_nonzero(a, bitwise=True):
+        return zero_vector(ctx, n)
+    return device_vector(a, ctx=ctx)
 
 
 def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
@@ -433,6 +467,7 @@ def _run(method, A, b, x0, k, tol, contol, conlist, pre, timing):
 
 def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     _cp()
+    t_call = tp = _stamp()
     # a device matrix carries its context (distributed rank / communicator); else the default one
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
     # cached uploads of SciPy matrices are re-verified against their full contents on the verifier
@@ -441,8 +476,10 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     Ad = device_matrix(A, ctx=ctx, checks=checks)
     n = Ad.shape[0]
     device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
+    tp = _tick("matrices", tp)
     bd = device_vector(b, ctx=ctx)
-    x0d = device_vector(x0, ctx=ctx)
+    x0d = x0 if isinstance(x0, DeviceVector) else _host_x0(x0, n, ctx)
+    tp = _tick("h2d", tp)
     if len(bd) != n or len(x0d) != n:
         raise ValueError(f"b/x0 length ({len(bd)}, {len(x0d)}) does not match A ({n})")
     k = int(k)
@@ -472,6 +509,7 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
         conls_fn=conls, conls_user=None,
     )
     _cp()
+    tp = _tick("constraints", tp)
     fbuf, ibuf, out = _out_buffers(k)
     fbuf.fill(0.0)
     ibuf.fill(0)
@@ -479,10 +517,14 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     out.steps, out.n_res, out.x_final_dev = 0, 0, xf.ptr
     ws = C.c_void_p()
     _cp()
+    tp = _stamp()
     status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
                               C.byref(out), C.byref(ws))
     _cp()
-    if not all([chk.ok() for chk in checks]):  # an input matrix changed in place since its upload
+    tp = _tick("solve", tp)
+    fresh = all([chk.ok() for chk in checks])
+    tp = _tick("verify_wait", tp)
+    if not fresh:  # an input matrix changed in place since its upload
         if status == _lib.OK and ws.value:
             ctx.L.spis_workspace_release(ws)
         for key in [key for key in _SLSQP_MESSAGES if key[0] == id(ctx)]:  # the discarded run's
@@ -497,11 +539,14 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     br, ev, msg = ibuf[:k].copy(), ibuf[k:2 * k].copy(), ibuf[2 * k:].copy()
     n_iter = out.n_res - 1
     final = xf if device_io else xf.numpy()
+    tp = _tick("d2h", tp)
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
     xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)
     xs.beta = float(res[0])  # ||r0||: with hessenberg(p), the exact LS problem of every step
     xs.stamps = stamps  # host clock: per-iteration / constraint-step stamps, [4k] call start, [4k+1] end
     _cp()
+    _tick("result", tp)
+    _tick("call", t_call)
     return dict(res=res[: out.n_res].copy(), steps=out.steps, branch=br, events=ev, msg=msg,
                 stamps=stamps, x=xs, final=final, n_iter=n_iter, ctx=ctx)
 

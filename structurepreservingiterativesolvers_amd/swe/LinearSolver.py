@@ -7,7 +7,7 @@ import numpy as np
 import scipy.sparse as sps
 
 from .. import solvers
-from .._wrapcache import derived
+from .._wrapcache import derived, zeros
 
 
 class _Constraint:
@@ -19,7 +19,7 @@ def constraints(dic, x0):
     A = dic["A"]
     return [
         _Constraint(derived([A], ["zero"], lambda: sps.csr_matrix(A.shape)), np.transpose(dic["omega"]), -dic["m0"]),
-        _Constraint(dic["L"], np.zeros_like(np.asarray(x0, dtype=np.float64)), -dic["e0"]),
+        _Constraint(dic["L"], zeros(len(x0)), -dic["e0"]),  # np.zeros_like(x0), shared read-only
     ]
 
 

@@ -208,6 +208,36 @@ def test_in_place_edit_of_a_cached_matrix_is_seen(spis, M):
     assert np.array_equal(x3, solve(A.copy(), L.copy()))
 
 
+@pytest.mark.parametrize("M", [30, 210])
+def test_in_place_edit_of_a_cached_constraint_vector_is_seen(spis, M):
+    """The mass constraint's omega is uploaded once per array too (device.cached_vector: the
+    wrapper passes a fresh np.transpose(omega) view each call, swe/LinearSolver.py:28) and
+    re-verified against its full contents on every call (inline below 4 MiB, M = 30; on the
+    verifier thread above, M = 210).  Scaling one entry in place must give the solve of a fresh
+    copy with the same edit, bitwise, and move the constrained step's answer."""
+    from structurepreservingiterativesolvers_amd import device, solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=M)
+    b, om = dic["b"], dic["omega"]
+    x0 = np.zeros_like(b)
+    assert (om.nbytes >= device._ASYNC_MIN_BYTES) == (M == 210)
+
+    def solve(om_):
+        d = solvers.cgmres(dic["A"], b, x0, 20, tol=1e-19, conlist=swe_ls.constraints(dict(dic, omega=om_), x0))
+        return d[0], d[1]["x"].trace[-1][1]
+
+    x1, br1 = solve(om)
+    assert br1 == "con"
+    assert np.array_equal(solve(om)[0], x1)  # the cached copy, verified unchanged
+    nz = np.flatnonzero(om)  # omega weighs the rho DoFs only (the mass integral)
+    om[nz[len(nz) // 2 + 5]] *= 1.0 + 1e-3
+    x2, br2 = solve(om)
+    assert br2 == "con" and not np.array_equal(x2, x1)
+    assert np.array_equal(x2, solve(om.copy())[0])
+
+
 def test_residual_norm_and_blas1(spis):
     from structurepreservingiterativesolvers_amd import primitives as P
 
@@ -288,14 +318,15 @@ def chain_mode(request, spis, monkeypatch):
     one-reduce two-pass MGS with the fused update GEMV (4: the several-GPU kernels on one GPU).
     The default takes the one-reduce MGS in its one-launch form (K2s) for N <= 262,144 (k <= 32):
     "pipelined" forces K2q there
-    (SPIS_K2W_SMALL_N = 0), so both kernels stay covered at every size."""
+    (option k2w_small_n = 0), so both kernels stay covered at every size."""
     from structurepreservingiterativesolvers_amd.device import set_option
 
     if request.param == "pipelined":
-        monkeypatch.setenv("SPIS_K2W_SMALL_N", "0")
+        set_option("k2w_small_n", 0)
     set_option("mgs_chain", request.param)
     yield request.param
     set_option("mgs_chain", True)
+    set_option("k2w_small_n", -1)
 
 
 @pytest.mark.parametrize("name", names())
@@ -511,7 +542,7 @@ def test_fused_dual_spmv_bit_identical(spis):
     chain, where the update GEMV runs on the side stream); the default's one-reduce MGS at these
     small N to roundoff (its fused GEMV sums in another order)."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
-    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.device import get_context, set_option
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
 
@@ -526,10 +557,7 @@ def test_fused_dual_spmv_bit_identical(spis):
             c = Case("lkdv_m50_cgmres_tol1e-19")
             A, b, cons = c.A, c.b, c.conlist()
         for chain, small in ((3, None), (3, "0"), (2, None)):  # (3, "0"): K2q at these small N
-            if small is None:
-                os.environ.pop("SPIS_K2W_SMALL_N", None)
-            else:
-                os.environ["SPIS_K2W_SMALL_N"] = small
+            set_option("k2w_small_n", -1 if small is None else int(small))
             runs = []
             for fuse in (0, 1):
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
@@ -552,7 +580,7 @@ def test_fused_dual_spmv_bit_identical(spis):
                 continue
             for a, bb in zip(runs[0], runs[1]):
                 assert np.array_equal(a, bb), (case, chain, small)
-        os.environ.pop("SPIS_K2W_SMALL_N", None)
+        set_option("k2w_small_n", -1)
         outs.append(case)
     assert outs == ["swe", "lkdv"]
 
@@ -683,7 +711,7 @@ def test_swe_vs_oracle_medium(spis, M, k, tol):
 
 
 @pytest.mark.parametrize("method", ["cgmres_tol1e-9", "cgmres_p"])
-def test_incremental_constraint_gram(spis, method, monkeypatch):
+def test_incremental_constraint_gram(spis, method, request):
     """The incremental constraint Gram (spis.cpp con_step_*: after a solve's first constrained step,
     each later one reduces only its new basis column, M z_a and [z_0 .. z_a, x0] . M z_a) against
     the full reduction at every constrained step (SPIS_GRAM_INC=0, transpose + K7t each time):
@@ -691,9 +719,11 @@ def test_incremental_constraint_gram(spis, method, monkeypatch):
     (every step constrained, solvers.py:396-401) on swe with mass + energy + the synthetic third
     constraint.  Same branches and steps; the last step's reduced terms to 1e-12 of their scale
     (and not bitwise equal: the other reduction order ran); iterates to 1e-10; the invariants."""
+    from structurepreservingiterativesolvers_amd import device
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
+    request.addfinalizer(lambda: device.set_option("gram_inc", True))
 
     dic, _ = sa.linforms(M=40)
     n = dic["A"].shape[0]
@@ -704,7 +734,7 @@ def test_incremental_constraint_gram(spis, method, monkeypatch):
     k = 24
     runs = []
     for inc in ("0", "1"):
-        monkeypatch.setenv("SPIS_GRAM_INC", inc)
+        device.set_option("gram_inc", inc == "1")
         if method == "cgmres_p":
             x, d = solvers.cgmres_p(dic["A"], dic["b"], x0, k, conlist=cons)
         else:
@@ -734,15 +764,17 @@ def test_incremental_constraint_gram(spis, method, monkeypatch):
 
 
 @pytest.mark.parametrize("M", [40, 97])
-def test_pipelined_transpose_bit_identical(spis, M, monkeypatch):
+def test_pipelined_transpose_bit_identical(spis, M, request):
     """K7t's transpose with the next tile's loads in flight (transpose_basis_pipe_kernel) against the
     one-tile-at-a-time kernel (SPIS_TRANSPOSE_PIPE=0): Ut is a copy and every linear-term partial
     sums its tiles' rows in the same order, so the forced constrained step's terms, the branch, the
     iterates and the residuals are bitwise equal.  swe with mass + energy + the synthetic third
     constraint (a linear term v); M = 97 gives N = 112,908, not a multiple of the 64-row tile."""
+    from structurepreservingiterativesolvers_amd import device
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
+    request.addfinalizer(lambda: device.set_option("transpose_pipe", True))
 
     dic, _ = sa.linforms(M=M)
     n = dic["A"].shape[0]
@@ -752,7 +784,7 @@ def test_pipelined_transpose_bit_identical(spis, M, monkeypatch):
     cons.append(swe_ls._Constraint(D, np.random.default_rng(M).standard_normal(n) * 1e-3, c3))
     runs = []
     for pipe in ("0", "1"):
-        monkeypatch.setenv("SPIS_TRANSPOSE_PIPE", pipe)
+        device.set_option("transpose_pipe", pipe == "1")
         x, d = solvers.cgmres(dic["A"], dic["b"], x0, 20, tol=1e-19, conlist=cons)
         its = d["x"]
         runs.append((np.asarray(x), np.asarray(d["res"]), list(its.trace),
@@ -1385,7 +1417,7 @@ def test_distributed_code_path_self_halo(spis, dist_mgs, gram):
 
 
 @pytest.mark.parametrize("n", [1001, 300_001, 600_002, 1_044_481, 1_048_575, 2_000_001, 3_500_000, 5_000_001, 7_500_001, 10_000_001])
-def test_mgs_chain_matches_per_step_launches(spis, n, monkeypatch):
+def test_mgs_chain_matches_per_step_launches(spis, n, request):
     """K2p / K2b / K2q (SPIS_OPT_MGS_CHAIN): the persistent MGS chains against one launch per MGS step,
     on sizes that select each register tiling (K2p: PER = 2, 4, 8 double2 per thread; K2b, the
     dedicated-gatherer mode beyond 2^20: PER = 8, 16, 24, 32, 40), the largest N K2p takes (odd: a
@@ -1394,10 +1426,11 @@ def test_mgs_chain_matches_per_step_launches(spis, n, monkeypatch):
     agree to 1e-11 relative; the chains are bitwise reproducible run to run; orthogonality as
     MGS's."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
-    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.device import get_context, set_option
 
     ctx = get_context()
-    monkeypatch.setenv("SPIS_K2W_SMALL_N", "0")  # mode 3 is K2q at every n here
+    set_option("k2w_small_n", 0)  # mode 3 is K2q at every n here
+    request.addfinalizer(lambda: set_option("k2w_small_n", -1))
     rng = np.random.default_rng(n)
     A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
                    0.3 * rng.random(n - 7)], [0, -1, 1, 7], format="csr")
@@ -1436,7 +1469,7 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
     reducing workgroup takes several; 1,002,252: the full 1024-workgroup grid at C3's size, with
     the temporal window on and off.  Repeated solves reuse the tag slots (a fresh tag per launch)."""
     from structurepreservingiterativesolvers_amd import _lib, solvers
-    from structurepreservingiterativesolvers_amd.device import get_context
+    from structurepreservingiterativesolvers_amd.device import get_context, set_option
 
     ctx = get_context()
     rng = np.random.default_rng(n)
@@ -1448,15 +1481,14 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
     _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 4), "spis_set_option")
     try:
         for fold, tw in ((0, None), (1, None), (1, None), (1, "0"), (0, "0")):
-            monkeypatch.setenv("SPIS_K2W_FOLD", str(fold))
-            if tw is None:
-                monkeypatch.delenv("SPIS_K2W_TW", raising=False)
-            else:
-                monkeypatch.setenv("SPIS_K2W_TW", tw)
+            set_option("k2w_fold", bool(fold))
+            set_option("k2w_tw", -1 if tw is None else int(tw))
             x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
             runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
     finally:
         _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, 3), "spis_set_option")
+        set_option("k2w_fold", True)
+        set_option("k2w_tw", -1)
     xa, ra, Qa = runs[0]
     assert ra[-1] < 1e-3 * ra[0]
     for xb, rb, Qb in runs[1:]:
@@ -1464,15 +1496,17 @@ def test_k2w_fold_bit_identical(spis, n, monkeypatch):
 
 
 @pytest.mark.parametrize("x0_kind", ["zeros", "negzeros", "nonzero"])
-def test_x0_zero_fast_path_bit_identical(spis, x0_kind, monkeypatch):
+def test_x0_zero_fast_path_bit_identical(spis, x0_kind, request):
     """r0 = b - A x0 with x0 all zeros skips the matrix (spis.cpp: the x0 copy flags a nonzero entry,
     spmv_pipe_kernel MODE 3 reads the flag): on a finite matrix every product is +-0 and every row sum
     +0, so r0 = b bit for bit and the ||r0||^2 partials are the full path's.  The whole constrained
     solve (C3's shape at M = 30) bitwise equal with the test on and off (SPIS_X0_ZERO_TEST=0), for
     +0 and -0 zeros and for a nonzero x0 (the flag set: the full SpMV either way); and x[0] = b."""
+    from structurepreservingiterativesolvers_amd import device
     from structurepreservingiterativesolvers_amd import solvers
     from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
     from structurepreservingiterativesolvers_amd.swe import assembly as sa
+    request.addfinalizer(lambda: device.set_option("x0_zero_test", True))
 
     dic, _ = sa.linforms(M=30)
     n = dic["A"].shape[0]
@@ -1481,7 +1515,7 @@ def test_x0_zero_fast_path_bit_identical(spis, x0_kind, monkeypatch):
     cons = swe_ls.constraints(dic, np.zeros(n))
     runs = []
     for flag in ("1", "0", "1"):
-        monkeypatch.setenv("SPIS_X0_ZERO_TEST", flag)
+        device.set_option("x0_zero_test", flag == "1")
         x, d = solvers.cgmres(dic["A"], dic["b"], x0, 20, tol=1e-19, conlist=cons)
         runs.append((np.asarray(x), np.asarray(d["res"]), np.asarray(d["x"][0]), list(d["x"].trace)))
     for r in runs[1:]:
@@ -1492,10 +1526,10 @@ def test_x0_zero_fast_path_bit_identical(spis, x0_kind, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [65_536, 100_002, 196_608, 1001, 300_006, 393_216])
-def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
+def test_k2s_onepass_vs_two_pass(spis, n):
     """K2s (small N, one GPU: K2w's dots, coefficients, update with the fused GEMV, norm and
     normalise in one launch over register-resident basis slices) against K2w's launches
-    (SPIS_K2W_ONEPASS = 0): the same grouping of every partial for n a multiple of 256, and at
+    (option k2w_onepass = False): the same grouping of every partial for n a multiple of 256, and at
     every n that is a multiple of 256 (65,536 and 196,608 here) bitwise equal, otherwise the last
     chunk is grouped differently: roundoff.  (Until round 5 one step's ||w'|| at 196,608 came out one
     ulp apart: hipcc had contracted different multiply-adds into FMAs in the one-pass and the
@@ -1505,6 +1539,7 @@ def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     two chunks, the second streamed (300,006 and 393,216 here): its dot and norm partials carry both
     chunks, so the grouping differs from the two-pass kernels' at every n: roundoff."""
     from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.device import set_option
 
     rng = np.random.default_rng(n)
     A = sps.diags([4.0 + rng.random(n), -1.0 - 0.1 * rng.random(n - 1), -1.0 + 0.1 * rng.random(n - 1),
@@ -1512,10 +1547,13 @@ def test_k2s_onepass_vs_two_pass(spis, n, monkeypatch):
     b = rng.standard_normal(n)
     k = 12
     runs = []
-    for onepass in (0, 1, 1):
-        monkeypatch.setenv("SPIS_K2W_ONEPASS", str(onepass))
-        x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
-        runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
+    try:
+        for onepass in (0, 1, 1):
+            set_option("k2w_onepass", bool(onepass))
+            x, d = solvers.gmres(A, b, np.zeros(n), k, tol=1e-50)
+            runs.append((np.asarray(x), np.asarray(d["res"]), d["x"].basis(k)))
+    finally:
+        set_option("k2w_onepass", True)
     xa, ra, Qa = runs[0]
     assert ra[-1] < 1e-3 * ra[0]
     assert all(np.array_equal(p, q) for p, q in zip(runs[1], runs[2]))  # run to run

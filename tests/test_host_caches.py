@@ -135,3 +135,65 @@ def test_host_hash_independent_of_threads():
     a[12345] = np.nextafter(a[12345], 2.0)
     _lib.check(L.spis_host_hash(C.c_void_p(a.ctypes.data), a.nbytes, 4, C.byref(h2)), "spis_host_hash")
     assert h2.value not in outs
+
+
+def test_host_nonzero_matches_numpy_truthiness():
+    """spis_host_nonzero is np.any on fp64 entries: -0.0 is zero, NaN and subnormals are not; a
+    lone nonzero anywhere (head, a pooled piece, the ragged tail) is found."""
+    n = (3 << 20) + 77  # head + several 1 MiB pieces + a tail
+    z = np.zeros(n)
+    assert device.host_nonzero(z) is False
+    z[::3] = -0.0
+    assert device.host_nonzero(z) is False and bool(np.any(z)) is False
+    for pos in (0, 4095, 4096, n // 2, n - 1):
+        for val in (1.0, np.nan, 5e-324, -np.inf):
+            w = np.zeros(n)
+            w[pos] = val
+            assert device.host_nonzero(w) is True, (pos, val)
+    assert device.host_nonzero(np.zeros(0)) is False
+    assert device.host_nonzero(np.zeros(10)[::2]) is False  # non-contiguous: numpy's own any
+    assert device.host_nonzero(np.arange(10.0)[::2]) is True
+
+
+def test_host_hash_concurrent_callers():
+    """Two threads hashing at once (the verifier thread and an inline check) both get the
+    digest a lone caller gets: one of them runs on the pool, the other on its own thread."""
+    import threading
+
+    rng = np.random.default_rng(3)
+    arrs = [rng.random(5 << 20) for _ in range(2)]
+    want = [device.vector_digest(a) for a in arrs]
+    got = [[], []]
+
+    def worker(i):
+        for _ in range(5):
+            got[i].append(device.vector_digest(arrs[i]))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got[0] == [want[0]] * 5 and got[1] == [want[1]] * 5
+
+
+def test_vector_cache_keyed_on_owner():
+    """A constraint vector passed as a fresh view each call (np.transpose(omega),
+    swe/LinearSolver.py:28) keys on its owner: the entry lives as long as omega, not the view."""
+    key_of = lambda a: (id(device._root(a)), device._root(a).ctypes.data, a.ctypes.data, a.size)  # noqa: E731
+    omega = np.random.default_rng(1).random(1000)
+    v1, v2 = np.transpose(omega), np.transpose(omega)
+    assert v1 is not v2 and key_of(v1) == key_of(v2) == (id(omega), omega.ctypes.data, omega.ctypes.data, 1000)
+
+
+def test_host_nonzero_bitwise_counts_negative_zero():
+    """The x0 test is bitwise: an x0 of -0.0 entries is uploaded as given (its sign reaches
+    x_j = Z y + x0), only +0.0 entries take the shared zero vector."""
+    n = (2 << 20) + 3
+    z = np.zeros(n)
+    assert device.host_nonzero(z, bitwise=True) is False
+    for pos in (0, 5000, n - 1):
+        w = np.zeros(n)
+        w[pos] = -0.0
+        assert device.host_nonzero(w, bitwise=True) is True
+        assert device.host_nonzero(w) is False

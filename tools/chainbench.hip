@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
   // the chain reads w and never writes it: repeated launches see the same inputs
   if (argc > 3 && std::string(argv[3]) == "trace") {  // phase timestamps of K2q + FX (the solver's chain)
     set_chain_lag(2);
-    for (int j : {1, 5, 15, 29}) {
+    for (int j : {1, 2, 5, 15, 29}) {
       auto run = [&]() {
         CK(launch_mgs_chain(n, w, Q, pitch, j, part, 1024, hcol_dev, gran, ep, err, s, nullptr, nullptr, 0, nullptr,
                             nullptr, nullptr, true, 1, gsub, y.data(), j, x0, xo));
