@@ -300,6 +300,11 @@ int spis_malloc(spis_context* ctx, int64_t bytes, void** dev_out);
 int spis_free(spis_context* ctx, void* dev);
 int spis_memcpy_h2d(spis_context* ctx, void* dst_dev, const void* src_host, int64_t bytes);
 int spis_memcpy_d2h(spis_context* ctx, void* dst_host, const void* src_dev, int64_t bytes);
+/* Page-locked host memory (hipHostMalloc): the drop-in returns x[-1] in such a buffer (device.py
+ * keeps a few per length and recycles them when the caller drops the array), so its download is
+ * one DMA at the link's rate instead of a staged pageable copy. */
+int spis_host_alloc(int64_t bytes, void** host_out);
+int spis_host_free(void* host);
 
 /* y = A x (x must hold n_rows + n_ghost entries; ghosts are exchanged first) */
 int spis_spmv(spis_context* ctx, spis_matrix* A, double* x_dev, double* y_dev);

@@ -154,6 +154,8 @@ SIGNATURES = [
     ("spis_free", C.c_int, [_VP, _VP]),
     ("spis_memcpy_h2d", C.c_int, [_VP, _VP, _VP, _I64]),
     ("spis_memcpy_d2h", C.c_int, [_VP, _VP, _VP, _I64]),
+    ("spis_host_alloc", C.c_int, [_I64, C.POINTER(_VP)]),
+    ("spis_host_free", C.c_int, [_VP]),
     ("spis_spmv", C.c_int, [_VP, _VP, _VP, _VP]),
     ("spis_residual_norm", C.c_int, [_VP, _VP, _VP, _VP, _PD]),
     ("spis_dot", C.c_int, [_VP, _I64, _VP, _VP, _PD]),

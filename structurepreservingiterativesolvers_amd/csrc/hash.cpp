@@ -14,6 +14,7 @@
 // to a persistent pool of workers (created on first use; a call that finds the pool busy — the
 // verifier thread and the caller's thread hashing at once — runs on its own thread), so a scan of
 // the C3 operator (~154 MB) pays no thread start-up and no core waits on a slower one's share.
+// The digests and the zero scans have a pool each.
 //
 // The zero test (spis_host_nonzero) is numpy's truthiness of every fp64 entry (-0.0 counts as
 // zero, NaN as nonzero; solvers.py drops an all-zero constraint vector, its v.Z term being 0) or
@@ -87,9 +88,12 @@ bool piece_nonzero(const uint64_t* p, int64_t n, bool bitwise) {
 // piece claimed from an atomic counter by whichever thread (the caller included) is free.
 class Pool {
  public:
-  static Pool& get() {
-    static Pool* p = new Pool();  // never destroyed: workers may outlive static destructors
-    return *p;
+  // one pool per kind of caller (0: the digests, run on the verifier thread; 1: the zero scans of
+  // the calling thread), so a scan never finds the pool held by a digest of a cached operator and
+  // runs alone, nor a digest by a scan
+  static Pool& get(int which) {
+    static Pool* p[2] = {new Pool(), new Pool()};  // never destroyed: workers may outlive static destructors
+    return *p[which & 1];
   }
 
   // false when another caller holds the pool (the caller then runs the job alone)
@@ -160,8 +164,8 @@ class Pool {
   uint64_t gen_ = 0;
 };
 
-void for_pieces(int threads, int64_t n_pieces, const std::function<void(int64_t)>& job) {
-  if (threads > 1 && n_pieces >= 4 && Pool::get().run(threads, n_pieces, job)) return;
+void for_pieces(int pool, int threads, int64_t n_pieces, const std::function<void(int64_t)>& job) {
+  if (threads > 1 && n_pieces >= 4 && Pool::get(pool).run(threads, n_pieces, job)) return;
   for (int64_t k = 0; k < n_pieces; ++k) job(k);
 }
 
@@ -173,7 +177,7 @@ extern "C" int spis_host_hash(const void* data, int64_t bytes, int32_t threads, 
   const int64_t np = (bytes + kPiece - 1) / kPiece;
   try {
     std::vector<uint64_t> d(static_cast<size_t>(std::max<int64_t>(np, 1)), 0);
-    for_pieces(threads, np, [&](int64_t k) {
+    for_pieces(0, threads, np, [&](int64_t k) {
       const int64_t o = k * kPiece;
       d[k] = piece_digest(p + o, std::min(kPiece, bytes - o), static_cast<uint64_t>(k));
     });
@@ -203,7 +207,7 @@ extern "C" int spis_host_nonzero(const double* data, int64_t count, int32_t bitw
   const int64_t rest = count - kHead, np = (rest + kEl - 1) / kEl;
   std::atomic<int> found{0};
   try {
-    for_pieces(threads, np, [&](int64_t k) {
+    for_pieces(1, threads, np, [&](int64_t k) {
       if (found.load(std::memory_order_relaxed)) return;
       const int64_t o = kHead + k * kEl;
       if (piece_nonzero(w + o, std::min(kEl, count - o), bitwise != 0)) found.store(1, std::memory_order_relaxed);

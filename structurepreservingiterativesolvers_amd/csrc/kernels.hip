@@ -864,6 +864,10 @@ constexpr int kChainThreads = kBlock + 64;  // 4 data waves + 1 exchange wave
 // sum_partials' exact arithmetic (same per-thread loop, same shuffle wave sums, same combine) on
 // the 4 data waves, with the exchange wave joining the barriers: the first h and the piggybacked
 // residual get the same bits as from the per-step kernels and finalize_kernel
+// s_waitcnt vmcnt(0) alone (gfx9 encoding: vmcnt [3:0] + [15:14] = 0, expcnt and lgkmcnt at
+// their max): every load of the wave, LDS DMA (global_load_lds) included, has completed
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8)); }
+
 __device__ __forceinline__ double chain_sum_partials(const double* __restrict__ part, int n, double* s_wave) {
   const int tid = threadIdx.x;
   double v = 0.0;
@@ -1126,15 +1130,13 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       if (data && p0 + k * DT < npair) r[k] = ld_basis(v2 + p0 + k * DT, nt);
   };
   // start-up: the data workgroups issue their loads in the order of need (loads complete in issue
-  // order): x0 (stored to LDS as soon as it arrives: that wait covers x0 alone), w and q_1, q_2
-  // (step 0's dots), q_0 (step 1's update), the rest of the ring.  h_0 = q_0 . w (the SpMV's
+  // order): w and q_1, q_2 (step 0's dots), q_0 (step 1's update), the rest of the ring, then x0
+  // by LDS DMA (read at the last step only).  h_0 = q_0 . w (the SpMV's
   // partials) and the piggybacked residual are summed by the gatherer, which has no basis loads to
   // queue behind; h_0 reaches the data workgroups through the exchange slots (E_0) when step 1's
   // update needs it.  The first exchange then starts after four vectors have arrived, not after
   // six vectors and two partial sums behind them.
   if (!agg) {
-    double2 xr[PER];
-    if (FX) load(xr, x0, NT && tw == 0);
     if (FX && data) {
 #pragma unroll
       for (int k = 0; k < PER; ++k) s_acc[k * DT + tid] = make_double2(0.0, 0.0);
@@ -1144,10 +1146,15 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     for (int m = 1; m < NS - 1; ++m)
       if (m <= j) load(S[m], Q + static_cast<int64_t>(m) * pitch, NT && m >= tw);
     load(S[0], Q, NT && 0 >= tw);
-    if (FX && data) {  // x0 into LDS (added at the end: its load latency off the tail)
+    if (FX && data) {  // x0 straight into LDS (global_load_lds: no registers, nothing waits on it
+                       // before the last step, which drains it: vm_drain)
+      const double2* x02 = reinterpret_cast<const double2*>(x0);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (p0 + k * DT < npair) s_x0[k * DT + tid] = xr[k];
+        if (p0 + k * DT < npair)
+          __builtin_amdgcn_global_load_lds(x02 + p0 + k * DT,
+                                           (__attribute__((address_space(3))) void*)(s_x0 + k * DT + (tid & ~63)), 16,
+                                           0, 0);
     }
   }
   if (tid == 0) s_fail = 0;
@@ -1161,7 +1168,8 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       if (tid == 0) publish(x_out, t, flag, seq);
     }
     if (tid == 0) {  // E_0: h_0 in h slot 0 under tag base (slot 0's next use, E_4, is published
-                     // after every workgroup has read h_0 at its step 1, before its E_4 partials)
+                     // after every workgroup has read h_0 at its step 1, before its E_4 partials;
+                     // the caller's tag base is never 0, the zero-initialised slots' tag)
       const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(h0));
       chain_store(hslots, base, static_cast<unsigned>(bits));
       chain_store(hslots + 1, base, static_cast<unsigned>(bits >> 32));
@@ -1366,6 +1374,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     if (i == j) {  // last: subtract h_j q_j, ||w||^2 through the gatherer, normalise
       if (FX) {  // x is complete (its last term, q_{px-1}, passed at step j - 1): stored now, its
                  // write drains during the two exchanges still ahead instead of after them
+        vm_drain();  // x0's LDS DMA (issued after the ring's first loads) has landed
         double2* xo2 = reinterpret_cast<double2*>(xo);
 #pragma unroll
         for (int k = 0; k < PER; ++k)

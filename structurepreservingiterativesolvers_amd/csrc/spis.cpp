@@ -600,6 +600,11 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipMemset(c->chain_gsub, 0, sizeof(double) * kChainGsub));
     HIP_TRY(hipMalloc(&c->chain_epoch, 16));
     HIP_TRY(hipMemset(c->chain_epoch, 0, 16));
+    {  // the tag base starts at 1: K2q's E_0 carries tag base + 0, which must never equal the 0
+       // tags of the zero-initialised exchange slots
+      const unsigned one = 1;
+      HIP_TRY(hipMemcpy(c->chain_epoch, &one, sizeof one, hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->chain_err), 16, hipHostMallocMapped));
     *c->chain_err = 0;
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->chain_err_dev), c->chain_err, 0));
@@ -1346,12 +1351,14 @@ extern "C" int spis_free(spis_context* c, void* p) {
   })
 }
 
+// the copies finish by an event spin (a blocking stream synchronize wakes the host up tens of us
+// late: a drop-in call downloads x and uploads b each time)
 extern "C" int spis_memcpy_h2d(spis_context* c, void* dst, const void* src, int64_t bytes) {
   ABI_GUARD({
     if (!c || (bytes > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
     if (bytes > 0) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return SPIS_OK;
+    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));
+    return wait_event(c->ev_gram);
   })
 }
 
@@ -1359,7 +1366,23 @@ extern "C" int spis_memcpy_d2h(spis_context* c, void* dst, const void* src, int6
   ABI_GUARD({
     if (!c || (bytes > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
     if (bytes > 0) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));
+    return wait_event(c->ev_gram);
+  })
+}
+
+extern "C" int spis_host_alloc(int64_t bytes, void** out) {
+  ABI_GUARD({
+    if (!out || bytes < 0) return fail(SPIS_ERR_ARG, "bad argument");
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, static_cast<size_t>(std::max<int64_t>(bytes, 8)), hipHostMallocDefault));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_host_free(void* p) {
+  ABI_GUARD({
+    if (p) HIP_TRY(hipHostFree(p));
     return SPIS_OK;
   })
 }

@@ -181,12 +181,58 @@ class DeviceBuffer:
                                               8 * a.size), "spis_memcpy_h2d")
         return self
 
-    def download(self, n=None):
+    def download(self, n=None, pinned=False):
+        """The first ``n`` entries as a new host array (``pinned``: in a page-locked buffer from
+        :func:`pinned_empty` when one is free or may be made, a pageable one otherwise)."""
         n = self.n if n is None else int(n)
-        out = np.empty(n, dtype=np.float64)
+        out = pinned_empty(n) if pinned else None
+        if out is None:
+            out = np.empty(n, dtype=np.float64)
         _lib.check(self.ctx.L.spis_memcpy_d2h(self.ctx.handle, out.ctypes.data_as(C.c_void_p),
                                               C.c_void_p(self.ptr), 8 * n), "spis_memcpy_d2h")
         return out
+
+
+# page-locked host buffers for returned iterates: a C3 x (8 MB) comes down at the link's rate in
+# one DMA instead of through the runtime's pageable staging.  At most _PINNED_MAX live buffers per
+# length; a buffer goes back to its free list when the caller drops the last view of the array
+# (so a loop that keeps each result for one step alternates between two), and past the cap (a
+# caller that keeps every result) downloads go to ordinary arrays.
+_PINNED_FREE: dict = {}
+_PINNED_LIVE: dict = {}
+_PINNED_MAX = 4
+
+
+def _pinned_release(n, ptr):
+    _PINNED_LIVE[n] = _PINNED_LIVE.get(n, 1) - 1
+    if len(_PINNED_FREE.setdefault(n, [])) < _PINNED_MAX:
+        _PINNED_FREE[n].append(ptr)
+        _PINNED_LIVE[n] += 1  # still allocated, now idle
+    else:
+        _lib.load_library().spis_host_free(C.c_void_p(ptr))
+
+
+def pinned_empty(n):
+    """A length-``n`` fp64 array in page-locked host memory, or None past the cap."""
+    n = int(n)
+    free = _PINNED_FREE.get(n)
+    ptr = None
+    if free:
+        try:
+            ptr = free.pop()
+        except IndexError:
+            ptr = None
+    if ptr is None:
+        if _PINNED_LIVE.get(n, 0) >= _PINNED_MAX:
+            return None
+        p = C.c_void_p()
+        if _lib.load_library().spis_host_alloc(8 * max(n, 1), C.byref(p)) != _lib.OK or not p.value:
+            return None
+        ptr = p.value
+        _PINNED_LIVE[n] = _PINNED_LIVE.get(n, 0) + 1
+    arr = np.ctypeslib.as_array((C.c_double * max(n, 1)).from_address(ptr))[:n]
+    weakref.finalize(arr.base, _pinned_release, n, ptr)
+    return arr
 
 
 # recycled allocations of solver outputs (DeviceVector.scratch): a solve's result vector is
@@ -610,20 +656,25 @@ def _root(a):
     return a
 
 
-def cached_vector(v, ctx=None, checks=None) -> DeviceVector:
+def cached_vector(v, ctx=None, checks=None):
     """HBM copy of a host fp64 vector that is part of the problem definition (a constraint's
     ``v``: the wrappers pass the same ``omega`` on every call, e.g. ``swe/LinearSolver.py:28``),
-    cached like :func:`device_matrix`: keyed on the array's owner and buffer, evicted with the
-    owner, re-verified against a digest of its full contents on every call."""
+    or None when every entry is zero (np.any's sense: solvers.py drops such a term), cached like
+    :func:`device_matrix`: keyed on the array's owner and buffer, evicted with the owner,
+    re-verified against a digest of its full contents on every call."""
     if isinstance(v, DeviceVector):
         return v
     ctx = ctx or get_context()
     a = np.asarray(v)
+
+    def make():
+        return DeviceVector.from_host(a, ctx=ctx) if host_nonzero(a) else None
+
     if a.dtype != np.float64 or not a.flags.c_contiguous or a.ndim != 1:
-        return DeviceVector.from_host(a, ctx=ctx)
+        return make()
     root = _root(a)
     key = (id(root), root.ctypes.data, a.ctypes.data, a.size, ctx.device)
-    return _cached(_VECTOR_CACHE, key, a, lambda: DeviceVector.from_host(a, ctx=ctx), checks, vector_digest, root)
+    return _cached(_VECTOR_CACHE, key, a, make, checks, vector_digest, root)
 
 
 _ZERO_VECTORS: dict = {}

@@ -149,10 +149,10 @@ def _constraint_desc(const, n, ctx, checks=None):
         vh = v.ptr
     elif v is not None and not is_known_zero(v):
         v = np.asarray(v, dtype=np.float64).reshape(-1)
-        if host_nonzero(v):
-            if len(v) != n:
-                raise ValueError(f"constraint vector has {len(v)} entries, expected {n}")
-            vd = cached_vector(v, ctx=ctx, checks=checks)
+        if len(v) != n and host_nonzero(v):
+            raise ValueError(f"constraint vector has {len(v)} entries, expected {n}")
+        vd = cached_vector(v, ctx=ctx, checks=checks) if len(v) == n else None  # None: all zero
+        if vd is not None:
             keep.append(vd)
             vh = vd.ptr
     c = getattr(const, "c", 0.0)
@@ -472,14 +472,16 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     ctx = A.ctx if isinstance(A, DeviceMatrix) else get_context()
     # cached uploads of SciPy matrices are re-verified against their full contents on the verifier
     # thread while the solve runs (device.PendingCheck); a stale one makes the call run again
+    device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
+    # b and x0 first: the cached operators' digests (started by the lookups below) then share the
+    # host's memory bandwidth with the solve, not with these copies
+    bd = device_vector(b, ctx=ctx)
+    x0d = x0 if isinstance(x0, DeviceVector) else _host_x0(x0, int(A.shape[0]), ctx)
+    tp = _tick("h2d", tp)
     checks = []
     Ad = device_matrix(A, ctx=ctx, checks=checks)
     n = Ad.shape[0]
-    device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
     tp = _tick("matrices", tp)
-    bd = device_vector(b, ctx=ctx)
-    x0d = x0 if isinstance(x0, DeviceVector) else _host_x0(x0, n, ctx)
-    tp = _tick("h2d", tp)
     if len(bd) != n or len(x0d) != n:
         raise ValueError(f"b/x0 length ({len(bd)}, {len(x0d)}) does not match A ({n})")
     k = int(k)
@@ -538,7 +540,7 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     res, ys, stamps = fbuf[:k + 1].copy(), fbuf[k + 1:k + 1 + k * k].copy(), fbuf[k + 1 + k * k:].copy()
     br, ev, msg = ibuf[:k].copy(), ibuf[k:2 * k].copy(), ibuf[2 * k:].copy()
     n_iter = out.n_res - 1
-    final = xf if device_io else xf.numpy()
+    final = xf if device_io else xf.download(n, pinned=True)
     tp = _tick("d2h", tp)
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
     xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)

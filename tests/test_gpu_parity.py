@@ -1564,3 +1564,29 @@ def test_k2s_onepass_vs_two_pass(spis, n):
         assert np.linalg.norm(xa - xb) <= 1e-12 * np.linalg.norm(xa)
         np.testing.assert_allclose(rb, ra, rtol=1e-9, atol=1e-14 * ra[0])
         np.testing.assert_allclose(Qb, Qa, rtol=0, atol=1e-11)
+
+
+def test_first_chain_of_a_process_matches_later_ones(spis):
+    """The first K2q chain of a fresh process (its context's first exchange tags) gives the same
+    solve, bitwise, as every later one: swe at M = 210 (N = 529,200, K2q's pipelined chain), three
+    solves in a new process.  K2q's E_0 (h_0 from the gatherer) carries tag base + 0; a tag base of
+    0 would match the zero-initialised slots before the gatherer wrote them (round 6: the first
+    solve of each process read h_0 = 0)."""
+    import subprocess
+    import sys
+
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import numpy as np, sys\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "from structurepreservingiterativesolvers_amd import solvers\n"
+        "from structurepreservingiterativesolvers_amd.swe import LinearSolver as ls, assembly as sa\n"
+        "dic, _ = sa.linforms(M=210)\n"
+        "x0 = np.zeros_like(dic['b'])\n"
+        "xs = [np.array(solvers.cgmres(dic['A'], dic['b'], x0, 20, tol=1e-19,\n"
+        "      conlist=ls.constraints(dic, x0))[0]) for _ in range(3)]\n"
+        "print('SAME' if all(np.array_equal(x, xs[0]) for x in xs) else 'DIFF')\n"
+    )
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "SAME", out.stdout

@@ -197,3 +197,29 @@ def test_host_nonzero_bitwise_counts_negative_zero():
         w[pos] = -0.0
         assert device.host_nonzero(w, bitwise=True) is True
         assert device.host_nonzero(w) is False
+
+
+@pytest.mark.gpu
+def test_pinned_buffers_recycled_and_capped():
+    """Returned iterates live in page-locked buffers (device.pinned_empty): a dropped array's buffer
+    is reused, every view keeps it alive, and past the cap per length downloads fall back to
+    ordinary arrays (None here)."""
+    n = 1000 + 7
+    a = device.pinned_empty(n)
+    assert a is not None and a.shape == (n,) and a.dtype == np.float64
+    a[:] = 3.0
+    addr = a.ctypes.data
+    view = a[10:20]
+    del a
+    gc.collect()
+    assert (view == 3.0).all()  # the view keeps the buffer
+    del view
+    gc.collect()
+    b = device.pinned_empty(n)
+    assert b.ctypes.data == addr  # recycled
+    held = [b] + [device.pinned_empty(n) for _ in range(device._PINNED_MAX - 1)]
+    assert all(h is not None for h in held)
+    assert device.pinned_empty(n) is None  # capped
+    del held, b
+    gc.collect()
+    assert device.pinned_empty(n) is not None

@@ -50,6 +50,10 @@ int main(int argc, char** argv) {
   CK(hipMemset(gran, 0, sizeof(unsigned long long) * kChainGranLag));
   CK(hipMalloc(&ep, 16));
   CK(hipMemset(ep, 0, 16));
+  {  // tag base 1 (as libspis): K2q's E_0 tag must never be the slots' initial 0
+    const unsigned one = 1;
+    CK(hipMemcpy(ep, &one, sizeof one, hipMemcpyHostToDevice));
+  }
   CK(hipMalloc(&err, 16));
   CK(hipMemset(err, 0, 16));
   double* hcol;

@@ -1,0 +1,30 @@
+"""Debug: repeated identical solves at M=210 must agree bitwise (pinned output on / off)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from structurepreservingiterativesolvers_amd import device, solvers  # noqa: E402
+from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls  # noqa: E402
+from structurepreservingiterativesolvers_amd.swe import assembly as sa  # noqa: E402
+
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 210
+for mode in ("pinned", "pageable", "pinned"):
+    if mode == "pageable":
+        orig = device.pinned_empty
+        device.pinned_empty = lambda n: None
+    dic, _ = sa.linforms(M=M)
+    b, om = dic["b"], dic["omega"]
+    x0 = np.zeros_like(b)
+    xs = []
+    for r in range(4):
+        x, d = solvers.cgmres(dic["A"], b, x0, 20, tol=1e-19, conlist=swe_ls.constraints(dict(dic, omega=om), x0))
+        xs.append((np.array(x, copy=True), x, d["res"][-1], d["x"].trace[-1][1]))
+    for r in range(4):
+        c, live, res, br = xs[r]
+        print(mode, r, br, f"res {res:.6e}", "copy==first", np.array_equal(c, xs[0][0]),
+              "live==copy", np.array_equal(live, c), flush=True)
+    if mode == "pageable":
+        device.pinned_empty = orig
