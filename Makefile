@@ -34,7 +34,7 @@ build/hash.o: $(SRC)/hash.cpp include/spis.h
 
 # the host least squares on x86-64-v3 (AVX2, FMA) with contraction off: the loops vectorise, every
 # product is rounded then added as written, so results are bitwise the baseline build's
-LSQFLAGS := -march=x86-64-v3 -ffp-contract=off
+LSQFLAGS ?= -march=x86-64-v3 -ffp-contract=off
 
 build/lsq.o: $(SRC)/lsq.cpp $(SRC)/lsq.h include/spis.h
 	@mkdir -p build

@@ -137,12 +137,13 @@ def kernels_sha256():
 
 
 def load_traffic(args, c16, pipe):
-    """Per-launch PMC bytes from profiles/r05_traffic_<config>.json (tools/archive/r05_pmc.sh; else r04), with the
+    """Per-launch PMC bytes from profiles/r06_traffic_<config>.json (tools/r06_pmc.sh; else r05, r04), with the
     reason when there are none: the file must have been measured on this csrc/kernels.hip (SHA-256)
     with this run's SpMV and chain options, on the configuration's default size."""
-    path = os.path.join(ROOT, "profiles", f"r05_traffic_{args.config}.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", f"r04_traffic_{args.config}.json")
+    for rnd in ("r06", "r05", "r04"):  # the newest round's file that exists
+        path = os.path.join(ROOT, "profiles", f"{rnd}_traffic_{args.config}.json")
+        if os.path.exists(path):
+            break
     if args.M is not None:
         return {}, "no PMC traffic for a non-default mesh size"
     if not os.path.exists(path):

@@ -99,6 +99,10 @@ int spis_context_stream(spis_context* ctx, void** stream_out);
  * a second host thread beside spis_solve.  The bytes are hashed in 1 MiB pieces on up to
  * `threads` threads; the digest does not depend on the thread count. */
 int spis_host_hash(const void* data, int64_t bytes, int32_t threads, uint64_t* out);
+/* 1 when the host CPU runs the x86-64-v3 code the host least squares is built as (AVX2, FMA,
+ * BMI2: Makefile LSQFLAGS), else 0; the Python loader refuses the library on 0 with a rebuild
+ * hint instead of an illegal instruction at the first constrained step. */
+int spis_host_isa_ok(void);
 /* Whether any of `count` host fp64 entries is nonzero: in numpy's truthiness when `bitwise` is 0
  * (-0.0 is zero, NaN is not: the wrappers drop an all-zero constraint vector), any bit set when 1
  * (an x0 of +0.0 entries needs no upload).  Stops at the first nonzero entry; up to `threads`
@@ -305,6 +309,19 @@ int spis_memcpy_d2h(spis_context* ctx, void* dst_host, const void* src_dev, int6
  * one DMA at the link's rate instead of a staged pageable copy. */
 int spis_host_alloc(int64_t bytes, void** host_out);
 int spis_host_free(void* host);
+/* Page-lock an existing host range (hipHostRegister) and undo it: the drop-in registers a
+ * right-hand side it sees a second time (device.py), so its upload is an asynchronous DMA that
+ * overlaps the call's set-up; the caller unregisters before the memory is freed. */
+int spis_host_register(void* host, int64_t bytes);
+int spis_host_unregister(void* host);
+/* Host -> device copy enqueued on the context stream without waiting (the source must be
+ * page-locked: spis_host_alloc or spis_host_register); later work on the stream is ordered
+ * after it, and the source must not change until it has run (the next spis_* call that waits). */
+int spis_memcpy_h2d_async(spis_context* ctx, void* dst_dev, const void* src_host, int64_t bytes);
+/* dst_host[0 .. n) = src_dev[0 .. n) by a copy kernel storing straight into page-locked host
+ * memory (spis_host_alloc / spis_host_register: mapped into the device's address space), then an
+ * event spin; any other destination falls back to spis_memcpy_d2h. */
+int spis_copy_to_host(spis_context* ctx, double* dst_host, const double* src_dev, int64_t n);
 
 /* y = A x (x must hold n_rows + n_ghost entries; ghosts are exchanged first) */
 int spis_spmv(spis_context* ctx, spis_matrix* A, double* x_dev, double* y_dev);

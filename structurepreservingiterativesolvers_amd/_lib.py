@@ -132,6 +132,7 @@ SIGNATURES = [
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
     ("spis_host_hash", C.c_int, [_VP, _I64, _I32, C.POINTER(C.c_uint64)]),
     ("spis_host_nonzero", C.c_int, [_VP, _I64, _I32, _I32, _PI32]),
+    ("spis_host_isa_ok", C.c_int, []),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),
     ("spis_spmv_bench", C.c_int, [_VP, _VP, _I32, _I32, _I32, _PD]),
@@ -156,6 +157,10 @@ SIGNATURES = [
     ("spis_memcpy_d2h", C.c_int, [_VP, _VP, _VP, _I64]),
     ("spis_host_alloc", C.c_int, [_I64, C.POINTER(_VP)]),
     ("spis_host_free", C.c_int, [_VP]),
+    ("spis_host_register", C.c_int, [_VP, _I64]),
+    ("spis_host_unregister", C.c_int, [_VP]),
+    ("spis_memcpy_h2d_async", C.c_int, [_VP, _VP, _VP, _I64]),
+    ("spis_copy_to_host", C.c_int, [_VP, _PD, _VP, _I64]),
     ("spis_spmv", C.c_int, [_VP, _VP, _VP, _VP]),
     ("spis_residual_norm", C.c_int, [_VP, _VP, _VP, _VP, _PD]),
     ("spis_dot", C.c_int, [_VP, _I64, _VP, _VP, _PD]),
@@ -195,6 +200,9 @@ def load_library(path=LIB_PATH):
         fn.argtypes = args
     if lib.spis_abi_version() != ABI_VERSION:
         raise SpisUnavailable(f"{path}: ABI {lib.spis_abi_version()} != expected {ABI_VERSION}")
+    if not lib.spis_host_isa_ok():
+        raise SpisUnavailable(f"{path}: its host least squares is built for x86-64-v3 (AVX2, FMA, BMI2), which "
+                              "this CPU lacks; rebuild with `make LSQFLAGS=-ffp-contract=off` (INTEGRATION.md)")
     _LIB = lib
     return lib
 

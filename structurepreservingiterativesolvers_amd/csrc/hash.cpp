@@ -218,3 +218,11 @@ extern "C" int spis_host_nonzero(const double* data, int64_t count, int32_t bitw
   *any_out = found.load();
   return SPIS_OK;
 }
+
+// The host least squares (lsq.cpp) is built for x86-64-v3 (Makefile LSQFLAGS: AVX2, FMA); this
+// translation unit is not, so the loader (_lib.py) can ask before the first KKT solve would
+// fault on an older host CPU with an illegal instruction.
+extern "C" int spis_host_isa_ok(void) {
+  __builtin_cpu_init();
+  return (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") && __builtin_cpu_supports("bmi2")) ? 1 : 0;
+}

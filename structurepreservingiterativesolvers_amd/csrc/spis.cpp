@@ -1387,6 +1387,44 @@ extern "C" int spis_host_free(void* p) {
   })
 }
 
+extern "C" int spis_host_register(void* p, int64_t bytes) {
+  ABI_GUARD({
+    if (!p || bytes <= 0) return fail(SPIS_ERR_ARG, "bad argument");
+    HIP_TRY(hipHostRegister(p, static_cast<size_t>(bytes), hipHostRegisterDefault));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_host_unregister(void* p) {
+  ABI_GUARD({
+    if (p) HIP_TRY(hipHostUnregister(p));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_memcpy_h2d_async(spis_context* c, void* dst, const void* src, int64_t bytes) {
+  ABI_GUARD({
+    if (!c || (bytes > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
+    if (bytes > 0) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return SPIS_OK;
+  })
+}
+
+extern "C" int spis_copy_to_host(spis_context* c, double* dst, const double* src, int64_t n) {
+  ABI_GUARD({
+    if (!c || n < 0 || (n > 0 && (!dst || !src))) return fail(SPIS_ERR_ARG, "bad argument");
+    void* dd = nullptr;
+    if (n > 0 && hipHostGetDevicePointer(&dd, dst, 0) == hipSuccess && dd != nullptr) {
+      HIP_TRY(launch_copy(n, src, static_cast<double*>(dd), c->stream));
+    } else {
+      (void)hipGetLastError();
+      if (n > 0) HIP_TRY(hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipEventRecord(c->ev_gram, c->stream));
+    return wait_event(c->ev_gram);
+  })
+}
+
 extern "C" int spis_spmv(spis_context* c, spis_matrix* A, double* x, double* y) {
   ABI_GUARD({
     if (!c || !A || !x || !y) return fail(SPIS_ERR_ARG, "null argument");

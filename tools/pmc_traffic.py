@@ -8,7 +8,7 @@ counter group per pass), then the reduction (tools/archive/r04_pmc.sh runs all t
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d D/w -o run -- python tools/pmc_traffic.py run c3
   python tools/pmc_traffic.py reduce c3 D/f/..._counter_collection.csv D/w/..._counter_collection.csv OUT.json
 
-``run`` is ``bench.py --config CFG --steps 3 --warmup 1 --no-cpu-baseline`` with the default
+``run`` is ``bench.py --config CFG --steps 3 --warmup 1 --no-cpu-baseline --no-wrapper`` with the default
 options.  Its last launches are the bench's standalone timing of the solver's SpMV
 (spis_spmv_bench: 22 back to back, then 22 each behind a 1 GiB evicting read), which also carry the
 calibration: the evicting read (stream_read_kernel, 1 GiB of 16-B loads per lane) gives
@@ -125,7 +125,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if a.what == "run":
         steps = "1" if a.cfg == "c5" else "3"
-        sys.argv = ["bench.py", "--config", a.cfg, "--steps", steps, "--warmup", "1", "--no-cpu-baseline"]
+        sys.argv = ["bench.py", "--config", a.cfg, "--steps", steps, "--warmup", "1", "--no-cpu-baseline", "--no-wrapper"]
         import bench
 
         bench.main()
