@@ -391,6 +391,12 @@ typedef struct spis_solve_out {
   double* stamps_host;       /* capacity 4k+2 or NULL: iter start/end, constraint
                                 build start/end (seconds), then run start/end   */
   double* x_final_dev;       /* [n] receives x[-1] (device), or NULL             */
+  /* [n] page-locked host buffer (spis_host_alloc) or NULL: when the run reaches its last step,
+   * x_{k-1} is copied there by DMA on the side stream while the last residual SpMV runs, and
+   * x_host_ready is set to 1 when that copy is x[-1]; 0 otherwise (the caller downloads
+   * x_final_dev itself) */
+  double* x_final_host;
+  int32_t x_host_ready;
 } spis_solve_out;
 
 /* Runs the solver; *ws_out receives a workspace holding the Krylov basis so

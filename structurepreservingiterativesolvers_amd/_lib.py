@@ -116,6 +116,8 @@ class SolveOut(C.Structure):
         ("msg_host", C.POINTER(C.c_int32)),
         ("stamps_host", C.POINTER(C.c_double)),
         ("x_final_dev", C.c_void_p),
+        ("x_final_host", C.c_void_p),
+        ("x_host_ready", C.c_int32),
     ]
 
 

@@ -107,6 +107,7 @@ struct spis_context {
   size_t pinned_len = 0;     // doubles
   hipEvent_t ev_arn = nullptr, ev_upd[2] = {nullptr, nullptr};  // solver pipeline events
   hipEvent_t ev_gram = nullptr;  // constrained step: the Gram tile has reached pinned memory
+  hipEvent_t ev_xd = nullptr, ev_xd2 = nullptr;  // x_{k-1} written (main stream) / copied to the host (stream2)
   unsigned long long seq = 0;  // last completion sequence number handed to a publishing kernel
   double* gram_part = nullptr;
   size_t gram_part_len = 0;
@@ -632,6 +633,8 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[0], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_upd[1], evf));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_xd, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_xd2, hipEventDisableTiming));
     *out = c.release();
     return SPIS_OK;
   })
@@ -703,7 +706,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->stream2);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram})
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_xd, c->ev_xd2})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
@@ -3036,6 +3039,8 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // recomputes x_j after c_{j+1}), and enqueues [U_j res | a_{j+2}] (res + finalize at the end).
     std::vector<double> yspec(k);
     int last_x = -1;  // iteration whose x_j is x[-1]
+    bool x_host_spec = false;  // x_{k-1} is on its way to out->x_final_host (stream2, ev_xd2)
+    out->x_host_ready = 0;
     // L mode: U_{k-2}'s residual held back and read with U_{k-1}'s in one SpMV (the matrix read
     // once) when it cannot stop the run: CGMRES with safety not True at k-2 (solvers.py:296-297)
     // or CGMRES_P; the record order stays res_{k-2}, res_{k-1}
@@ -3276,6 +3281,15 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         PHASE_IF(j == k - 1, 15);
         if (need_gemv && !gemv_done) ST_TRY(S.enqueue_gemv(j, p, y.data(), !fused && j + 1 < k));
         PHASE_IF(j == k - 1, 16);
+        // x_{k-1} (the caller's buffer) to the caller's host buffer on the side stream, under the
+        // last residual SpMV; used when x_{k-1} is x[-1] (below)
+        if (j == k - 1 && need_gemv && !gemv_done && out->x_final_host && S.x_last && !c->dist_on()) {
+          HIP_TRY(hipEventRecord(c->ev_xd, s));
+          HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_xd, 0));
+          HIP_TRY(hipMemcpyAsync(out->x_final_host, S.x_last, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream2));
+          HIP_TRY(hipEventRecord(c->ev_xd2, c->stream2));
+          x_host_spec = true;
+        }
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
           PHASE_IF(j == 10, 26);
@@ -3314,6 +3328,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     bool tail_launch = pending != k - 1;
     // x[-1] -> caller's buffer, stream-ordered after the last update (and any speculative
     // Arnoldi step, which never touches xj / r0), then one synchronisation
+    // the side-stream copy of x_{k-1} is x[-1] when x_{k-1} is the last iterate and stays in the
+    // caller's buffer (no copy below)
+    const bool x_host_ok = x_host_spec && !ws->broke_at_start && have_x && last_x == k - 1 &&
+                           out->x_final_dev && S.xbuf(last_x) == out->x_final_dev;
     if (out->x_final_dev) {
       if (ws->broke_at_start) {
         HIP_TRY(launch_copy(n, x0, out->x_final_dev, s));
@@ -3351,6 +3369,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       ST_TRY(wait_event(c->ev_gram));
     }
     PHASE(8);
+    if (x_host_spec) {  // the side-stream copy has finished (the caller may read or reuse the buffer)
+      ST_TRY(wait_event(c->ev_xd2));
+      out->x_host_ready = x_host_ok ? 1 : 0;
+    }
     prof_drain(c);
     if (o->pre_ilu) ST_TRY(ilu_check(o->pre_ilu));
     if (const unsigned ce = *reinterpret_cast<volatile unsigned*>(c->chain_err)) {  // never on a healthy device

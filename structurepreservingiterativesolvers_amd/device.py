@@ -181,6 +181,12 @@ class DeviceBuffer:
                                               8 * a.size), "spis_memcpy_h2d")
         return self
 
+    def download_into(self, out):
+        """The first ``len(out)`` entries into the host array ``out`` (returned)."""
+        _lib.check(self.ctx.L.spis_memcpy_d2h(self.ctx.handle, out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr),
+                                              8 * out.size), "spis_memcpy_d2h")
+        return out
+
     def download(self, n=None, pinned=False):
         """The first ``n`` entries as a new host array (``pinned``: in a page-locked buffer from
         :func:`pinned_empty` when one is free or may be made, a pageable one otherwise)."""

@@ -43,7 +43,7 @@ import scipy.sparse as sps
 from . import _lib
 from ._wrapcache import is_known_zero
 from .device import (DeviceMatrix, DeviceVector, cached_vector, choose_ilu, device_matrix, device_vector, get_context,
-                     host_nonzero, is_superlu, is_zero_matrix, zero_vector)
+                     host_nonzero, is_superlu, is_zero_matrix, pinned_empty, zero_vector)
 
 log = logging.getLogger("structurepreservingiterativesolvers_amd")
 
@@ -516,7 +516,11 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     fbuf.fill(0.0)
     ibuf.fill(0)
     xf = DeviceVector.scratch(ctx, n)  # overwritten whole by the solve (x[-1], or x0 on breakdown)
+    # host inputs: a page-locked buffer the library fills with x_{k-1} under the last residual
+    # SpMV when that is x[-1] (x_host_ready), else x[-1] is downloaded after the solve
+    xh = None if device_io else pinned_empty(n)
     out.steps, out.n_res, out.x_final_dev = 0, 0, xf.ptr
+    out.x_final_host, out.x_host_ready = (None if xh is None else xh.ctypes.data), 0
     ws = C.c_void_p()
     _cp()
     tp = _stamp()
@@ -540,7 +544,12 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     res, ys, stamps = fbuf[:k + 1].copy(), fbuf[k + 1:k + 1 + k * k].copy(), fbuf[k + 1 + k * k:].copy()
     br, ev, msg = ibuf[:k].copy(), ibuf[k:2 * k].copy(), ibuf[2 * k:].copy()
     n_iter = out.n_res - 1
-    final = xf if device_io else xf.download(n, pinned=True)
+    if device_io:
+        final = xf
+    elif xh is not None and out.x_host_ready:
+        final = xh
+    else:
+        final = xf.download(n, pinned=True) if xh is None else xf.download_into(xh)
     tp = _tick("d2h", tp)
     xs = IterateList(ctx, ws.value, n, n_iter + 1, final, as_device=device_io)
     xs._set_meta(br, ev[: max(n_iter, out.steps)].copy(), ys, k, n_iter)
