@@ -300,7 +300,7 @@ def spawn_ranks(n, script=None, argv=None):
     return 0
 
 
-def wrapper_rate(wl, args, reps=10, warm=3):
+def wrapper_rate(wl, args, reps=30, warm=3):
     """SURVEY §8(d)'s it/s as defined there: ``dict['steps']`` / wall time of the drop-in call
     ``swe.LinearSolver.cgmresWrapper(dic, x0, k, tol)`` (reference ``swe/LinearSolver.py:12-49``) on
     host SciPy/NumPy inputs, warm (the operator uploads cached by the warm-up calls, as a

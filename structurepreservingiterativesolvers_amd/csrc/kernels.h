@@ -127,6 +127,7 @@ constexpr int kChainGranLag = 12 * kChainMaxWG + 16;
 constexpr int kLagDW = 8;  // K2q data waves per workgroup (+1 exchange wave): PER <= 4 pairs per thread
 constexpr int kLagDepth = 2;  // K2q: dot products this many MGS steps early (1 or 2)
 void set_chain_lag(int lag);  // tuning tools only (tools/chainbench): 1 or 2, process-wide
+void set_store_wt(int on);     // write-through (sc1) output stores of K2q and the SpMVs (default 1; process-wide)
 constexpr int kLagNS = 5;     // K2q basis ring: q_{i-1} .. q_{i+3} in registers
 constexpr int kChainGsub = 2 * kMaxK + 8;  // K2q gsub: G(m, m-1) at [m], G(m, m-2) at [kMaxK + m]
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
@@ -227,8 +228,16 @@ struct SymTabView {
   int32_t nblk;
   int32_t ns;
 };
+// a column reduction riding in another launch: out[j] = sum over rows of part[row][j], j < npairs
+// (reduce_cols_kernel's arithmetic); the transpose's linear terms ride in K7t's H + H^T launch
+struct ColReduce {
+  int npairs;
+  int rows;
+  const double* part;
+  double* out;
+};
 hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
-                                      hipStream_t s, bool pin = false);
+                                      hipStream_t s, bool pin = false, const ColReduce* lin = nullptr);
 // Ut in the perm order plus the linear terms Gv[c][a] = sum_r U[r][a] v_c[r] (vpart: partials of
 // kTransposeGrid x nvv np1; Gv: nvv x np1); np1 <= 32, nvv <= 4
 constexpr int kTransposeGrid = 2048;
@@ -236,7 +245,8 @@ constexpr int kTransposeGrid = 2048;
 // one-tile-at-a-time kernel (bitwise the same Ut and terms)
 hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                       double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
-                                      hipStream_t s, bool pin = false, bool pipe = true);
+                                      hipStream_t s, bool pin = false, bool pipe = true,
+                                      ColReduce* defer = nullptr);  // defer: no reduce launch, *defer describes it
 hipError_t launch_constraint_gram_mfma(int64_t n, int np1, const CsrView* M, const GramSplit* split,
                                        const double* Ut, int nvv, const double* const* v, double* partials,
                                        double* G, hipStream_t s);

@@ -109,6 +109,33 @@ __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, int voff, int 
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
 }
 
+// Write-through (sc1) stores for a kernel's output vectors.  A kernel boundary writes back every
+// line its kernel left dirty in the XCD L2s (≈ B / 6 TB/s, MI355X_MICROARCH.md "boundary"); a
+// write-through line is already in memory (and stays cached, clean), so the boundary has nothing
+// to write back.  The data and every later read are unchanged.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_out(double* p, double v, bool wt) {
+  if (wt)
+    st_wt(p, v);
+  else
+    *p = v;
+}
+__device__ __forceinline__ void buf_st2_wt(__amdgpu_buffer_rsrc_t r, int voff, double2 d) {
+  u32x4_t v;
+  v.x = static_cast<unsigned>(__double2loint(d.x));
+  v.y = static_cast<unsigned>(__double2hiint(d.x));
+  v.z = static_cast<unsigned>(__double2loint(d.y));
+  v.w = static_cast<unsigned>(__double2hiint(d.y));
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 16);  // aux 16 = sc1 (write-through)
+}
+
+// the store form of the hot path's output vectors (K2q's q_{j+1} and x_j, the SpMVs' w): 1 = sc1
+static int g_store_wt = 1;
+void set_store_wt(int on) { g_store_wt = on ? 1 : 0; }
+
 // a descriptor over [p, p + 2^31 B) with a wave-uniform base (callers index it with valid offsets)
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const T* p) {
@@ -393,7 +420,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
     const double* __restrict__ aux1, double* __restrict__ y1, double* __restrict__ part1,
     const double* __restrict__ x2, const double* __restrict__ aux2, double* __restrict__ y2,
     double* __restrict__ part2, const uint16_t* __restrict__ c16, const int4* __restrict__ base,
-    const unsigned* __restrict__ zf, unsigned gen) {
+    const unsigned* __restrict__ zf, unsigned gen, int wt) {
   constexpr bool DUAL = MODE == 4 || MODE == 6;
   constexpr int kPer = PipeStage<CAP>::kPer;
   // products at padded index i + i/16: one thread per row reads its row left to right, and rows
@@ -556,12 +583,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, C16 ?
           const double t2 = s2 - cur.a2;
           pt2 += t2 * t2;
         } else {
-          y2[r] = s2;
+          st_out(y2 + r, s2, wt);
           pt2 += cur.a2 * s2;
         }
       }
-      if (MODE == kEpiPlain) y1[r] = s1;
-      if (MODE == kEpiDot) { y1[r] = s1; pt1 += cur.a1 * s1; }
+      if (MODE == kEpiPlain) st_out(y1 + r, s1, wt);
+      if (MODE == kEpiDot) { st_out(y1 + r, s1, wt); pt1 += cur.a1 * s1; }
       if (MODE == kEpiResNorm) { const double t = s1 - cur.a1; pt1 += t * t; }
       if (MODE == kEpiR0) { const double t = cur.a1 - s1; y1[r] = t; pt1 += t * t; }
     }
@@ -592,21 +619,21 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   if (mode == kEpiR0 && zf != nullptr) {  // r0 with the x0 = 0 test
     if (A.col16 != nullptr)
       launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,
-               A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, zf, gen);
+               A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, zf, gen, g_store_wt);
     else
       launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,
-               A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, zf, gen);
+               A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, zf, gen, g_store_wt);
     return hipGetLastError();
   }
 #define SPIS_PIPE(M)                                                                                            \
   if (A.col16 != nullptr)                                                                                       \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
              A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base,                  \
-             static_cast<const unsigned*>(nullptr), 0u);                                                       \
+             static_cast<const unsigned*>(nullptr), 0u, g_store_wt);                                           \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr,                                \
-             static_cast<const unsigned*>(nullptr), 0u)
+             static_cast<const unsigned*>(nullptr), 0u, g_store_wt)
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
@@ -1094,7 +1121,7 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
     const double* __restrict__ part_in, int n_in, double* __restrict__ hcol, unsigned long long* gran,
     unsigned* epoch, unsigned* err, const double* __restrict__ xpart, int n_x, double* __restrict__ x_out,
     unsigned long long* __restrict__ flag, const unsigned long long* __restrict__ seq, double* __restrict__ gsub,
-    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo, int tw) {
+    YArg yx, int px, const double* __restrict__ x0, double* __restrict__ xo, int tw, int wt) {
 #pragma clang fp contract(off)
   static_assert(LAG >= 1 && LAG <= 2 && NS >= LAG + 3, "ring: q_{i-1}, the dotted q_{i+LAG}, one loading");
   // NT: nontemporal basis loads, except q_0 .. q_{tw-1} and x0 when tw > 0 (a window every chain
@@ -1375,13 +1402,17 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       if (FX) {  // x is complete (its last term, q_{px-1}, passed at step j - 1): stored now, its
                  // write drains during the two exchanges still ahead instead of after them
         vm_drain();  // x0's LDS DMA (issued after the ring's first loads) has landed
-        double2* xo2 = reinterpret_cast<double2*>(xo);
+        const __amdgpu_buffer_rsrc_t xr = span_rsrc(xo);
 #pragma unroll
         for (int k = 0; k < PER; ++k)
           if (data && p0 + k * DT < npair) {
             const double2 a = s_acc[k * DT + tid];
             const double2 b = s_x0[k * DT + tid];
-            xo2[p0 + k * DT] = make_double2(a.x + b.x, a.y + b.y);
+            const double2 xv = make_double2(a.x + b.x, a.y + b.y);
+            if (wt)
+              buf_st2_wt(xr, static_cast<int>((p0 + k * DT) * 16), xv);
+            else
+              buf_st2(xr, static_cast<int>((p0 + k * DT) * 16), 0, xv);
           }
       }
       double hj = 0.0;
@@ -1401,10 +1432,16 @@ __global__ __launch_bounds__(DW * 64 + 64, 1) void mgs_chain_lag_kernel(
       if (!wait_h(j + 1, &nn)) return false;
       const double hh = sqrt(nn);
       double2* q2 = reinterpret_cast<double2*>(Q + static_cast<int64_t>(j + 1) * pitch);
+      const __amdgpu_buffer_rsrc_t qr = span_rsrc(q2);
 #pragma unroll
       for (int k = 0; k < PER; ++k)
-        if (data && p0 + k * DT < npair)
-          q2[p0 + k * DT] = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+        if (data && p0 + k * DT < npair) {
+          const double2 qv = hh == 0.0 ? make_double2(0.0, 0.0) : make_double2(y[k].x / hh, y[k].y / hh);
+          if (wt)
+            buf_st2_wt(qr, static_cast<int>((p0 + k * DT) * 16), qv);
+          else
+            buf_st2(qr, static_cast<int>((p0 + k * DT) * 16), 0, qv);
+        }
       if (tid == 0 && tr_row >= 0) CHAIN_TR(tr_row, 40);
       return false;
     }
@@ -1695,7 +1732,8 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
     for (int i = 0; i < px; ++i) ya.v[i] = yx_host[i];
 #define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
   launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
-           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo, tw)
+           pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo, tw, \
+           g_store_wt)
 #define SPIS_LAG_PER(FX_, NT_, LAG_)          \
   switch (per) {                              \
     case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \
@@ -3268,6 +3306,54 @@ __global__ __launch_bounds__(kBlock) void reduce_cols_kernel(int npairs, int row
   }
 }
 
+// K7t's H + H^T for the np1 x np1 block: one workgroup per pair a <= b (np1 (np1 + 1) / 2 of them,
+// about half of reduce_cols_kernel's np1^2).  Both sums are reduce_cols_kernel's (same strided
+// per-thread sums, same block_sum tree), and out[a][b] = s_ab + s_ba, out[b][a] = s_ba + s_ab are
+// the same double (addition commutes), so every value is bitwise reduce_cols_kernel's.
+// Blocks past the pairs (lin.npairs of them) reduce lin's columns as reduce_cols_kernel does (the
+// transpose's linear terms: one launch fewer on the constrained step).
+__global__ __launch_bounds__(kBlock) void reduce_sym_kernel(int np1, int rows, const double* __restrict__ part,
+                                                            double* __restrict__ out, bool pin, ColReduce lin) {
+  __shared__ double s_wave[4];
+  const int np2 = np1 * np1;
+  const int nsym = np1 * (np1 + 1) / 2;
+  if (static_cast<int>(blockIdx.x) >= nsym) {
+    const int j = static_cast<int>(blockIdx.x) - nsym;
+    double s = 0.0;
+    for (int r = threadIdx.x; r < lin.rows; r += kBlock) s += lin.part[static_cast<int64_t>(r) * lin.npairs + j];
+    const double tot = block_sum(s, s_wave);
+    if (threadIdx.x == 0) {
+      if (pin)
+        pin_store(lin.out + j, tot);
+      else
+        lin.out[j] = tot;
+    }
+    return;
+  }
+  int a = 0, t = static_cast<int>(blockIdx.x);
+  while (t >= np1 - a) {  // row a of the upper triangle holds np1 - a pairs
+    t -= np1 - a;
+    ++a;
+  }
+  const int b = a + t;
+  const int j = a * np1 + b, jt = b * np1 + a;
+  double s = 0.0, st = 0.0;
+  for (int r = threadIdx.x; r < rows; r += kBlock) s += part[static_cast<int64_t>(r) * np2 + j];
+  const double s_ab = block_sum(s, s_wave);
+  for (int r = threadIdx.x; r < rows; r += kBlock) st += part[static_cast<int64_t>(r) * np2 + jt];
+  const double s_ba = block_sum(st, s_wave);
+  if (threadIdx.x == 0) {
+    const double tot = s_ab + s_ba;
+    if (pin) {
+      pin_store(out + j, tot);
+      if (jt != j) pin_store(out + jt, tot);
+    } else {
+      out[j] = tot;
+      out[jt] = tot;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void gram_reduce_kernel(int npairs, int grid,
                                                              const double* __restrict__ partials,
                                                              double* __restrict__ G) {
@@ -3650,9 +3736,10 @@ hipError_t launch_transpose_basis(int64_t n, int p, const double* Z, int64_t pit
 
 hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t pitch, const double* x0,
                                       double* Ut, int nvv, const double* const* v, double* vpart, double* Gv,
-                                      hipStream_t s, bool pin, bool pipe) {
+                                      hipStream_t s, bool pin, bool pipe, ColReduce* defer) {
   const int np1 = p + 1;
   if (np1 > 32 || nvv < 0 || nvv > 4 || nvv * np1 > kBlock) return hipErrorInvalidValue;
+  if (defer != nullptr) *defer = ColReduce{0, 0, nullptr, nullptr};
   const double* vv[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int c = 0; c < nvv; ++c) vv[c] = v[c];
   const int64_t ntiles = (n + 63) / 64;
@@ -3667,6 +3754,10 @@ hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nvv == 0) return e;
   const int npairs = nvv * np1;
+  if (defer != nullptr) {
+    *defer = ColReduce{npairs, g, vpart, Gv};
+    return hipSuccess;
+  }
   hipLaunchKernelGGL(reduce_cols_kernel, dim3(npairs), dim3(kBlock), 0, s, npairs, g, vpart, Gv, 0, pin);
   return hipGetLastError();
 }
@@ -4099,15 +4190,16 @@ static int sym_grid() {
 }
 
 hipError_t launch_constraint_gram_sym(int np1, const SymTabView& T, const double* Ut, double* partials, double* G,
-                                      hipStream_t s, bool pin) {
+                                      hipStream_t s, bool pin, const ColReduce* lin) {
   if (np1 > 32) return hipErrorInvalidValue;
   if (T.ns != kSymSlots) return hipErrorInvalidValue;
   const int grid = sym_grid();
   hipLaunchKernelGGL(constraint_gram_sym_kernel<kSymSlots>, dim3(grid), dim3(kBlock), 0, s, T, Ut, partials, np1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int np2 = np1 * np1;
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3(np2), dim3(kBlock), 0, s, np2, grid, partials, G, np1, pin);
+  const ColReduce lr = lin != nullptr ? *lin : ColReduce{0, 0, nullptr, nullptr};
+  hipLaunchKernelGGL(reduce_sym_kernel, dim3(np1 * (np1 + 1) / 2 + lr.npairs), dim3(kBlock), 0, s, np1, grid, partials,
+                     G, pin, lr);
   return hipGetLastError();
 }
 

@@ -621,6 +621,7 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     c->gram_inc = env_flag("SPIS_GRAM_INC", true);
     c->x0_zero_test = env_flag("SPIS_X0_ZERO_TEST", true);
     c->transpose_pipe = env_flag("SPIS_TRANSPOSE_PIPE", true);
+    set_store_wt(env_flag("SPIS_STORE_WT", true) ? 1 : 0);  // A/B switch (process-wide, read at context creation)
     c->k2w_fold = env_flag("SPIS_K2W_FOLD", true);
     c->k2w_onepass = env_flag("SPIS_K2W_ONEPASS", true);
     if (const char* v = std::getenv("SPIS_K2W_TW")) c->k2w_tw = std::atoi(v);
@@ -1754,11 +1755,14 @@ static int con_gram_enqueue(spis_context* c, spis_workspace* ws, int m, const sp
     HIP_TRY(hipHostGetDevicePointer(&dp, dst, 0));
     double* dstd = static_cast<double*>(dp);
     if (!c->cg_vpart) HIP_TRY(hipMalloc(&c->cg_vpart, sizeof(double) * kTransposeGrid * 4 * 32));
+    // the linear terms' column reduction rides in the first K7t reduction launch (one launch fewer)
+    ColReduce lin{0, 0, nullptr, nullptr};
     HIP_TRY(launch_transpose_basis_lin(n, p, Z, pitch, x0, ws->Ut, nv, vlist.data(), c->cg_vpart, dstd + voff, st,
-                                       true, c->transpose_pipe));
-    for (const Launch& L : plan)
-      HIP_TRY(launch_constraint_gram_sym(np1, L.tv, ws->Ut, c->cg_part, dstd + static_cast<size_t>(L.ci) * np1 * np1,
-                                         st, true));
+                                       true, c->transpose_pipe, plan.empty() ? nullptr : &lin));
+    for (size_t i = 0; i < plan.size(); ++i)
+      HIP_TRY(launch_constraint_gram_sym(np1, plan[i].tv, ws->Ut, c->cg_part,
+                                         dstd + static_cast<size_t>(plan[i].ci) * np1 * np1, st, true,
+                                         i == 0 && lin.npairs > 0 ? &lin : nullptr));
     return SPIS_OK;
   }
   if (tsym) {  // Ut + the linear terms in one pass over the basis
@@ -2870,8 +2874,13 @@ struct Solver {
 // tools/host_phases.py: a build with -DSPIS_HOST_PHASES (make phases) prints the mean host time
 // of spis_solve's phases every 40 calls (the product build compiles the marks away)
 #ifdef SPIS_HOST_PHASES
-static double g_phase_t[32], g_phase_acc[32];
+static double g_phase_t[40], g_phase_acc[40];
 static int g_phase_calls = 0;
+// the iteration marks 20-27 record (SPIS_PHASE_ITER, default 10; marks 30-35: the start-up launches)
+static const int g_phase_iter = [] {
+  const char* e = std::getenv("SPIS_PHASE_ITER");
+  return e ? std::atoi(e) : 10;
+}();
 #define PHASE(i) (g_phase_t[i] = now_s())
 #define PHASE_IF(cond, i) ((cond) ? (void)(g_phase_t[i] = now_s()) : (void)0)
 extern "C" double spis_debug_phase_t(int i) { return g_phase_t[i]; }  // the last call's marks
@@ -2884,9 +2893,11 @@ static void phase_report(int np) {  // the first 10 calls (allocations, warm-up)
     std::fprintf(stderr, "\n");
   }
 }
+#define PHASE_ITER g_phase_iter
 #else
 #define PHASE(i) ((void)0)
 #define PHASE_IF(cond, i) ((void)0)
+#define PHASE_ITER 10
 static void phase_report(int) {}
 #endif
 
@@ -2971,6 +2982,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       }
       if (++c->x0_gen == 0) ++c->x0_gen;  // a stale word never equals a new generation
       HIP_TRY(launch_copy_flag(n, x0, ws->x0, c->x0_flag, c->x0_gen, s));
+      PHASE(30);
     } else {
       HIP_TRY(launch_copy(n, x0, ws->x0, s));
     }
@@ -2984,6 +2996,7 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     }
     HIP_TRY(launch_spmv(A->dual_view(), kEpiR0, xr0, ws->r0, b, c->partA, S.gs, s, nullptr,
                         x0_test ? c->x0_flag : nullptr, c->x0_gen));
+    PHASE(31);
     ST_TRY(allreduce(c, c->partA, S.gs));
     double* beta_slot = c->pinned + S.yoff() + kMaxK;
     // beta: the normalize kernel's one system-scope store into pinned memory; the host spins
@@ -2993,17 +3006,20 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     if (beta_spin) *reinterpret_cast<volatile uint64_t*>(beta_slot) = Solver::kHSentinel;
     HIP_TRY(launch_normalize(n, ws->r0, S.Qv(0), c->partA, S.gs, c->pinned_dev + S.yoff() + kMaxK, s, S.gb));
     if (!beta_spin) HIP_TRY(hipEventRecord(c->ev_gram, s));  // beta in pinned memory (system-scope event)
+    PHASE(32);
     // A_0 and A_1 are queued before beta is read: the GPU goes straight on while the host waits.
     // On beta == 0 they ran on q0 = 0 (normalize writes zeros) and are discarded unread.
     // L mode: the solver loop below (lag_chain: K2q chains publish H[:, j] to the host themselves)
     const bool L = S.lag_chain() && c->fuse_spmv;
     if (stamps) stamps[0] = now_s();
     ST_TRY(S.enqueue_arnoldi(0));
+    PHASE(33);
     if (!L) HIP_TRY(hipEventRecord(c->ev_arn, s));  // L mode waits for H[:, 0] itself
     if (k > 1) {
       if (stamps) stamps[1] = now_s();
       ST_TRY(S.enqueue_arnoldi(1, !L));  // L: A_1's chain is enqueued at iteration 0
     }
+    PHASE(34);
     if (beta_spin) {
       bool ok = false;
       ST_TRY(S.wait_slot(reinterpret_cast<const uint64_t*>(beta_slot), &ok));
@@ -3070,10 +3086,10 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
       bool fused = false, col_added = false;
       if (L) {
         bool ok = false;
-        PHASE_IF(j == 10, 20);
+        PHASE_IF(j == PHASE_ITER, 20);
         ST_TRY(S.wait_hcol(j, &ok));
         PHASE_IF(j == k - 1, 10);
-        PHASE_IF(j == 10, 21);
+        PHASE_IF(j == PHASE_ITER, 21);
         if (!ok) {  // the chain failed (c->chain_err): reported at the end of the solve
           (void)hipStreamSynchronize(s);
           break;
@@ -3092,9 +3108,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
             qr.solve(j + 1, yspec.data());
             fused = true;
           }
-          PHASE_IF(j == 10, 22);
+          PHASE_IF(j == PHASE_ITER, 22);
           ST_TRY(S.enqueue_chain(j + 1, j >= 1 ? j - 1 : -1, fused ? yspec.data() : nullptr));
-          PHASE_IF(j == 10, 23);
+          PHASE_IF(j == PHASE_ITER, 23);
         } else if (brk && j >= 1 && j + 1 < k) {  // no c_{j+1}: U_{j-1}'s residual on its own
           ST_TRY(S.enqueue_finalize(j - 1));
         }
@@ -3131,9 +3147,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
           PHASE_IF(j == k - 1, 14);
         }
       }
-      PHASE_IF(j == 10, 24);
+      PHASE_IF(j == PHASE_ITER, 24);
       ST_TRY(j == 0 ? (L ? SPIS_OK : wait_event(c->ev_arn)) : (deferred == j - 1 ? SPIS_OK : S.wait_update(j - 1)));
-      PHASE_IF(j == 10, 25);
+      PHASE_IF(j == PHASE_ITER, 25);
       prof_drain(c);
       if (pending >= 0 && pending != deferred) {  // finish iteration j-1: true residual + stop test (:290-297)
         out->res_host[n_res++] = S.residual(pending);
@@ -3292,9 +3308,9 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
         }
         if (j + 2 < k) {
           if (stamps) stamps[j + 2] = now_s();
-          PHASE_IF(j == 10, 26);
+          PHASE_IF(j == PHASE_ITER, 26);
           ST_TRY(S.enqueue_dual(j, j + 2));
-          PHASE_IF(j == 10, 27);
+          PHASE_IF(j == PHASE_ITER, 27);
         } else {
           // the forced constrained last step's reduction first (its inputs, q_0 .. q_{k-1} and
           // x0, are complete): the host's KKT then runs while the GPU computes this residual

@@ -366,8 +366,8 @@ _MATRIX_CACHE: dict = {}
 _VERIFY = True  # set_option("verify_uploads", ...)
 # host threads of the content scans (a persistent pool in libspis, hash.cpp): the C3 operator
 # and energy matrix (~0.3 GB) are re-verified within one solve's time at ~16 threads; a GPU box
-# grants one process about 16 cores
-_HASH_THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+# grants one process about 16 cores (SPIS_HASH_THREADS overrides the count)
+_HASH_THREADS = max(1, int(os.environ.get("SPIS_HASH_THREADS", 0)) or min(16, len(os.sched_getaffinity(0))))
 _ASYNC_MIN_BYTES = 1 << 22  # smaller matrices are re-verified inline (a thread hand-off costs more)
 
 

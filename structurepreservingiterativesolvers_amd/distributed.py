@@ -584,7 +584,9 @@ def bench_main(args, metric):
             },
             "kernels": {"mgs_us_mean": 1e3 * mgs_ms, "spmv_us": 1e3 * spmv_ms},
         }
-        if not args.no_cpu_baseline:  # the reference's CPU path on the same global system
+        # the reference's CPU path on the same global system, at one rank only (several ranks: the
+        # N = 1 line carries it, and the other ranks would wait at the barrier for the sample)
+        if not args.no_cpu_baseline and P == 1:
             import bench as _bench
 
             out["cpu_baseline"] = _bench.cpu_baseline(wl, wl["conlist"], args.k, args.tol, args.cpu_budget)

@@ -1138,6 +1138,68 @@ def test_full_size_lkdvrk_c4_vs_oracle(spis):
 
 
 @pytest.mark.slow
+def test_full_size_lkdvrk_c4_projection_succeeds(spis):
+    """Config C4's operator (lkdvRK GL(3) M=16,667, N=300,006) with constraints the forced step can
+    meet: a quadratic 1/2 X'DX + c (D random SPD diagonal) and a linear v.X + c, both through the
+    exact solution (the lifted lkdvRK mass constraint of test_full_size_lkdvrk_c4_vs_oracle has a
+    roundoff gradient, so that step falls back in the reference too).  The oracle's SLSQP projects
+    (branch "con"); so must the device, with y the reference's SLSQP minimum on the device's own
+    final-step inputs, both constraints met to 1e-12 of their scale on the returned x, steps 1..29
+    within 10x the oracle's 8-seed envelope and x[-1] within 1e-6 of the oracle's (SLSQP's stop)."""
+    import scipy.sparse as sps
+    import scipy.sparse.linalg as spla
+
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.lkdvRK import assembly as ra
+
+    dic, _ = ra.linforms(M=16667, tstages=3)
+    A, b = dic["A"], dic["b"]
+    n = A.shape[0]
+    assert n == 300006
+    xs_exact = spla.spsolve(A.tocsc(), b)
+    rng = np.random.default_rng(7)
+    dg = 0.5 + rng.random(n)
+    D = sps.diags(dg, format="csr")
+    v = rng.normal(size=n)
+
+    class _Quad:
+        def __init__(self):
+            self.M, self.v, self.c = D, np.zeros(n), -0.5 * float(xs_exact @ (dg * xs_exact))
+
+    class _Lin:
+        def __init__(self):
+            self.M, self.v, self.c = 0 * D, v, -float(v @ xs_exact)
+
+    cons = [_Quad(), _Lin()]
+    x0 = np.zeros(n)
+    k = 30
+    x, d = solvers.cgmres(A, b, x0, k, tol=1e-19, conlist=cons)
+    xr, dr, trace, bad = _oracle_run(A, b, x0, k, tol=1e-19, conlist=cons)
+    assert not bad
+    assert trace[-1] == (k - 1, "con")
+    tdev = d["x"].trace
+    assert tdev == trace, (tdev[-3:], trace[-3:])
+    env, _ = _envelope_xr(A, b, x0, k, 1e-19, cons, seeds=range(8))
+    xs, xrs = np.asarray(d["x"]), np.asarray(dr["x"])
+    xsl, _ = _slsqp_slack(A, b, x0, k, xrs, np.asarray(dr["res"]))
+    for i in range(1, k):
+        tol_i = max(1e-8, 10 * env[i]) + 2 * xsl[i]
+        assert np.linalg.norm(xs[i] - xrs[i]) <= tol_i * np.linalg.norm(xrs[i]), (i, tol_i)
+    branch, sol, func, _, _, _ = _slsqp_on_device_inputs(d["x"], k, len(cons))
+    assert branch == "con"
+    yd = d["x"].y[k - 1]
+    assert np.linalg.norm(yd - sol.x) <= 1e-6 * np.linalg.norm(sol.x)
+    assert func(yd) <= func(sol.x) * (1 + 1e-9)
+    _assert_invariants(cons, x)
+    vals = [0.5 * x @ (D @ x) + cons[0].c, v @ x + cons[1].c]
+    print("c4 projection: constraint values", vals, "scales", [abs(c.c) for c in cons])
+    # the oracle's SLSQP stops at ftol = 1e-24 on the LS objective, so its y is the minimum only to
+    # the 1e-6 the y comparison above allows
+    assert np.linalg.norm(x - xr) <= max(1e-6, 10 * env[-1]) * np.linalg.norm(xr)
+    np.testing.assert_allclose(d["res"][-1], np.linalg.norm(A @ x - b), rtol=1e-10)
+
+
+@pytest.mark.slow
 def test_full_size_swe_c5_cycle0_vs_oracle(spis):
     """Config C5 (swe M=913, N=10,002,828, mass + energy + the synthetic third constraint), the
     first restart cycle against the oracle on the same system: the same 30 steps and branches,

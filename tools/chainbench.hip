@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
         auto run = [&]() {
           hipLaunchKernelGGL(kern, dim3(GD + 1), dim3(DW * 64 + 64), 0, s, n, w, Q, pitch, j, part, 1024, hcol_dev, gran,
                              ep, err, (const double*)nullptr, 0, (double*)nullptr, (unsigned long long*)nullptr,
-                             (const unsigned long long*)nullptr, gsub, ya, j, x0, xo, 0);
+                             (const unsigned long long*)nullptr, gsub, ya, j, x0, xo, 0, 1);
         };
         for (int r = 0; r < 3; ++r) run();
         CK(hipStreamSynchronize(s));

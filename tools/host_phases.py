@@ -50,7 +50,7 @@ for _ in range(reps):
     t = time.perf_counter()
     _, d = solve()
     marks.append((t, time.perf_counter(), d["x"].stamps[4 * 30], d["x"].stamps[4 * 30 + 1]))
-    entry.append([t_fn(i) for i in range(28)] if t_fn is not None else [np.nan] * 28)
+    entry.append([t_fn(i) for i in range(40)] if t_fn is not None else [np.nan] * 40)
 solvers._CHECKPOINTS = None
 ph = np.array(cps).reshape(reps, 5)
 m = np.array(marks)
@@ -73,11 +73,15 @@ print("t_start - mark 4 (us): mean %.2f" % (1e6 * np.mean(m[:, 2] - P[:, 4])))
 L10 = 1e6 * np.diff(P[:, 10:17], axis=1)
 print("last iteration, mark 10 -> 16 deltas (us): mean", np.round(L10.mean(axis=0), 1), "median",
       np.round(np.median(L10, axis=0), 1))
-# iteration 10: wait for H[:, 10] (20 -> 21), Givens (-> 22), enqueue c_11 (-> 23), LS and
+# iteration SPIS_PHASE_ITER (10): wait for H[:, j] (20 -> 21), Givens (-> 22), enqueue c_11 (-> 23), LS and
 # branch (-> 24), wait for res_9 (-> 25), (-> 26), enqueue the dual (-> 27)
 L20 = 1e6 * np.diff(P[:, 20:28], axis=1)
-print("iteration 10, mark 20 -> 27 deltas (us): mean", np.round(L20.mean(axis=0), 1), "median",
+print("iteration %s, mark 20 -> 27 deltas (us): mean" % os.environ.get("SPIS_PHASE_ITER", "10"), np.round(L20.mean(axis=0), 1), "median",
       np.round(np.median(L20, axis=0), 1))
+# the start-up launches (marks 4 -> 30 copy_flag, -> 31 r0 SpMV, -> 32 normalize, -> 33 A_0 SpMV + chain,
+# -> 34 A_1 SpMV, 34 -> 5 the wait for beta)
+S0 = 1e6 * np.diff(P[:, [4, 30, 31, 32, 33, 34, 5]], axis=1)
+print("start-up, mark 4 -> 30 -> 31 -> 32 -> 33 -> 34 -> 5 deltas (us): mean", np.round(S0.mean(axis=0), 1))
 # the ctypes call alone: spis_solve with a null context returns at its argument check
 opts, out, ws = solvers._lib.SolveOpts(), solvers._lib.SolveOut(), C.c_void_p()
 t = time.perf_counter()
