@@ -132,9 +132,16 @@ __device__ __forceinline__ void buf_st2_wt(__amdgpu_buffer_rsrc_t r, int voff, d
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 16);  // aux 16 = sc1 (write-through)
 }
 
-// the store form of the hot path's output vectors (K2q's q_{j+1} and x_j, the SpMVs' w): 1 = sc1
+// the store form of the output vectors, a mask (SPIS_STORE_WT): 1 K2q's q_{j+1} and x_j and the
+// normalise's q, 2 the SpMVs' w, 4 the rest (the transpose's Ut, the GEMV's x, the x0 copy); a set
+// bit = sc1.  Default 1: at C3 K2q 39.9 -> 38.5 us, C3 +1.5%; bits 2 and 4 measured no better (the
+// dual SpMV's 8-B sc1 stores cost it 0.3-0.5 us), and K2s's 8-B sc1 stores cost it 1.5-1.8 us at
+// C4 (profiles/r06_store_wt_ab.txt)
 static int g_store_wt = 1;
-void set_store_wt(int on) { g_store_wt = on ? 1 : 0; }
+void set_store_wt(int mask) { g_store_wt = mask & 7; }
+static inline int wt_mgs() { return g_store_wt & 1; }
+static inline int wt_spmv() { return (g_store_wt >> 1) & 1; }
+static inline int wt_other() { return (g_store_wt >> 2) & 1; }
 
 // a descriptor over [p, p + 2^31 B) with a wave-uniform base (callers index it with valid offsets)
 template <typename T>
@@ -619,21 +626,21 @@ hipError_t launch_spmv_pipe(const CsrView& A, int mode, const double* x1, const 
   if (mode == kEpiR0 && zf != nullptr) {  // r0 with the x0 = 0 test
     if (A.col16 != nullptr)
       launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,
-               A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, zf, gen, g_store_wt);
+               A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base, zf, gen, wt_spmv());
     else
       launch_k(spmv_pipe_kernel<kPipeCap, kEpiR0>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,
-               A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, zf, gen, g_store_wt);
+               A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr, zf, gen, wt_spmv());
     return hipGetLastError();
   }
 #define SPIS_PIPE(M)                                                                                            \
   if (A.col16 != nullptr)                                                                                       \
     launch_k(spmv_pipe_kernel<kPipeCap, M, true>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta,      \
              A.n_blk, A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, A.col16, A.blk_base,                  \
-             static_cast<const unsigned*>(nullptr), 0u, g_store_wt);                                           \
+             static_cast<const unsigned*>(nullptr), 0u, wt_spmv());                                           \
   else                                                                                                          \
     launch_k(spmv_pipe_kernel<kPipeCap, M>, g, b, 0, s, ev, A.indptr, A.indices, A.vals, A.blk_meta, A.n_blk,  \
              A.walk, x1, aux1, y1, part1, x2, aux2, y2, part2, nullptr, nullptr,                                \
-             static_cast<const unsigned*>(nullptr), 0u, g_store_wt)
+             static_cast<const unsigned*>(nullptr), 0u, wt_spmv())
   switch (mode) {
     case 0: SPIS_PIPE(0); break;
     case 1: SPIS_PIPE(1); break;
@@ -1733,7 +1740,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
 #define SPIS_LAG(PER_, FX_, NT_, LAG_)                                                                          \
   launch_k(mgs_chain_lag_kernel<kLagDW, PER_, kLagNS, LAG_, FX_, NT_>, dim3(GD + 1), dim3(DT + 64), 0, s, ev, n, w, Q, \
            pitch, j, part_in, n_in, hcol, gran, epoch, err, xpart, n_x, x_out, flag, seq, gsub, ya, px, x0, xo, tw, \
-           g_store_wt)
+           wt_mgs())
 #define SPIS_LAG_PER(FX_, NT_, LAG_)          \
   switch (per) {                              \
     case 1: SPIS_LAG(1, FX_, NT_, LAG_); break; \
@@ -1780,7 +1787,7 @@ hipError_t launch_mgs_chain(int64_t n, const double* w, double* Q, int64_t pitch
 __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const double* __restrict__ y,
                                                            double* __restrict__ qn,
                                                            const double* __restrict__ part_in,
-                                                           int n_in, double* __restrict__ h_out) {
+                                                           int n_in, double* __restrict__ h_out, int wt) {
   __shared__ double s_wave[4];
   const bool vec = ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(qn)) & 15) == 0;
   const int64_t npair = vec ? (n >> 1) : 0;
@@ -1800,7 +1807,15 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
 #pragma unroll
     for (int u = 0; u < kMgsPer; ++u) {
       const int64_t p = base + u * kBlock;
-      if (p < npair) q2[p] = h == 0.0 ? make_double2(0.0, 0.0) : make_double2(yv[u].x / h, yv[u].y / h);
+      if (p < npair) {
+        const double2 qv = h == 0.0 ? make_double2(0.0, 0.0) : make_double2(yv[u].x / h, yv[u].y / h);
+        if (wt) {
+          st_wt(qn + 2 * p, qv.x);
+          st_wt(qn + 2 * p + 1, qv.y);
+        } else {
+          q2[p] = qv;
+        }
+      }
     }
     base += round;
 #pragma unroll
@@ -1809,12 +1824,12 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
   }
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;  // scalar tail / unaligned
   for (int64_t e = 2 * npair + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride)
-    qn[e] = h == 0.0 ? 0.0 : y[e] / h;
+    st_out(qn + e, h == 0.0 ? 0.0 : y[e] / h, wt);
 }
 
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev) {
-  launch_k(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qnext, part_in, n_in, h_out);
+  launch_k(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qnext, part_in, n_in, h_out, wt_mgs());
   return hipGetLastError();
 }
 
@@ -2904,7 +2919,7 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
                                                       const double* __restrict__ Z, int64_t pitch,
                                                       YArg yarg, const double* __restrict__ ycoef,
                                                       const double* __restrict__ x0,
-                                                      double* __restrict__ x) {
+                                                      double* __restrict__ x, int wt) {
 #pragma clang fp contract(off)
   __shared__ double s_y[ARG ? 1 : kMaxK];
   if (!ARG) {
@@ -2925,19 +2940,24 @@ __global__ __launch_bounds__(kBlock) void gemv_kernel(int64_t n, int p,
         a1 += z.y * c;
       }
       const double2 b = reinterpret_cast<const double2*>(x0)[q];
-      reinterpret_cast<double2*>(x)[q] = make_double2(a0 + b.x, a1 + b.y);
+      if (wt) {
+        st_wt(x + 2 * q, a0 + b.x);
+        st_wt(x + 2 * q + 1, a1 + b.y);
+      } else {
+        reinterpret_cast<double2*>(x)[q] = make_double2(a0 + b.x, a1 + b.y);
+      }
     }
     if ((n & 1) && tid == 0) {
       const int64_t e = n - 1;
       double a = 0.0;
       for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * yc[i];
-      x[e] = a + x0[e];
+      st_out(x + e, a + x0[e], wt);
     }
   } else {
     for (int64_t e = tid; e < n; e += stride) {
       double a = 0.0;
       for (int i = 0; i < p; ++i) a += Z[i * pitch + e] * yc[i];
-      x[e] = a + x0[e];
+      st_out(x + e, a + x0[e], wt);
     }
   }
 }
@@ -2956,15 +2976,15 @@ hipError_t launch_gemv(int64_t n, int p, const double* Z, int64_t pitch, const d
     for (int i = 0; i < p; ++i) ya.v[i] = y_host_or_dev[i];
   const double* yd = arg ? nullptr : y_host_or_dev;
   if (vec && arg && nt)
-    launch_k(gemv_kernel<true, true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<true, true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x, wt_other());
   else if (vec && arg)
-    launch_k(gemv_kernel<true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<true, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x, wt_other());
   else if (vec)
-    launch_k(gemv_kernel<true, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<true, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x, wt_other());
   else if (arg)
-    launch_k(gemv_kernel<false, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<false, true>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x, wt_other());
   else
-    launch_k(gemv_kernel<false, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x);
+    launch_k(gemv_kernel<false, false>, dim3(g), dim3(kBlock), 0, s, ev, n, p, Z, pitch, ya, yd, x0, x, wt_other());
   return hipGetLastError();
 }
 
@@ -3120,12 +3140,13 @@ hipError_t launch_copy(int64_t n, const double* x, double* y, hipStream_t s) {
 // write the same value).  The solver's x0 copy: with flag != gen afterwards x0 is all zeros and the
 // r0 SpMV skips the matrix (spmv_pipe_kernel MODE 3, zf)
 __global__ __launch_bounds__(kBlock) void copy_flag_kernel(int64_t n, const double* __restrict__ x,
-                                                           double* __restrict__ y, unsigned* flag, unsigned gen) {
+                                                           double* __restrict__ y, unsigned* flag, unsigned gen,
+                                                           int wt) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   bool nz = false;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < n; e += stride) {
     const double v = x[e];
-    y[e] = v;
+    st_out(y + e, v, wt);
     nz = nz || v != 0.0;
   }
   if (nz) *flag = gen;
@@ -3135,7 +3156,7 @@ hipError_t launch_copy_flag(int64_t n, const double* x, double* y, unsigned* fla
   int64_t g = (n + kBlock - 1) / kBlock;
   if (g > 4 * kRedGrid) g = 4 * kRedGrid;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(copy_flag_kernel, dim3(g), dim3(kBlock), 0, s, n, x, y, flag, gen);
+  hipLaunchKernelGGL(copy_flag_kernel, dim3(g), dim3(kBlock), 0, s, n, x, y, flag, gen, wt_other());
   return hipGetLastError();
 }
 
@@ -3469,7 +3490,7 @@ __global__ __launch_bounds__(kBlock) void transpose_basis_pipe_kernel(int64_t n,
                                                                       const double* __restrict__ v1,
                                                                       const double* __restrict__ v2,
                                                                       const double* __restrict__ v3,
-                                                                      double* __restrict__ vpart) {
+                                                                      double* __restrict__ vpart, int wt) {
   __shared__ double tile[32 * 65];
   __shared__ double s_v[4 * 64];
   const int np1 = p + 1;
@@ -3506,6 +3527,7 @@ __global__ __launch_bounds__(kBlock) void transpose_basis_pipe_kernel(int64_t n,
     __syncthreads();
     if (tb + gridDim.x < ntiles) load(tb + gridDim.x);
     double* out = Ut + r0 * 32;
+    const __amdgpu_buffer_rsrc_t orr = span_rsrc(out);  // (the tile base: wave-uniform)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // row r, positions (2 m, 2 m + 1) = columns (m, m + 16)
       const int idx = threadIdx.x + kBlock * q;
@@ -3513,7 +3535,10 @@ __global__ __launch_bounds__(kBlock) void transpose_basis_pipe_kernel(int64_t n,
       if (r < rows) {
         const double lo = m < np1 ? tile[m * 65 + r] : 0.0;
         const double hi = m + 16 < np1 ? tile[(m + 16) * 65 + r] : 0.0;
-        *reinterpret_cast<double2*>(out + r * 32 + 2 * m) = make_double2(lo, hi);
+        if (wt)
+          buf_st2_wt(orr, (r * 32 + 2 * m) * 8, make_double2(lo, hi));
+        else
+          buf_st2(orr, (r * 32 + 2 * m) * 8, 0, make_double2(lo, hi));
       }
     }
     if (threadIdx.x < nl)
@@ -3746,7 +3771,7 @@ hipError_t launch_transpose_basis_lin(int64_t n, int p, const double* Z, int64_t
   const int g = static_cast<int>(ntiles < kTransposeGrid ? (ntiles < 1 ? 1 : ntiles) : kTransposeGrid);
   if (pipe && aligned16d(Ut))
     hipLaunchKernelGGL(transpose_basis_pipe_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock), 0, s, n, p, Z, pitch,
-                       x0, Ut, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr);
+                       x0, Ut, nvv, vv[0], vv[1], vv[2], vv[3], nvv > 0 ? vpart : nullptr, wt_other());
   else
     hipLaunchKernelGGL(transpose_basis_kernel, dim3(static_cast<unsigned>(g)), dim3(kBlock),
                        static_cast<size_t>(np1) * 65 * sizeof(double) + 4 * 64 * sizeof(double), s, n, p, Z, pitch,

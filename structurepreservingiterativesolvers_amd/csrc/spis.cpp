@@ -621,7 +621,10 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     c->gram_inc = env_flag("SPIS_GRAM_INC", true);
     c->x0_zero_test = env_flag("SPIS_X0_ZERO_TEST", true);
     c->transpose_pipe = env_flag("SPIS_TRANSPOSE_PIPE", true);
-    set_store_wt(env_flag("SPIS_STORE_WT", true) ? 1 : 0);  // A/B switch (process-wide, read at context creation)
+    {  // write-through output stores, a mask (kernels.hip g_store_wt; A/B switch, process-wide)
+      const char* e = std::getenv("SPIS_STORE_WT");
+      set_store_wt(e ? std::atoi(e) : 1);
+    }
     c->k2w_fold = env_flag("SPIS_K2W_FOLD", true);
     c->k2w_onepass = env_flag("SPIS_K2W_ONEPASS", true);
     if (const char* v = std::getenv("SPIS_K2W_TW")) c->k2w_tw = std::atoi(v);
