@@ -127,7 +127,7 @@ constexpr int kChainGranLag = 12 * kChainMaxWG + 16;
 constexpr int kLagDW = 8;  // K2q data waves per workgroup (+1 exchange wave): PER <= 4 pairs per thread
 constexpr int kLagDepth = 2;  // K2q: dot products this many MGS steps early (1 or 2)
 void set_chain_lag(int lag);  // tuning tools only (tools/chainbench): 1 or 2, process-wide
-void set_store_wt(int mask);   // write-through (sc1) output stores: 1 MGS, 2 SpMV, 4 the rest (default 1; process-wide)
+void set_store_wt(int mask);   // write-through (sc1) output stores: 1 K2q, 2 SpMV, 4 the rest, 8 K2w (default 1; process-wide)
 constexpr int kLagNS = 5;     // K2q basis ring: q_{i-1} .. q_{i+3} in registers
 constexpr int kChainGsub = 2 * kMaxK + 8;  // K2q gsub: G(m, m-1) at [m], G(m, m-2) at [kMaxK + m]
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,

@@ -132,14 +132,16 @@ __device__ __forceinline__ void buf_st2_wt(__amdgpu_buffer_rsrc_t r, int voff, d
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 16);  // aux 16 = sc1 (write-through)
 }
 
-// the store form of the output vectors, a mask (SPIS_STORE_WT): 1 K2q's q_{j+1} and x_j and the
-// normalise's q, 2 the SpMVs' w, 4 the rest (the transpose's Ut, the GEMV's x, the x0 copy); a set
-// bit = sc1.  Default 1: at C3 K2q 39.9 -> 38.5 us, C3 +1.5%; bits 2 and 4 measured no better (the
-// dual SpMV's 8-B sc1 stores cost it 0.3-0.5 us), and K2s's 8-B sc1 stores cost it 1.5-1.8 us at
-// C4 (profiles/r06_store_wt_ab.txt)
+// the store form of the output vectors, a mask (SPIS_STORE_WT): 1 K2q's q_{j+1} and x_j, 2 the
+// SpMVs' w, 4 the rest (the transpose's Ut, the GEMV's x, the x0 copy), 8 K2w's update pass and the
+// normalise; a set bit = sc1.  Default 1: at C3 K2q 39.9 -> 38.5 us, C3 +1.5%; bits 2 and 4 measured
+// no better (the dual SpMV's 8-B sc1 stores cost it 0.3-0.5 us); bit 8 costs K2w's step 62 -> 66 us
+// at one rank and 491 -> 526 us at C5 (a streaming pass: its write-back overlaps at the boundary
+// anyway), and K2s's 8-B sc1 stores cost it 1.5-1.8 us at C4 (profiles/r06_store_wt_ab.txt)
 static int g_store_wt = 1;
-void set_store_wt(int mask) { g_store_wt = mask & 7; }
+void set_store_wt(int mask) { g_store_wt = mask & 15; }
 static inline int wt_mgs() { return g_store_wt & 1; }
+static inline int wt_k2w() { return (g_store_wt >> 3) & 1; }
 static inline int wt_spmv() { return (g_store_wt >> 1) & 1; }
 static inline int wt_other() { return (g_store_wt >> 2) & 1; }
 
@@ -1829,7 +1831,7 @@ __global__ __launch_bounds__(kBlock) void normalize_kernel(int64_t n, const doub
 
 hipError_t launch_normalize(int64_t n, const double* y, double* qnext, const double* part_in,
                             int n_in, double* h_out, hipStream_t s, int grid, const LaunchEv* ev) {
-  launch_k(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qnext, part_in, n_in, h_out, wt_mgs());
+  launch_k(normalize_kernel, dim3(grid), dim3(kBlock), 0, s, ev, n, y, qnext, part_in, n_in, h_out, wt_k2w());
   return hipGetLastError();
 }
 
@@ -1968,7 +1970,7 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
                                                             const double* __restrict__ coef,
                                                             double* __restrict__ part, int px, YArg yx,
                                                             const double* __restrict__ x0, double* __restrict__ xo,
-                                                            int64_t n_gx, CoefArg ca, int tw) {
+                                                            int64_t n_gx, CoefArg ca, int tw, int wt) {
   // contraction off: every product rounded, then added, in all three one-reduce kernels (K2w's
   // two passes and K2s), so their arithmetic is fixed by the source, not by the compiler's
   // choice of fused multiply-adds in each kernel
@@ -2058,17 +2060,29 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     t[1] = wa.y - t[1];
     t[2] = wb.x - t[2];
     t[3] = wb.y - t[3];
-    if (wid == 0) {
-      *reinterpret_cast<double2*>(w + e) = make_double2(t[0], t[1]);
-      *reinterpret_cast<double2*>(w + e + 128) = make_double2(t[2], t[3]);
+    if (wid == 0) {  // (buffer stores from the chunk base: sc1 when wt, see st_wt)
+      const __amdgpu_buffer_rsrc_t wr = span_rsrc(w + e0);
+      if (wt) {
+        buf_st2_wt(wr, 16 * lane, make_double2(t[0], t[1]));
+        buf_st2_wt(wr, 16 * lane + 1024, make_double2(t[2], t[3]));
+      } else {
+        buf_st2(wr, 16 * lane, 0, make_double2(t[0], t[1]));
+        buf_st2(wr, 16 * lane + 1024, 0, make_double2(t[2], t[3]));
+      }
     }
     if (FX && wid == 1) {
       double xs[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         xs[k] = (((s_x[0][k][lane] + s_x[1][k][lane]) + s_x[2][k][lane]) + s_x[3][k][lane]);
-      *reinterpret_cast<double2*>(xo + e) = make_double2(xs[0] + ba.x, xs[1] + ba.y);
-      *reinterpret_cast<double2*>(xo + e + 128) = make_double2(xs[2] + bb.x, xs[3] + bb.y);
+      const __amdgpu_buffer_rsrc_t xr = span_rsrc(xo + e0);
+      if (wt) {
+        buf_st2_wt(xr, 16 * lane, make_double2(xs[0] + ba.x, xs[1] + ba.y));
+        buf_st2_wt(xr, 16 * lane + 1024, make_double2(xs[2] + bb.x, xs[3] + bb.y));
+      } else {
+        buf_st2(xr, 16 * lane, 0, make_double2(xs[0] + ba.x, xs[1] + ba.y));
+        buf_st2(xr, 16 * lane + 1024, 0, make_double2(xs[2] + bb.x, xs[3] + bb.y));
+      }
     }
     if (DOT) {
 #pragma unroll
@@ -2103,9 +2117,9 @@ __global__ __launch_bounds__(kBlock) void cgs_update_kernel(int64_t n, double* _
     if (FX) s_x[wid][0][lane] = gs;
     __syncthreads();
     const double t = we - (((s_sum[0][0][lane] + s_sum[1][0][lane]) + s_sum[2][0][lane]) + s_sum[3][0][lane]);
-    if (wid == 0 && ok) w[e] = t;
+    if (wid == 0 && ok) st_out(w + e, t, wt);
     if (FX && wid == 1 && ok)
-      xo[e] = (((s_x[0][0][lane] + s_x[1][0][lane]) + s_x[2][0][lane]) + s_x[3][0][lane]) + x0[e];
+      st_out(xo + e, (((s_x[0][0][lane] + s_x[1][0][lane]) + s_x[2][0][lane]) + s_x[3][0][lane]) + x0[e], wt);
     if (DOT) {
 #pragma unroll
       for (int m = 0; m < kCgsPerWave; ++m) acc[m] += q[m] * t;
@@ -2304,7 +2318,7 @@ static void launch_update0(int grid, hipStream_t s, int64_t n, double* w, const 
                            const double* coef, double* part, int px, const YArg& ya, const double* x0, double* xo,
                            int64_t n_gx, const CoefArg& ca, int tw) {
   hipLaunchKernelGGL((cgs_update_kernel<0, NT, FX, COEF>), dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef,
-                     part, px, ya, x0, xo, n_gx, ca, tw);
+                     part, px, ya, x0, xo, n_gx, ca, tw, wt_k2w());
 }
 
 template <bool NT, bool FX>
@@ -2332,7 +2346,7 @@ static hipError_t cgs_update_any(int64_t n, double* w, const double* Q, int64_t 
   if (cf && (dot || ca.G == nullptr)) return hipErrorInvalidValue;
   if (dot)
     hipLaunchKernelGGL(cgs_update_kernel<1>, dim3(grid), dim3(kBlock), 0, s, n, w, Q, pitch, nv, coef, part, 0, ya,
-                       x0, xo, n_gx, ca, 0);
+                       x0, xo, n_gx, ca, 0, wt_k2w());
   else if (fx && nt)
     launch_update0c<true, true>(cf, grid, s, n, w, Q, pitch, nv, coef, part, px, ya, x0, xo, n_gx, ca, tw);
   else if (fx)
