@@ -219,7 +219,13 @@ enum spis_option {
   SPIS_OPT_K2W_SMALL_N = 20,
   SPIS_OPT_K2W_FOLD = 21,
   SPIS_OPT_K2W_TW = 22,
-  SPIS_OPT_K2W_ONEPASS = 23
+  SPIS_OPT_K2W_ONEPASS = 23,
+  /* Output stores (bitwise-neutral; PROCESS-WIDE, every context): a mask of the kernels that store
+   * their output vectors write-through (sc1) rather than write-back, so a kernel boundary has
+   * fewer dirty L2 lines to write back: 1 the MGS chain K2q (default), 2 the SpMVs, 4 the
+   * constraint transpose / update GEMV / x0 copy, 8 the one-reduce MGS update pass and the
+   * normalise.  Starts from SPIS_STORE_WT when the first context is created. */
+  SPIS_OPT_STORE_WT = 24
 };
 int spis_set_option(spis_context* ctx, int32_t option, int64_t value);
 

@@ -35,6 +35,7 @@ OPT_SLAB_KEY = 16
 OPT_GRAM_INC = 17
 OPT_X0_ZERO_TEST = 18
 OPT_TRANSPOSE_PIPE = 19
+OPT_STORE_WT = 24
 OPT_K2W_SMALL_N = 20
 OPT_K2W_FOLD = 21
 OPT_K2W_TW = 22

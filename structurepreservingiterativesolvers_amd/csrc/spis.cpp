@@ -621,9 +621,14 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     c->gram_inc = env_flag("SPIS_GRAM_INC", true);
     c->x0_zero_test = env_flag("SPIS_X0_ZERO_TEST", true);
     c->transpose_pipe = env_flag("SPIS_TRANSPOSE_PIPE", true);
-    {  // write-through output stores, a mask (kernels.hip g_store_wt; A/B switch, process-wide)
-      const char* e = std::getenv("SPIS_STORE_WT");
-      set_store_wt(e ? std::atoi(e) : 1);
+    {  // write-through output stores, a mask (kernels.hip g_store_wt; process-wide): from
+       // SPIS_STORE_WT once, at the process's first context (spis_set_option changes it later)
+      static const bool once = [] {
+        const char* e = std::getenv("SPIS_STORE_WT");
+        set_store_wt(e ? std::atoi(e) : 1);
+        return true;
+      }();
+      (void)once;
     }
     c->k2w_fold = env_flag("SPIS_K2W_FOLD", true);
     c->k2w_onepass = env_flag("SPIS_K2W_ONEPASS", true);
@@ -792,6 +797,11 @@ extern "C" int spis_set_option(spis_context* c, int32_t option, int64_t value) {
       case SPIS_OPT_K2W_ONEPASS:
         if (value != 0 && value != 1) return fail(SPIS_ERR_ARG, "option %d takes 0 or 1", option);
         (option == SPIS_OPT_K2W_FOLD ? c->k2w_fold : c->k2w_onepass) = value == 1;
+        return SPIS_OK;
+      case SPIS_OPT_STORE_WT:
+        if (value < 0 || value > 15) return fail(SPIS_ERR_ARG, "store_wt %lld: a mask 0 .. 15", (long long)value);
+        HIP_TRY(hipDeviceSynchronize());  // process-wide: no kernel of any context in flight under the old form
+        set_store_wt(static_cast<int>(value));
         return SPIS_OK;
       default: return fail(SPIS_ERR_ARG, "unknown option %d", option);
     }

@@ -78,6 +78,7 @@ _OPTIONS = {
     "k2w_fold": (_lib.OPT_K2W_FOLD, None),
     "k2w_tw": (_lib.OPT_K2W_TW, int),
     "k2w_onepass": (_lib.OPT_K2W_ONEPASS, None),
+    "store_wt": (_lib.OPT_STORE_WT, int),
 }
 
 
@@ -119,6 +120,8 @@ def set_option(name, value, ctx=None):
     * ``gram_inc``, ``x0_zero_test``, ``transpose_pipe`` (True), ``k2w_small_n`` (-1), ``k2w_fold``
       (True), ``k2w_tw`` (-1), ``k2w_onepass`` (True): A/B switches of parity tests, each
       bitwise-neutral or within roundoff (include/spis.h SPIS_OPT_GRAM_INC ..);
+    * ``store_wt`` (1): which kernels store their output vectors write-through, a mask
+      (include/spis.h SPIS_OPT_STORE_WT; bitwise-neutral, process-wide);
     * ``verify_uploads`` (True): solver calls that take a SciPy matrix check its full content
       against the cached HBM copy (see :func:`device_matrix`); False trusts identity and buffer
       addresses only (then call :func:`invalidate` after an in-place change)."""

@@ -1652,3 +1652,30 @@ def test_first_chain_of_a_process_matches_later_ones(spis):
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip().splitlines()[-1] == "SAME", out.stdout
+
+
+@pytest.mark.parametrize("mask", [0, 15])
+def test_write_through_stores_bit_identical(spis, mask, request):
+    """SPIS_OPT_STORE_WT only changes how output vectors are stored (sc1 write-through against
+    write-back), never their values: a constrained swe solve (K2q with the fused GEMV, the dual
+    SpMV, the transpose / GEMV, and the one-reduce MGS when forced) is bitwise the default's with
+    no write-through stores (0) and with every class of them (15)."""
+    from structurepreservingiterativesolvers_amd import device
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as sw_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=60)
+    x0 = np.zeros_like(dic["b"])
+    request.addfinalizer(lambda: device.set_option("store_wt", 1))
+    request.addfinalizer(lambda: device.set_option("mgs_chain", "pipelined"))
+    request.addfinalizer(lambda: device.set_option("k2w_small_n", -1))
+    device.set_option("k2w_small_n", 0)  # K2q at this N (K2s would take it by default)
+    for chain in ("pipelined", "one_reduce"):
+        device.set_option("mgs_chain", chain)
+        device.set_option("store_wt", 1)
+        xa, da = sw_ls.cgmresWrapper(dic, x0, 30, tol=1e-19)
+        device.set_option("store_wt", mask)
+        xb, db = sw_ls.cgmresWrapper(dic, x0, 30, tol=1e-19)
+        assert np.array_equal(xa, xb), chain
+        assert da["res"] == db["res"], chain
+        assert all(np.array_equal(a, b) for a, b in zip(da["x"], db["x"])), chain
