@@ -560,6 +560,7 @@ def test_fused_dual_spmv_bit_identical(spis):
             set_option("k2w_small_n", -1 if small is None else int(small))
             runs = []
             for fuse in (0, 1):
+                print("fused dual case", case, "chain", chain, "small_n", small, "fuse", fuse, flush=True)
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_FUSE_SPMV, fuse), "spis_set_option")
                 _lib.check(ctx.L.spis_set_option(ctx.handle, _lib.OPT_MGS_CHAIN, chain), "spis_set_option")
                 try:
