@@ -647,8 +647,10 @@ def invalidate(A=None):
 def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
     """HBM copy of a host vector for one call (b, a nonzero x0): its buffer comes from the
     context's pool of released ones (DeviceVector.scratch), so a call pays the copy, not a
-    hipMalloc and a hipFree; an array seen before is page-locked (:func:`_page_locked`) and its
-    copy only enqueued (it overlaps the call's set-up; the solve on the same stream follows it)."""
+    hipMalloc and a hipFree.  The copy is synchronous from the caller's own (pageable) array: the
+    caller's memory is never page-locked.  (Round 6 briefly registered an array seen twice with
+    hipHostRegister for an asynchronous copy; after such an array was freed, copies through the
+    same host pages faulted with an illegal address, intermittently, so it was removed.)"""
     if isinstance(v, DeviceVector):
         return v
     if capacity is not None:
@@ -656,54 +658,7 @@ def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
     a = np.ascontiguousarray(v, dtype=np.float64).reshape(-1)
     ctx = ctx or get_context()
     d = DeviceVector.scratch(ctx, a.size)
-    if a.size and _page_locked(a):
-        _lib.check(ctx.L.spis_memcpy_h2d_async(ctx.handle, C.c_void_p(d.ptr), C.c_void_p(a.ctypes.data), a.nbytes),
-                   "spis_memcpy_h2d_async")
-        return d
     return d.upload(a)
-
-
-# host arrays page-locked for the uploads of later calls (spis_host_register): an array is
-# registered the second time a call hands it over (a driver that passes the same b every call;
-# one that makes a new b each step never pays the ~0.3 ms registration), and unregistered by a
-# finalizer on its owning array before numpy frees the memory
-_LOCKED: dict = {}
-_SEEN: "collections.OrderedDict" = None
-_SEEN_MAX = 8
-
-
-def _unlock(key, ptr):
-    if _LOCKED.pop(key, None) is not None:
-        _lib.load_library().spis_host_unregister(C.c_void_p(ptr))
-
-
-def _page_locked(a):
-    global _SEEN
-    import collections
-
-    if _SEEN is None:
-        _SEEN = collections.OrderedDict()
-    root = _root(a)
-    if not root.flags.c_contiguous or root.nbytes > 4 * a.nbytes or type(root) is not np.ndarray:
-        return False
-    key = (id(root), root.ctypes.data, root.nbytes)
-    if key in _LOCKED:
-        return True
-    seen = _SEEN.pop(key, None)
-    if seen is None or seen() is not root:  # first sight (or a new array at a freed one's address)
-        _SEEN[key] = weakref.ref(root)
-        while len(_SEEN) > _SEEN_MAX:
-            _SEEN.popitem(last=False)
-        return False
-    if _lib.load_library().spis_host_register(C.c_void_p(root.ctypes.data), root.nbytes) != _lib.OK:
-        return False
-    try:
-        weakref.finalize(root, _unlock, key, root.ctypes.data)
-    except TypeError:  # pragma: no cover - ndarrays take weak references
-        _lib.load_library().spis_host_unregister(C.c_void_p(root.ctypes.data))
-        return False
-    _LOCKED[key] = True
-    return True
 
 
 _VECTOR_CACHE: dict = {}

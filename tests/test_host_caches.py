@@ -224,36 +224,3 @@ def test_pinned_buffers_recycled_and_capped():
     gc.collect()
     assert device.pinned_empty(n) is not None
 
-
-def test_page_lock_policy_second_sight(monkeypatch):
-    """device._page_locked: an array is page-locked the second time a call hands it over (not the
-    first: a driver that makes a new b each step never pays the registration), a new array at a
-    freed one's address counts as a first sight, and the registration is undone when the array
-    is collected.  The library calls are stubbed (no HIP runtime here)."""
-    calls = []
-
-    class Fake:
-        def spis_host_register(self, p, nbytes):
-            calls.append(("reg", p.value, nbytes))
-            return _lib.OK
-
-        def spis_host_unregister(self, p):
-            calls.append(("unreg", p.value))
-            return _lib.OK
-
-    monkeypatch.setattr(_lib, "load_library", lambda *a: Fake())
-    monkeypatch.setattr(device, "_SEEN", None)
-    monkeypatch.setattr(device, "_LOCKED", {})
-    b = np.random.default_rng(0).random(1000)
-    assert device._page_locked(b) is False and not calls
-    assert device._page_locked(np.transpose(b)) is True  # the same owner, second sight
-    assert calls == [("reg", b.ctypes.data, b.nbytes)]
-    assert device._page_locked(b) is True and len(calls) == 1  # stays locked
-    big = np.zeros((10, 1000))
-    assert device._page_locked(big[0]) is False and device._page_locked(big[0]) is False  # owner 10x the row
-    addr = b.ctypes.data
-    del b
-    gc.collect()
-    assert calls[-1] == ("unreg", addr)
-    c = np.random.default_rng(1).random(1000)
-    assert device._page_locked(c) is False  # first sight of a new array, whatever its address
