@@ -108,6 +108,10 @@ int spis_host_isa_ok(void);
  * (an x0 of +0.0 entries needs no upload).  Stops at the first nonzero entry; up to `threads`
  * threads. */
 int spis_host_nonzero(const double* data, int64_t count, int32_t bitwise, int32_t threads, int32_t* any_out);
+/* dst[0 .. bytes) = src[0 .. bytes) on up to `threads` host threads (1 MiB pieces): the drop-in
+ * stages a caller's right-hand side into its own page-locked buffer with it, then uploads that
+ * buffer asynchronously (device.py: callers' memory is never page-locked). */
+int spis_host_copy(void* dst, const void* src, int64_t bytes, int32_t threads);
 
 /* ---- live kernel timing ------------------------------------------------------
  * spis_profile_enable(ctx, period): period > 0 makes spis_solve record HIP
@@ -315,9 +319,11 @@ int spis_memcpy_d2h(spis_context* ctx, void* dst_host, const void* src_dev, int6
  * one DMA at the link's rate instead of a staged pageable copy. */
 int spis_host_alloc(int64_t bytes, void** host_out);
 int spis_host_free(void* host);
-/* Page-lock an existing host range (hipHostRegister) and undo it: the drop-in registers a
- * right-hand side it sees a second time (device.py), so its upload is an asynchronous DMA that
- * overlaps the call's set-up; the caller unregisters before the memory is freed. */
+/* Page-lock an existing host range (hipHostRegister) and undo it.  The caller owns the lifetime:
+ * unregister before the memory is freed, and never register ranges that share a page with another
+ * registration.  (The drop-in does not use it: registering callers' arrays led to intermittent
+ * illegal-address faults in later copies through the same pages; it stages through
+ * spis_host_alloc buffers with spis_host_copy instead.) */
 int spis_host_register(void* host, int64_t bytes);
 int spis_host_unregister(void* host);
 /* Host -> device copy enqueued on the context stream without waiting (the source must be

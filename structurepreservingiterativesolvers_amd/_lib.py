@@ -135,6 +135,7 @@ SIGNATURES = [
     ("spis_context_stream", C.c_int, [_VP, C.POINTER(_VP)]),
     ("spis_host_hash", C.c_int, [_VP, _I64, _I32, C.POINTER(C.c_uint64)]),
     ("spis_host_nonzero", C.c_int, [_VP, _I64, _I32, _I32, _PI32]),
+    ("spis_host_copy", C.c_int, [_VP, _VP, _I64, _I32]),
     ("spis_host_isa_ok", C.c_int, []),
     ("spis_profile_enable", C.c_int, [_VP, _I32]),
     ("spis_profile_read", C.c_int, [_VP, _PD, _PI64]),

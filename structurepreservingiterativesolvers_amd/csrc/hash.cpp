@@ -190,6 +190,23 @@ extern "C" int spis_host_hash(const void* data, int64_t bytes, int32_t threads, 
   return SPIS_OK;
 }
 
+extern "C" int spis_host_copy(void* dst, const void* src, int64_t bytes, int32_t threads) {
+  if (bytes < 0 || (bytes > 0 && (!dst || !src))) return SPIS_ERR_ARG;
+  unsigned char* d = static_cast<unsigned char*>(dst);
+  const unsigned char* s = static_cast<const unsigned char*>(src);
+  const int64_t np = (bytes + kPiece - 1) / kPiece;
+  try {
+    // the scan pool (1): the caller's thread is the one that runs the zero scans, one at a time
+    for_pieces(1, threads, np, [&](int64_t k) {
+      const int64_t o = k * kPiece;
+      std::memcpy(d + o, s + o, static_cast<size_t>(std::min(kPiece, bytes - o)));
+    });
+  } catch (...) {
+    return SPIS_ERR_STATE;
+  }
+  return SPIS_OK;
+}
+
 extern "C" int spis_host_nonzero(const double* data, int64_t count, int32_t bitwise, int32_t threads,
                                  int32_t* any_out) {
   if (!any_out || count < 0 || (count > 0 && !data)) return SPIS_ERR_ARG;

@@ -43,6 +43,7 @@ class Context:
         self.nranks = 1
         self.rank = 0
         self.device_ilu = "auto"  # SuperLU preconditioners on the device (K8) where the plan predicts a win
+        self.solves = 0  # spis_solve calls returned (device_vector's staging slots: see _stage)
 
     def synchronize(self):
         _lib.check(self.L.spis_context_synchronize(self.handle), "spis_context_synchronize")
@@ -56,6 +57,10 @@ class Context:
                     for p in ptrs:
                         self.L.spis_free(self.handle, C.c_void_p(p))
                     ptrs.clear()
+            self.L.spis_context_synchronize(self.handle)
+            for key in [k for k in _STAGING if k[0] == self.token]:
+                for q, _s in _STAGING.pop(key)["slots"]:
+                    self.L.spis_host_free(C.c_void_p(q))
             self.L.spis_context_destroy(self.handle)
             self.handle = None
 
@@ -647,10 +652,12 @@ def invalidate(A=None):
 def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
     """HBM copy of a host vector for one call (b, a nonzero x0): its buffer comes from the
     context's pool of released ones (DeviceVector.scratch), so a call pays the copy, not a
-    hipMalloc and a hipFree.  The copy is synchronous from the caller's own (pageable) array: the
-    caller's memory is never page-locked.  (Round 6 briefly registered an array seen twice with
-    hipHostRegister for an asynchronous copy; after such an array was freed, copies through the
-    same host pages faulted with an illegal address, intermittently, so it was removed.)"""
+    hipMalloc and a hipFree.  From 1 MiB on the array is copied by the host threads into one of
+    the context's own page-locked staging buffers (:func:`_stage`) and uploaded from there
+    asynchronously (the copy overlaps the call's set-up; the solve on the same stream follows
+    it); smaller ones are copied synchronously.  The caller's memory is never page-locked: round
+    6 first registered an array seen twice with hipHostRegister, and after such an array was
+    freed, copies through the same host pages faulted with an illegal address (intermittently)."""
     if isinstance(v, DeviceVector):
         return v
     if capacity is not None:
@@ -658,7 +665,47 @@ def device_vector(v, ctx=None, capacity=None) -> DeviceVector:
     a = np.ascontiguousarray(v, dtype=np.float64).reshape(-1)
     ctx = ctx or get_context()
     d = DeviceVector.scratch(ctx, a.size)
+    if a.nbytes >= _STAGE_MIN_BYTES and _stage(ctx, d, a):
+        return d
     return d.upload(a)
+
+
+# page-locked staging buffers of the asynchronous uploads (device_vector): two per (context,
+# size), used in turn (b and x0 of one call take one each).  A slot is rewritten only after a
+# solve on its context has returned since its last upload (the solve's stream follows the
+# upload), or after a context synchronize
+_STAGE_MIN_BYTES = 1 << 20
+_STAGING: dict = {}
+_STAGE_MAX = 4  # sizes kept
+
+
+def _stage(ctx, d, a):
+    key = (ctx.token, a.nbytes)
+    ent = _STAGING.get(key)
+    if ent is None:
+        if sum(1 for k in _STAGING if k[0] == ctx.token) >= _STAGE_MAX:
+            return False
+        L = _lib.load_library()
+        slots = []
+        for _ in range(2):
+            p = C.c_void_p()
+            if L.spis_host_alloc(a.nbytes, C.byref(p)) != _lib.OK or not p.value:
+                for q, _s in slots:
+                    L.spis_host_free(C.c_void_p(q))
+                return False
+            slots.append([p.value, -1])
+        ent = _STAGING[key] = {"slots": slots, "next": 0}
+    slot = ent["slots"][ent["next"]]
+    ent["next"] ^= 1
+    if slot[1] >= ctx.solves:  # its last upload may not have run yet
+        ctx.synchronize()
+    L = ctx.L
+    _lib.check(L.spis_host_copy(C.c_void_p(slot[0]), C.c_void_p(a.ctypes.data), a.nbytes, _HASH_THREADS),
+               "spis_host_copy")
+    _lib.check(L.spis_memcpy_h2d_async(ctx.handle, C.c_void_p(d.ptr), C.c_void_p(slot[0]), a.nbytes),
+               "spis_memcpy_h2d_async")
+    slot[1] = ctx.solves
+    return True
 
 
 _VECTOR_CACHE: dict = {}

@@ -526,6 +526,8 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     tp = _stamp()
     status = ctx.L.spis_solve(ctx.handle, Ad.handle, C.c_void_p(bd.ptr), C.c_void_p(x0d.ptr), C.byref(opts),
                               C.byref(out), C.byref(ws))
+    if status == _lib.OK:
+        ctx.solves += 1  # the uploads enqueued before this call have run (device._stage)
     _cp()
     tp = _tick("solve", tp)
     fresh = all([chk.ok() for chk in checks])

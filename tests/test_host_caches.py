@@ -224,3 +224,60 @@ def test_pinned_buffers_recycled_and_capped():
     gc.collect()
     assert device.pinned_empty(n) is not None
 
+
+
+def test_staged_upload_slots(monkeypatch):
+    """device._stage: a call's b (and nonzero x0) go through two page-locked staging buffers per
+    size, used in turn; a slot is rewritten without a context synchronize only when a solve has
+    returned since its last upload (that solve's stream ran the upload first).  The library is
+    stubbed (no HIP runtime here)."""
+    calls = []
+
+    class FakeLib:
+        def __init__(self):
+            self.next_ptr = 1 << 20
+
+        def spis_host_alloc(self, nbytes, out):
+            out._obj.value = self.next_ptr
+            self.next_ptr += 1 << 24
+            calls.append(("alloc", nbytes))
+            return _lib.OK
+
+        def spis_host_free(self, p):
+            calls.append(("free", p.value))
+            return _lib.OK
+
+        def spis_host_copy(self, dst, src, nbytes, threads):
+            calls.append(("copy", dst.value))
+            return _lib.OK
+
+        def spis_memcpy_h2d_async(self, h, dst, src, nbytes):
+            calls.append(("h2d", src.value))
+            return _lib.OK
+
+    class FakeCtx:
+        def __init__(self):
+            self.L = FakeLib()
+            self.token = -12345
+            self.handle = None
+            self.solves = 0
+
+        def synchronize(self):
+            calls.append(("sync",))
+
+    class Dev:
+        ptr = 777
+
+    fake = FakeCtx()
+    monkeypatch.setattr(_lib, "load_library", lambda *a: fake.L)
+    monkeypatch.setattr(device, "_STAGING", {})
+    a = np.ones(1 << 18)  # 2 MiB
+    assert device._stage(fake, Dev(), a) and device._stage(fake, Dev(), a)  # b, x0 of one call
+    s0, s1 = [c[1] for c in calls if c[0] == "copy"]
+    assert s0 != s1 and ("sync",) not in calls and [c[0] for c in calls].count("alloc") == 2
+    calls.clear()
+    assert device._stage(fake, Dev(), a)  # no solve since slot 0's upload: wait for it
+    assert calls[0] == ("sync",) and calls[1] == ("copy", s0)
+    calls.clear()
+    fake.solves += 1  # a solve returned
+    assert device._stage(fake, Dev(), a) and calls == [("copy", s1), ("h2d", s1)]
