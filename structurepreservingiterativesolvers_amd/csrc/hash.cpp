@@ -35,6 +35,13 @@
 namespace {
 
 constexpr int64_t kPiece = int64_t(1) << 20;
+// the copies and zero scans of the calling thread (b, x0: one vector of a few MiB) split finer,
+// so a 1.5 MiB vector still spreads over the pool (two 1 MiB pieces ran on one thread; six
+// 256 KiB pieces wake six workers, where 64 KiB ones woke all sixteen for no gain)
+#ifndef SPIS_FINE_SHIFT
+#define SPIS_FINE_SHIFT 18  // 256 KiB (tools/r06_hostcopy.sh: 2^16, 2^18, 2^20 A/B on the box)
+#endif
+constexpr int64_t kFine = int64_t(1) << SPIS_FINE_SHIFT;
 
 inline uint64_t mix(uint64_t h) {  // murmur3's finaliser
   h ^= h >> 33;
@@ -194,12 +201,12 @@ extern "C" int spis_host_copy(void* dst, const void* src, int64_t bytes, int32_t
   if (bytes < 0 || (bytes > 0 && (!dst || !src))) return SPIS_ERR_ARG;
   unsigned char* d = static_cast<unsigned char*>(dst);
   const unsigned char* s = static_cast<const unsigned char*>(src);
-  const int64_t np = (bytes + kPiece - 1) / kPiece;
+  const int64_t np = (bytes + kFine - 1) / kFine;
   try {
     // the scan pool (1): the caller's thread is the one that runs the zero scans, one at a time
     for_pieces(1, threads, np, [&](int64_t k) {
-      const int64_t o = k * kPiece;
-      std::memcpy(d + o, s + o, static_cast<size_t>(std::min(kPiece, bytes - o)));
+      const int64_t o = k * kFine;
+      std::memcpy(d + o, s + o, static_cast<size_t>(std::min(kFine, bytes - o)));
     });
   } catch (...) {
     return SPIS_ERR_STATE;
@@ -220,7 +227,7 @@ extern "C" int spis_host_nonzero(const double* data, int64_t count, int32_t bitw
     *any_out = 0;
     return SPIS_OK;
   }
-  constexpr int64_t kEl = kPiece / 8;
+  constexpr int64_t kEl = kFine / 8;
   const int64_t rest = count - kHead, np = (rest + kEl - 1) / kEl;
   std::atomic<int> found{0};
   try {
