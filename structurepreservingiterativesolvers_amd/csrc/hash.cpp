@@ -30,6 +30,8 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "spis.h"
 
 namespace {
@@ -171,6 +173,28 @@ class Pool {
   uint64_t gen_ = 0;
 };
 
+// dst <- src with streaming (non-temporal) 16-byte stores where both are 16-byte aligned: the
+// staging buffer is read next by the DMA engine, not by this CPU, so its lines are written without
+// being read first (16 B moved per byte copied instead of 24); sfence before the piece counts as
+// done, since streaming stores are not ordered by the pool's mutex hand-off
+void copy_stream(unsigned char* d, const unsigned char* s, int64_t n) {
+  int64_t i = 0;
+  if (((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 15) == 0) {
+    for (; i + 64 <= n; i += 64) {
+      const __m128i a = _mm_load_si128(reinterpret_cast<const __m128i*>(s + i));
+      const __m128i b = _mm_load_si128(reinterpret_cast<const __m128i*>(s + i + 16));
+      const __m128i c = _mm_load_si128(reinterpret_cast<const __m128i*>(s + i + 32));
+      const __m128i e = _mm_load_si128(reinterpret_cast<const __m128i*>(s + i + 48));
+      _mm_stream_si128(reinterpret_cast<__m128i*>(d + i), a);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16), b);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 32), c);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 48), e);
+    }
+    _mm_sfence();
+  }
+  if (i < n) std::memcpy(d + i, s + i, static_cast<size_t>(n - i));
+}
+
 void for_pieces(int pool, int threads, int64_t n_pieces, const std::function<void(int64_t)>& job) {
   if (threads > 1 && n_pieces >= 4 && Pool::get(pool).run(threads, n_pieces, job)) return;
   for (int64_t k = 0; k < n_pieces; ++k) job(k);
@@ -206,7 +230,7 @@ extern "C" int spis_host_copy(void* dst, const void* src, int64_t bytes, int32_t
     // the scan pool (1): the caller's thread is the one that runs the zero scans, one at a time
     for_pieces(1, threads, np, [&](int64_t k) {
       const int64_t o = k * kFine;
-      std::memcpy(d + o, s + o, static_cast<size_t>(std::min(kFine, bytes - o)));
+      copy_stream(d + o, s + o, std::min(kFine, bytes - o));
     });
   } catch (...) {
     return SPIS_ERR_STATE;

@@ -641,7 +641,7 @@ def is_zero_matrix(M, checks=None):
 def invalidate(A=None):
     """Forget cached uploads and zero tests (of ``A``, or all).  Not needed for correctness (every
     call re-verifies the full contents); it frees the HBM copy early."""
-    for cache in (_MATRIX_CACHE, _ZERO_CACHE, _VECTOR_CACHE):
+    for cache in (_MATRIX_CACHE, _ZERO_CACHE, _VECTOR_CACHE, _X0_ZERO_CACHE):
         if A is None:
             cache.clear()
             continue
@@ -736,6 +736,31 @@ def cached_vector(v, ctx=None, checks=None):
     root = _root(a)
     key = (id(root), root.ctypes.data, a.ctypes.data, a.size, ctx.device)
     return _cached(_VECTOR_CACHE, key, a, make, checks, vector_digest, root)
+
+
+_X0_ZERO_CACHE: dict = {}
+
+
+def host_x0_zero(a, checks=None):
+    """True when the host x0 ``a`` (fp64, 1-D, C-contiguous) is bitwise all +0.0.  The verdict is
+    cached like :func:`cached_vector` (keyed on the array's owner and buffer, evicted with it): a
+    call handed the same array again takes it from the cache and re-checks it on the verifier
+    thread beside the solve (from 4 MiB, a :class:`PendingCheck`; an x0 edited in place since
+    discards the run, which then scans inline).  A time-stepping caller's x0 = 0 (8 MB at C3) is
+    then read beside the solve, not before it."""
+
+    first = []  # a miss scans once: the verdict is both the value and the entry's "digest"
+
+    def make():
+        first.append(not host_nonzero(a, bitwise=True))
+        return first[0]
+
+    def verdict(v):
+        return first.pop() if first else not host_nonzero(v, bitwise=True)
+
+    root = _root(a)
+    key = (id(root), root.ctypes.data, a.ctypes.data, a.size)
+    return _cached(_X0_ZERO_CACHE, key, a, make, checks, verdict, root)
 
 
 _ZERO_VECTORS: dict = {}

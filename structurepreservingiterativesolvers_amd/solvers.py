@@ -43,7 +43,7 @@ import scipy.sparse as sps
 from . import _lib
 from ._wrapcache import is_known_zero
 from .device import (DeviceMatrix, DeviceVector, cached_vector, choose_ilu, device_matrix, device_vector, get_context,
-                     host_nonzero, is_superlu, is_zero_matrix, pinned_empty, zero_vector)
+                     host_nonzero, host_x0_zero, is_superlu, is_zero_matrix, pinned_empty, zero_vector)
 
 log = logging.getLogger("structurepreservingiterativesolvers_amd")
 
@@ -443,11 +443,15 @@ def _tick(name, t0):
 _MAX_STALE_RERUNS = 3
 
 
-def _host_x0(x0, n, ctx):
+def _host_x0(x0, n, ctx, checks=None):
     """The device x0 of a host x0: the context's shared zero vector when every entry is +0.0 (the
-    drivers' x0 = 0; no upload), else an upload (-0.0 entries keep their sign in x_j = Z y + x0)."""
+    drivers' x0 = 0; no upload), else an upload (-0.0 entries keep their sign in x_j = Z y + x0).
+    The verdict on an array seen before is re-checked beside the solve (device.host_x0_zero)."""
     a = np.asarray(x0)
-    if a.dtype == np.float64 and a.ndim == 1 and a.size == n and not host_nonzero(a, bitwise=True):
+    if a.dtype == np.float64 and a.ndim == 1 and a.size == n and a.flags.c_contiguous:
+        if host_x0_zero(a, checks):
+            return zero_vector(ctx, n)
+    elif a.dtype == np.float64 and a.ndim == 1 and a.size == n and not host_nonzero(a, bitwise=True):
         return zero_vector(ctx, n)
     return device_vector(a, ctx=ctx)
 
@@ -475,10 +479,10 @@ def _run_once(method, A, b, x0, k, tol, contol, conlist, pre, timing):
     device_io = isinstance(b, DeviceVector) or isinstance(x0, DeviceVector)
     # b and x0 first: the cached operators' digests (started by the lookups below) then share the
     # host's memory bandwidth with the solve, not with these copies
-    bd = device_vector(b, ctx=ctx)
-    x0d = x0 if isinstance(x0, DeviceVector) else _host_x0(x0, int(A.shape[0]), ctx)
-    tp = _tick("h2d", tp)
     checks = []
+    bd = device_vector(b, ctx=ctx)
+    x0d = x0 if isinstance(x0, DeviceVector) else _host_x0(x0, int(A.shape[0]), ctx, checks)
+    tp = _tick("h2d", tp)
     Ad = device_matrix(A, ctx=ctx, checks=checks)
     n = Ad.shape[0]
     tp = _tick("matrices", tp)

@@ -238,6 +238,29 @@ def test_in_place_edit_of_a_cached_constraint_vector_is_seen(spis, M):
     assert np.array_equal(x2, solve(om.copy())[0])
 
 
+@pytest.mark.parametrize("M", [30, 210])
+def test_in_place_edit_of_a_zero_x0_is_seen(spis, M):
+    """An all-zero x0 seen before takes its verdict from the cache and is re-checked beside the
+    solve (device.host_x0_zero; inline below 4 MiB, M = 30; on the verifier thread above, M = 210).
+    Setting one entry of that x0 in place must give the solve of a fresh copy, bitwise."""
+    from structurepreservingiterativesolvers_amd import device, solvers
+
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=M)
+    A, b = dic["A"], dic["b"]
+    x0 = np.zeros_like(b)
+    assert (x0.nbytes >= device._ASYNC_MIN_BYTES) == (M == 210)
+    x1 = solvers.gmres(A, b, x0, 10, tol=1e-19)[0]
+    assert np.array_equal(solvers.gmres(A, b, x0, 10, tol=1e-19)[0], x1)  # cached verdict, re-checked
+    x0[len(x0) - 3] = 0.25  # past the scan's head: only the full re-check sees it
+    x2 = solvers.gmres(A, b, x0, 10, tol=1e-19)[0]
+    assert not np.array_equal(x2, x1)
+    assert np.array_equal(x2, solvers.gmres(A, b, x0.copy(), 10, tol=1e-19)[0])
+    x0[len(x0) - 3] = 0.0
+    assert np.array_equal(solvers.gmres(A, b, x0, 10, tol=1e-19)[0], x1)
+
+
 def test_residual_norm_and_blas1(spis):
     from structurepreservingiterativesolvers_amd import primitives as P
 

@@ -199,6 +199,49 @@ def test_host_nonzero_bitwise_counts_negative_zero():
         assert device.host_nonzero(w) is False
 
 
+def test_host_copy_exact():
+    """spis_host_copy (the staging copy of b): every length, aligned (streaming stores) and not."""
+    import ctypes as C
+
+    from structurepreservingiterativesolvers_amd import _lib
+
+    L = _lib.load_library()
+    for n in (0, 1, 7, 100, 1 << 15, (1 << 15) + 3, 1000003):
+        a = np.random.default_rng(n).random(n)
+        d = np.zeros(n)
+        assert L.spis_host_copy(C.c_void_p(d.ctypes.data), C.c_void_p(a.ctypes.data), a.nbytes, 8) == 0
+        assert np.array_equal(a, d), n
+        s = np.frombuffer(a.tobytes(), dtype=np.uint8)
+        t = np.zeros(s.size + 1, np.uint8)
+        assert L.spis_host_copy(C.c_void_p(t.ctypes.data + 1), C.c_void_p(s.ctypes.data), s.size, 8) == 0
+        assert np.array_equal(t[1:], s), n
+
+
+def test_x0_zero_verdict_cached_and_rechecked(monkeypatch):
+    """device.host_x0_zero: a first sight scans once (inline); a repeat takes the cached verdict and,
+    from 4 MiB, queues the re-check on the verifier thread; an in-place edit fails that check, which
+    evicts the entry, so the next call scans inline again."""
+    scans = []
+    real = device.host_nonzero
+    monkeypatch.setattr(device, "host_nonzero", lambda v, bitwise=False: scans.append(v.size) or real(v, bitwise))
+    n = (device._ASYNC_MIN_BYTES // 8) + 5
+    x0 = np.zeros(n)
+    assert device.host_x0_zero(x0) is True and len(scans) == 1
+    checks = []
+    assert device.host_x0_zero(x0, checks) is True and len(checks) == 1
+    assert checks[0].ok() is True and len(scans) == 2
+    x0[n - 1] = 1.0
+    checks = []
+    assert device.host_x0_zero(x0, checks) is True  # the speculative verdict ...
+    assert checks[0].ok() is False  # ... which the re-check refutes (the caller re-runs)
+    assert device.host_x0_zero(x0) is False  # evicted: scanned inline
+    small = np.zeros(100)
+    assert device.host_x0_zero(small, []) is True
+    small[99] = -0.0
+    assert device.host_x0_zero(small, []) is False  # below 4 MiB: re-checked inline, bitwise
+    device.invalidate()
+
+
 @pytest.mark.gpu
 def test_pinned_buffers_recycled_and_capped():
     """Returned iterates live in page-locked buffers (device.pinned_empty): a dropped array's buffer
