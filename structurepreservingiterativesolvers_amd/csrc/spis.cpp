@@ -108,6 +108,7 @@ struct spis_context {
   hipEvent_t ev_arn = nullptr, ev_upd[2] = {nullptr, nullptr};  // solver pipeline events
   hipEvent_t ev_gram = nullptr;  // constrained step: the Gram tile has reached pinned memory
   hipEvent_t ev_xd = nullptr, ev_xd2 = nullptr;  // x_{k-1} written (main stream) / copied to the host (stream2)
+  hipEvent_t ev_side = nullptr;  // the end of a solve: stream2's work joined (Solver's last wait)
   unsigned long long seq = 0;  // last completion sequence number handed to a publishing kernel
   double* gram_part = nullptr;
   size_t gram_part_len = 0;
@@ -644,6 +645,7 @@ extern "C" int spis_context_create(int32_t device, spis_context** out) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));  // system scope: host reads
     HIP_TRY(hipEventCreateWithFlags(&c->ev_xd, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_xd2, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
     *out = c.release();
     return SPIS_OK;
   })
@@ -715,7 +717,7 @@ extern "C" int spis_context_destroy(spis_context* c) {
     }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
     (void)hipStreamSynchronize(c->stream2);
-    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_xd, c->ev_xd2})
+    for (auto e : {c->ev_arn, c->ev_upd[0], c->ev_upd[1], c->ev_gram, c->ev_xd, c->ev_xd2, c->ev_side})
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
@@ -3394,6 +3396,12 @@ extern "C" int spis_solve(spis_context* c, spis_matrix* A, const double* b, cons
     // idle per solve)
     const bool drained = !tail_launch && !c->dist_on() && !o->pre_ilu && hipStreamQuery(c->stream2) == hipSuccess;
     if (!drained) {
+      // a side-stream reduction the run never consumed (queue_gram(j, true), then a stop or a
+      // breakdown) still reads ws->Zb / x0 and writes the context's pinned slots: join it as well
+      if (hipStreamQuery(c->stream2) != hipSuccess) {  // event spin, as below
+        HIP_TRY(hipEventRecord(c->ev_side, c->stream2));
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_side, 0));
+      }
       HIP_TRY(hipEventRecord(c->ev_gram, s));
       ST_TRY(wait_event(c->ev_gram));
     }
