@@ -734,6 +734,31 @@ def test_swe_vs_oracle_medium(spis, M, k, tol):
     assert abs(inv_e) <= 1e-12 * max(1.0, abs(dic["e0"])) * 10
 
 
+def test_short_constrained_runs_back_to_back(spis):
+    """CGMRES_P with k = 1, 2, 3 (a constrained step's reduction queued on the side
+    stream that the run then never consumes, e.g. k = 1), each solve followed at once by the next on
+    the same context: every run matches the oracle (x to 1e-8 relative, as many residuals) and a repeat
+    of the first run is bitwise its first answer (nothing of an earlier solve lands in a later one)."""
+    import oracle
+    from structurepreservingiterativesolvers_amd import solvers
+    from structurepreservingiterativesolvers_amd.swe import LinearSolver as swe_ls
+    from structurepreservingiterativesolvers_amd.swe import assembly as sa
+
+    dic, _ = sa.linforms(M=30)
+    x0 = np.zeros_like(dic["b"])
+    cons = swe_ls.constraints(dic, x0)
+    first = None
+    for k in (1, 2, 3, 1):
+        x, d = solvers.cgmres_p(dic["A"], dic["b"], x0, k, conlist=cons)
+        xr, dr = oracle.cgmres_p(dic["A"], dic["b"], x0, k, conlist=cons)
+        assert len(d["res"]) == len(dr["res"]), k
+        assert np.linalg.norm(np.asarray(x) - xr) <= 1e-8 * max(np.linalg.norm(xr), 1e-300), k
+        if first is None:
+            first = np.asarray(x).copy()
+        elif k == 1:
+            assert np.array_equal(np.asarray(x), first)
+
+
 @pytest.mark.parametrize("method", ["cgmres_tol1e-9", "cgmres_p"])
 def test_incremental_constraint_gram(spis, method, request):
     """The incremental constraint Gram (spis.cpp con_step_*: after a solve's first constrained step,
